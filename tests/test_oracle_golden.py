@@ -1,0 +1,113 @@
+"""CPU: pin the oracle (oracle/) against the reference's golden vectors.
+
+The golden vectors were produced by importing the reference
+(tests/golden/gen_golden.py); here the oracle must reproduce them without
+the reference.  Tolerance: max|oracle - ref| / max|ref| <= 2e-6 (the oracle
+is float64, the reference float32), and exact for the KAT values.
+"""
+from __future__ import annotations
+
+import glob
+import os
+
+import numpy as np
+import pytest
+
+import prng
+from conftest import GOLDEN, corr_inputs, load_golden
+from oracle import oracle as orc
+from oracle import torch_cpu
+
+CORR_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "equiv_*.npz"))) + \
+    sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "edge_*.npz"))) + ["cfg2"]
+
+
+def test_sampler_kat():
+    g = load_golden("sampler_kat.npz")
+    v = np.zeros((1, 1, 8, 12, 16), np.float32)
+    v[0, 0, 3, 7, 11] = 1.0
+    assert np.array_equal(orc.sample(v, g["imp_queries"], False).astype(np.float32), g["imp_fixed"])
+    assert np.array_equal(orc.sample(v, g["imp_queries"], True).astype(np.float32), g["imp_legacy"])
+    # reference KATs (test_corr_sampler.py:45-56): exact hit, transposed miss, 0.75 / 0.5 weights
+    fixed = g["imp_fixed"].reshape(-1)
+    assert fixed[0] == 1.0 and fixed[1] == 0.0 and fixed[2] == 0.0
+    assert abs(fixed[3] - 0.75) < 1e-6 and abs(fixed[4] - 0.5) < 1e-6
+    cube = np.zeros((1, 1, 16, 16, 16), np.float32)
+    cube[0, 0, 3, 7, 11] = 1.0
+    cl = orc.sample(cube, g["cube_queries"], True).reshape(-1)
+    assert cl[0] == 0.0 and abs(cl[1] - 1.0) < 1e-6 and np.array_equal(cl.astype(np.float32), g["cube_legacy"].reshape(-1))
+    rv = prng.normal(101, (1, 2, 9, 7, 8))
+    for leg, key in ((False, "rand_fixed"), (True, "rand_legacy")):
+        assert orc.rel_err(orc.sample(rv, g["rand_pts"], leg), g[key]) < 1e-6
+
+
+def test_peak_shift():
+    g = load_golden("peak_shift.npz")
+    G, C = int(g["G"][0]), int(g["C"][0])
+    shift = tuple(int(s) for s in g["shift"])
+    f2 = prng.normal(int(g["seed"][0]), (1, C, G, G, G))
+    f1 = np.roll(f2, tuple(-s for s in shift), axis=(2, 3, 4)).copy()
+    coords = prng.identity_coords(1, G, G, G)
+    N = G ** 3
+    rows = np.array([(h * G + w) * G + d for (h, w, d) in g["probes"]], np.int64)
+    for leg, key in ((False, "out_fixed"), (True, "out_legacy")):
+        got = orc.corr_lookup(f1, f2, coords, 1, 4, leg, rows=rows)
+        assert orc.rel_err(got, g[key]) < 2e-6
+        offs = [tuple(int(i) - 4 for i in np.unravel_index(int(np.argmax(o)), (9, 9, 9))) for o in got]
+        if not leg:
+            assert offs == [shift] * 4
+        else:
+            assert offs != [shift] * 4
+    assert N == 4096
+
+
+@pytest.mark.parametrize("case", CORR_CASES)
+def test_corr_case(case):
+    g = load_golden(case + ".npz")
+    f1, f2, coords, L, r = corr_inputs(g)
+    rows = g["rows"]
+    for leg, tag in ((False, "fixed"), (True, "legacy")):
+        got = orc.corr_lookup(f1, f2, coords, L, r, leg, rows=rows)
+        assert orc.rel_err(got, g[f"out_rows_{tag}"]) < 2e-6, (case, tag)
+    pyr = orc.corr_rows(f1, f2, L, rows[: g["pyr_rows"].shape[0]])
+    assert orc.rel_err(pyr, g["pyr_rows"]) < 2e-6
+
+
+def test_cfg2_full_checksums():
+    """Full 16^3 output from the oracle matches the reference's checksums."""
+    g = load_golden("cfg2.npz")
+    f1, f2, coords, L, r = corr_inputs(g)
+    out = orc.corr_lookup(f1, f2, coords, L, r, False)
+    cs = g["checksum_fixed"]
+    assert abs(np.abs(out).max() - cs[3]) / cs[3] < 2e-6
+    assert abs((out * out).sum() - cs[2]) / cs[2] < 2e-6
+    assert abs(np.abs(out).sum() - cs[1]) / cs[1] < 2e-6
+
+
+def test_torch_cpu_restatement_matches_golden():
+    """The CPU-baseline restatement reproduces the reference rows bit-for-bit."""
+    import torch
+    g = load_golden("equiv_L2_r4.npz")
+    f1, f2, coords, L, r = corr_inputs(g)
+    for leg, tag in ((False, "fixed"), (True, "legacy")):
+        out = torch_cpu.corr_lookup(torch.from_numpy(f1), torch.from_numpy(f2), torch.from_numpy(coords),
+                                    L, r, leg).numpy()
+        B, Ch = out.shape[:2]
+        flat = out.reshape(B, Ch, -1)
+        N = flat.shape[2]
+        got = np.stack([flat[q // N, :, q % N] for q in g["rows"]])
+        np.testing.assert_array_equal(got, g[f"out_rows_{tag}"])
+
+
+def test_size1_level_raises_where_reference_raises():
+    with pytest.raises(RuntimeError):
+        orc.level_dims(8, 8, 2, 3)
+    assert orc.level_dims(8, 8, 2, 2)[1] == (4, 4, 1)
+
+
+def test_plumbing_fixture_consistent():
+    """Config #1 capture: oracle reproduces every GRU iteration's sampled lookup rows."""
+    g = load_golden("plumbing.npz")
+    for it in (0, 5, 11):
+        got = orc.corr_lookup(g["fmap1"], g["fmap2"], g["coords"][it], 4, 4, False, rows=g["rows"])
+        assert orc.rel_err(got, g["out_rows"][it]) < 2e-6
