@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""Benchmark of the RAFT-DVC correlation hot path on MI355X.
+
+Metric (BASELINE.json): corr build+lookup voxel-queries/s, 128^3 pair, 1/4
+encoder (32^3 x 128-channel feature maps), L=4, r=4, bf16-MFMA build, fp32
+lookup.  One step = one RAFTDVC forward's worth of correlation work:
+    [N>1: all-gather of the fmap2 slabs over RCCL]
+    pack queries + pack target pyramid + build (all levels)      CorrBlock.__init__
+    12 lookups with 12 different coordinate fields               12 x CorrBlock.__call__
+value = 12 * (query voxels, all ranks) * steps / wall time (whole job).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (query voxels sharded by H slabs)
+
+Prints one JSON line (rank 0) with roofline (dominant kernel, HIP-event timed
+on its stream) and cpu_baseline (oracle/torch_cpu.py on the host, rank 0, N=1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "raft-dvc_amd"))
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BF16_PEAK_TFS = 2500.0         # dense bf16 MFMA
+F32_PEAK_TFS = 157.3           # f32 MFMA / vector
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--size", type=int, default=32, help="feature-map edge (32 = 128^3 input, 1/4 encoder)")
+    ap.add_argument("--channels", type=int, default=128)
+    ap.add_argument("--levels", type=int, default=4)
+    ap.add_argument("--radius", type=int, default=4)
+    ap.add_argument("--iters", type=int, default=12)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--impl", default="materialised", choices=["materialised", "fused"])
+    ap.add_argument("--max-flow", type=float, default=2.0)
+    ap.add_argument("--gather-output", action="store_true", help="N>1: all-gather every lookup output")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-rows", type=int, default=4096, help="query rows of the bounded CPU sample")
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    return ap.parse_args()
+
+
+def lookup_algorithmic_bytes(coords: torch.Tensor, dims, radius: int, store_bytes: int) -> float:
+    """sum_q [ sum_l |W_l(q)| * store_bytes + 4 * L * (2r+1)^3 + 12 ].
+
+    |W_l(q)| = prod_axes |[k - r, k + r + 1] intersect [0, S - 1]|, k = floor(coord / 2^l);
+    levels with a size-1 axis read nothing."""
+    L = len(dims)
+    n3 = (2 * radius + 1) ** 3
+    c = coords.reshape(coords.shape[0], 3, -1).double()
+    nq = c.shape[0] * c.shape[2]
+    win = torch.zeros((), dtype=torch.float64, device=c.device)
+    for l, (H, W, D) in enumerate(dims):
+        if min(H, W, D) == 1:
+            continue
+        tot = torch.ones_like(c[:, 0])
+        for ax, S in enumerate((H, W, D)):
+            k = torch.floor(c[:, ax] / 2 ** l)
+            lo = torch.clamp(k - radius, min=0)
+            hi = torch.clamp(k + radius + 1, max=S - 1)
+            tot = tot * torch.clamp(hi - lo + 1, min=0)
+        win = win + tot.sum()
+    return float(win.item()) * store_bytes + nq * (4.0 * L * n3 + 12.0)
+
+
+def cpu_baseline(args, f1, f2, coords_list):
+    """oracle/torch_cpu.py (the reference op sequence) on a bounded row sample, host cores."""
+    sys.path.insert(0, ROOT)
+    from oracle import torch_cpu
+    nthreads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(nthreads)
+    f1c, f2c = f1.float().cpu(), f2.float().cpu()
+    cc = [c.cpu() for c in coords_list]
+    N = f1c[0, 0].numel()
+    rows = min(args.cpu_rows, N)
+    q0, q1 = 0, rows
+    pyr = torch_cpu.build_rows(f1c, f2c, args.levels, q0, q1)           # warmup (allocations)
+    torch_cpu.lookup_rows(pyr, cc[0], args.radius, False, q0, q1)
+    t0 = time.perf_counter()
+    pyr = torch_cpu.build_rows(f1c, f2c, args.levels, q0, q1)
+    t_build = time.perf_counter() - t0
+    nl = 3
+    t0 = time.perf_counter()
+    for i in range(nl):
+        torch_cpu.lookup_rows(pyr, cc[i], args.radius, False, q0, q1)
+    t_lookup = (time.perf_counter() - t0) / nl
+    t_step = t_build + args.iters * t_lookup
+    return {
+        "value": args.iters * rows / t_step, "unit": "voxel-queries/s", "cores": nthreads, "kind": "port",
+        "sample": (f"oracle/torch_cpu.py (reference op sequence, bit-identical to corr.py), fp32, query rows "
+                   f"[0,{rows}) of {N}: build {t_build * 1e3:.0f} ms + {args.iters} x lookup "
+                   f"{t_lookup * 1e3:.0f} ms (mean of {nl}); rows are independent, rate is per row"),
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if dist:
+        import torch.distributed as tdist
+        tdist.init_process_group("nccl", device_id=dev)
+    import dvccorr
+    from dvccorr import ops
+    from dvccorr.sharded import ShardedCorrBlock, slab_bounds
+
+    S, C, L, R = args.size, args.channels, args.levels, args.radius
+    B = 1
+    g = torch.Generator(device="cpu").manual_seed(1234)
+    f1 = torch.randn(B, C, S, S, S, generator=g)
+    f2 = torch.randn(B, C, S, S, S, generator=g)
+    base = dvccorr.coords_grid_3d(B, S, S, S, torch.device("cpu"))
+    coords_list = [base + (torch.rand(B, 3, S, S, S, generator=g) * 2 - 1) * args.max_flow
+                   for _ in range(args.iters)]
+    h0, h1 = slab_bounds(S, world, rank)
+    f1_slab = f1[:, :, h0:h1].contiguous().to(dev)
+    f2_slab = f2[:, :, h0:h1].contiguous().to(dev)
+    coords_slab = [c[:, :, h0:h1].contiguous().to(dev) for c in coords_list]
+    nq_local = (h1 - h0) * S * S
+    nq_total = S * S * S
+    lay = dvccorr.layout(S, S, S, L, C)
+    dims = lay.levels()
+    store_bytes = 2 if args.precision == "bf16" else 4
+    stream = torch.cuda.current_stream(dev)
+    group = None
+
+    ev = {"lookup": [], "build": []}
+
+    def step(timed: bool):
+        blk = ShardedCorrBlock(f1_slab, f2_slab, S, L, R, precision=args.precision, impl=args.impl,
+                               group=group, gather_output=args.gather_output,
+                               build_events=ev["build"] if timed else None)
+        for i in range(args.iters):
+            if timed:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            blk(coords_slab[i])
+            if timed:
+                e1.record(stream)
+                ev["lookup"].append((e0, e1))
+
+    def barrier():
+        if dist:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step(False)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step(True)
+        barrier()
+        elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    lk_ms = [a.elapsed_time(b) for a, b in ev["lookup"]]
+    bd_ms = [a.elapsed_time(b) for a, b in ev["build"]]
+    lk_avg = sum(lk_ms) / max(len(lk_ms), 1)
+    bd_avg = sum(bd_ms) / max(len(bd_ms), 1)
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = args.iters * nq_total * args.steps / elapsed
+
+    # roofline of the dominant kernel (by time per step, rank 0's view)
+    lk_bytes = sum(lookup_algorithmic_bytes(c, dims, R, store_bytes if args.impl == "materialised" else 0)
+                   for c in coords_slab) / len(coords_slab)
+    unpadded = sum(h * w * d for (h, w, d) in dims)
+    bd_bytes = nq_local * unpadded * store_bytes + 2 * C * 4 * nq_total
+    bd_flops = 2.0 * nq_local * nq_total * C
+    traffic = None
+    if os.path.exists(args.traffic_file):
+        try:
+            tf = json.load(open(args.traffic_file))
+            key = f"{args.impl}_{args.precision}_{S}_L{L}_r{R}_n{world}"
+            traffic = tf.get(key, {}).get("lookup_hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    if args.iters * lk_avg >= bd_avg or args.impl == "fused":
+        achieved = lk_bytes / (lk_avg * 1e-3) / 1e9
+        roof = {"kernel": "k_lookup_win (dvc_corr_lookup)" if args.impl == "materialised" else
+                "k_fused_dots + k_lookup_win (dvc_corr_lookup_fused)",
+                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "algorithmic_bytes_per_launch": lk_bytes, "avg_launch_ms": round(lk_avg, 4)}
+    else:
+        achieved = bd_bytes / (bd_avg * 1e-3) / 1e9
+        roof = {"kernel": "build (pack + k_build_bf16/f32)", "bound": "hbm", "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "algorithmic_bytes_per_launch": bd_bytes, "avg_launch_ms": round(bd_avg, 4)}
+    build_info = {"avg_ms": round(bd_avg, 4), "GB/s": round(bd_bytes / (bd_avg * 1e-3) / 1e9, 1) if bd_avg else None,
+                  "TFLOP/s": round(bd_flops / (bd_avg * 1e-3) / 1e12, 1) if bd_avg else None}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, f1, f2, coords_list)
+
+    if rank == 0:
+        line = {
+            "metric": "corr build+lookup voxel-queries/s (128^3 pair, 1/4 encoder)",
+            "value": value, "unit": "voxel-queries/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None,
+            "dtype": "bf16" if args.precision == "bf16" else "f32",
+            "data": "synthetic: N(0,1) feature maps, coords = identity + U(-2,2), 12 coord fields per step",
+            "config": {"workload": f"corr build + {args.iters} lookups, {S}^3 x {C} fmaps (128^3 input, 1/4 "
+                                   f"encoder), L={L}, r={R}, {args.impl}, {args.precision} build / fp32 lookup",
+                       "global_batch": B, "query_voxels": nq_total, "levels": L, "radius": R,
+                       "parallelism": f"query-voxel H-slabs x{world}" + (", output all-gather" if
+                                                                          args.gather_output else "")},
+            "roofline": roof,
+            "build": build_info,
+            "lookup_avg_ms": round(lk_avg, 4),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

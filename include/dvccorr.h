@@ -1,0 +1,131 @@
+/*
+ * dvccorr.h -- C ABI of the MI355X (gfx950) correlation hot path for RAFT-DVC.
+ *
+ * This is the drop-in boundary: plain pointers, sizes and an opaque stream,
+ * no torch types.  Every entry point is stream-ordered on the caller's HIP
+ * stream, never allocates device memory, never synchronises, and returns a
+ * dvc_status (0 = OK); dvc_last_error() returns a thread-local message.
+ * All device buffers are allocated by the caller (PyTorch in the Python host
+ * layer, raft-dvc_amd/dvccorr).
+ *
+ * Reference interface each entry point replaces (zachtong/RAFT-DVC):
+ *   dvc_layout_init        -- pyramid geometry of CorrBlock.__init__          src/core/corr.py:125-139
+ *   dvc_pack_queries       -- fmap1.reshape(B,C,N).transpose(1,2)             src/core/corr.py:155-161
+ *   dvc_pack_targets       -- fmap2 (+ its avg_pool3d pyramid, as in the
+ *                             on-the-fly block)                               src/core/corr.py:158-161,
+ *                                                                             src/core/corr_otf.py:83-86
+ *   dvc_corr_build         -- torch.matmul(...) / sqrt(C) [+ pyramid levels]  src/core/corr.py:141-167
+ *   dvc_corr_pool          -- F.avg_pool3d(corr, 2, stride=2)                 src/core/corr.py:136-139
+ *   dvc_corr_lookup        -- CorrBlock.__call__                              src/core/corr.py:169-208
+ *   dvc_corr_lookup_fused  -- CorrBlockOnTheFly.__call__ (any convention)     src/core/corr_otf.py:96-138,
+ *                             / the CUDA OTF forward_one_level* launchers     src/core/cuda/corr_otf_cuda.cu:448-488
+ *   dvc_sample3d           -- bilinear_sampler_3d                             src/core/corr.py:17-68
+ *
+ * Layouts (row-major, element counts):
+ *   fmap           (B, C, H, W, D) float32, channels-first, contiguous   (reference layout)
+ *   coords         (B, 3, Nq) float32, channel order (h, w, d)           (corr.py:169-173)
+ *   lookup out     (B, L*(2r+1)^3, Nq) float32; channel l*n^3+a*n^2+b*n+e (corr.py:188-208)
+ *   packed queries [B][Nq][c_pad]         dtype (f32 or bf16), zero channel padding
+ *   packed targets [B][row_stride][c_pad] dtype; rows = level-concatenated target voxels
+ *   corr pyramid   [B][Nq][row_stride]    store dtype; row q holds every level of query q:
+ *                  level l voxel (y,x,z) at offset[l] + (y*W_l + x)*Dp_l + z, Dp_l = ceil8(D_l),
+ *                  padding columns are 0.
+ * Nq is the number of query voxels per batch element; Nq == H*W*D for the
+ * reference CorrBlock, Nq < H*W*D for one rank's query slab (sharded path).
+ */
+#ifndef DVCCORR_H
+#define DVCCORR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DVC_MAX_LEVELS 8
+#define DVC_ABI_VERSION 1
+
+typedef enum {
+    DVC_OK = 0,
+    DVC_ERR_INVALID = 1,      /* bad argument (shape, pointer, range) -- maps to ValueError/RuntimeError */
+    DVC_ERR_UNSUPPORTED = 2,  /* valid but not implemented on this build */
+    DVC_ERR_LAUNCH = 3,       /* hipGetLastError after a launch */
+    DVC_ERR_RUNTIME = 4       /* other HIP runtime failure */
+} dvc_status;
+
+typedef enum { DVC_F32 = 0, DVC_BF16 = 1 } dvc_dtype;
+
+/* corr_sampler_version 2 = fixed, 1 = legacy W<->D swap (raft_dvc.py:71-77, corr.py:49-52). */
+typedef enum { DVC_FIXED = 0, DVC_LEGACY = 1 } dvc_convention;
+
+typedef struct {
+    int32_t num_levels;
+    int32_t channels;                 /* C */
+    int32_t c_pad;                    /* C rounded up to 32 (packed-row length) */
+    int32_t H[DVC_MAX_LEVELS];
+    int32_t W[DVC_MAX_LEVELS];
+    int32_t D[DVC_MAX_LEVELS];
+    int32_t Dp[DVC_MAX_LEVELS];       /* D rounded up to 8 */
+    int32_t zero_level[DVC_MAX_LEVELS]; /* a size-1 axis: the reference samples all zeros (corr.py:41-44) */
+    int64_t offset[DVC_MAX_LEVELS];   /* element offset of level l inside a row */
+    int64_t level_elems[DVC_MAX_LEVELS];
+    int64_t row_elems;                /* sum of padded level sizes */
+    int64_t row_stride;               /* row_elems rounded up to 128 */
+} dvc_layout;
+
+/* Pure host function (no GPU).  Fails (DVC_ERR_INVALID) exactly where the
+ * reference constructor raises: pooling an axis of size < 2. */
+int dvc_layout_init(int H, int W, int D, int num_levels, int C, dvc_layout *out);
+
+/* Bytes of float32 workspace dvc_pack_targets needs (pooled fmap2 levels 1..L-1). */
+size_t dvc_pack_workspace_bytes(int B, int C, int H, int W, int D, int num_levels);
+
+/* fmap1 query slab (B, C, Nq) float32 -> packed queries [B][Nq][c_pad] (dtype). */
+int dvc_pack_queries(const float *fmap1, void *packed, int B, int C, int64_t Nq, int dtype, void *stream);
+
+/* fmap2 (B, C, H, W, D) float32 -> packed targets [B][row_stride][c_pad] (dtype),
+ * level l = l-fold 2x2x2 mean of fmap2 (floor), computed in float32. */
+int dvc_pack_targets(const float *fmap2, void *packed, float *workspace, int B, int C, int H, int W, int D,
+                     int num_levels, int dtype, void *stream);
+
+/* corr[b][q][col] = (sum_c q[b][q][c] * t[b][col][c]) * (1/sqrt(C)) for col in
+ * [col_begin, col_end), stored as store_dtype.  in_dtype selects the MFMA path:
+ * DVC_BF16 -> v_mfma_f32_32x32x16_bf16, DVC_F32 -> v_mfma_f32_32x32x2_f32.
+ * col range [0, row_stride) builds every level from the pooled targets (by
+ * linearity equal to pooling the correlation); [0, level_elems[0]) builds
+ * level 0 only, for dvc_corr_pool to finish (the reference's op order). */
+int dvc_corr_build(const void *packed_q, const void *packed_t, void *corr, int B, int64_t Nq, int C, int H, int W,
+                   int D, int num_levels, int in_dtype, int store_dtype, int64_t col_begin, int64_t col_end,
+                   void *stream);
+
+/* Level src_level+1 of every row from level src_level: 2x2x2 mean, floor (avg_pool3d). */
+int dvc_corr_pool(void *corr, int B, int64_t Nq, int H, int W, int D, int num_levels, int src_level,
+                  int store_dtype, void *stream);
+
+/* Radius-r trilinear lookup of every level (CorrBlock.__call__). */
+int dvc_corr_lookup(const void *corr, const float *coords, float *out, int B, int64_t Nq, int H, int W, int D,
+                    int num_levels, int radius, int convention, int store_dtype, void *stream);
+
+/* Fused on-the-fly lookup: no correlation volume.  Dots of each query's
+ * packed feature row with the packed target rows of its (2r+2)^3 integer
+ * window, scattered by the trilinear weights.  workspace: see
+ * dvc_lookup_fused_workspace_bytes. */
+size_t dvc_lookup_fused_workspace_bytes(int B, int64_t Nq, int num_levels, int radius);
+int dvc_corr_lookup_fused(const void *packed_q, const void *packed_t, const float *coords, float *out,
+                          void *workspace, int B, int64_t Nq, int C, int H, int W, int D, int num_levels,
+                          int radius, int convention, int dtype, void *stream);
+
+/* bilinear_sampler_3d: vol (B, C, Hv, Wv, Dv), pts (B, Nq, 3) in (h, w, d) -> out (B, C, Nq). */
+int dvc_sample3d(const float *vol, const float *pts, float *out, int B, int C, int Hv, int Wv, int Dv, int64_t Nq,
+                 int convention, void *stream);
+
+const char *dvc_last_error(void);
+const char *dvc_version(void);
+int dvc_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DVCCORR_H */

@@ -1,0 +1,266 @@
+// build_gemm.hip -- the all-pairs correlation build on MFMA (reference src/core/corr.py:141-167).
+//
+//   corr[b][q][col] = (sum_k Q[b][q][k] * T[b][col][k]) * (1/sqrt(C))
+//
+// Q = packed queries [Nq][Cp], T = packed level-concatenated targets [row_stride][Cp]
+// (both K-contiguous).  K = Cp is short (128 for RAFT-DVC): one K sweep per output
+// tile, so a block keeps its query tile resident in LDS and streams column tiles.
+// At C = 128 the bf16 build does ~128 FLOP per stored byte against a ~310 FLOP/B
+// ridge: it is HBM-write-bound, so the epilogue goes through LDS and leaves the
+// CU as whole 256-byte row segments (16 B per lane, full 128 B lines).
+//
+// MFMA orientation: the MFMA "row" is the target column (A = T tile), the MFMA
+// "column" is the query (B = Q tile).  A 32x32 accumulator then holds, per lane,
+// 4 consecutive target columns of one query (regs 4g..4g+3 -> rows 8g+4h+0..3),
+// so a lane writes 8 contiguous bytes (bf16) / 16 bytes (f32) into the
+// [query][column] staging image.
+//
+// Blocks: blockIdx.x = (query tile, column chunk) with the chunk as the fast index;
+// with NCHUNK = 8 the blocks that share an XCD (b, b+8, ...) stream the same
+// eighth of T, so each XCD's L2 holds 1/8 of the targets.
+#include "common.h"
+
+namespace dvc {
+
+// ----------------------------------------------------------------------------- bf16
+// tile: 128 queries x 128 columns, 256 threads (4 waves as 2 (cols) x 2 (queries)),
+// each wave 64 x 64 = 2 x 2 accumulators of v_mfma_f32_32x32x16_bf16.
+// LDS: sQ [128][Cp] bf16, sT [128][Cp] bf16 (then reused as the [128 q][128 col]
+// bf16 staging image).  Rows are 16-byte-chunk XOR swizzled: chunk' = chunk ^ (row & m).
+constexpr int kBQ = 128, kBP = 128;
+
+__device__ __forceinline__ int swz_mask(int nch) { return (nch >= 16 ? 16 : nch) - 1; }
+
+__global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict__ Q, const bf16_t *__restrict__ T,
+                                                       bf16_t *__restrict__ corr, long long Nq, int Cp,
+                                                       long long t_batch_rows, long long row_stride,
+                                                       long long col_begin, long long col_end, int nchunk,
+                                                       float scale, int store_f32) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int nch = Cp / 8;                   // 16-byte chunks per row
+    const int msk = swz_mask(nch);
+    u32x4 *sQ = reinterpret_cast<u32x4 *>(smem);
+    u32x4 *sT = sQ + kBQ * nch;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int b = blockIdx.z;
+    const long long qtile = blockIdx.x / nchunk;
+    const int chunk = blockIdx.x % nchunk;
+    const long long q0 = qtile * kBQ;
+    const bf16_t *Qb = Q + (long long)b * Nq * Cp;
+    const bf16_t *Tb = T + (long long)b * t_batch_rows * Cp;
+
+    // resident query tile (zero rows past Nq)
+    for (int id = t; id < kBQ * nch; id += 256) {
+        const int row = id / nch, c = id - row * nch;
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (q0 + row < Nq) v = *reinterpret_cast<const u32x4 *>(Qb + (q0 + row) * Cp + c * 8);
+        sQ[row * nch + (c ^ (row & msk))] = v;
+    }
+
+    const long long ncol_tiles = (col_end - col_begin + kBP - 1) / kBP;
+    const int wp = w & 1, wq = w >> 1;
+    const int h = lane >> 5, r32 = lane & 31;
+
+    for (long long ct = chunk; ct < ncol_tiles; ct += nchunk) {
+        const long long p0 = col_begin + ct * kBP;
+        __syncthreads();   // previous staging image fully stored / sQ written
+        for (int id = t; id < kBP * nch; id += 256) {
+            const int row = id / nch, c = id - row * nch;
+            sT[row * nch + (c ^ (row & msk))] = *reinterpret_cast<const u32x4 *>(Tb + (p0 + row) * Cp + c * 8);
+        }
+        __syncthreads();
+
+        f32x16 acc[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int k = 0; k < 16; ++k) acc[i][j][k] = 0.0f;
+
+        for (int ks = 0; ks < Cp / 16; ++ks) {
+            const int c = 2 * ks + h;
+            bf16x8 a[2], bq[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int row = 64 * wp + 32 * i + r32;
+                a[i] = __builtin_bit_cast(bf16x8, sT[row * nch + (c ^ (row & msk))]);
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int row = 64 * wq + 32 * j + r32;
+                bq[j] = __builtin_bit_cast(bf16x8, sQ[row * nch + (c ^ (row & msk))]);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], bq[j], acc[i][j], 0, 0, 0);
+        }
+        __syncthreads();   // sT reads done: reuse as staging
+
+        if (!store_f32) {
+            // staging [128 q][16 chunks of 8 cols] bf16, chunk' = chunk ^ (q & 15)
+            u32x2 *st = reinterpret_cast<u32x2 *>(sT);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const int q = 64 * wq + 32 * j + r32;
+                        const int pch = 8 * wp + 4 * i + g;     // column chunk (8 columns)
+                        u32x2 v;
+                        v[0] = (unsigned)f32_to_bf16(acc[i][j][4 * g + 0] * scale) |
+                               ((unsigned)f32_to_bf16(acc[i][j][4 * g + 1] * scale) << 16);
+                        v[1] = (unsigned)f32_to_bf16(acc[i][j][4 * g + 2] * scale) |
+                               ((unsigned)f32_to_bf16(acc[i][j][4 * g + 3] * scale) << 16);
+                        st[(q * 16 + (pch ^ (q & 15))) * 2 + h] = v;
+                    }
+            __syncthreads();
+            bf16_t *cb = corr + (long long)b * Nq * row_stride;
+#pragma unroll
+            for (int it = 0; it < (kBQ * 16) / 256; ++it) {
+                const int id = it * 256 + t;
+                const int q = id >> 4, c = id & 15;
+                const long long col = p0 + 8 * c;
+                if (q0 + q < Nq && col < col_end) {
+                    const u32x4 v = sT[q * 16 + (c ^ (q & 15))];
+                    *reinterpret_cast<u32x4 *>(cb + (q0 + q) * row_stride + col) = v;
+                }
+            }
+        } else {
+            // float32 store of a bf16-input build: two passes of 64 queries each,
+            // staging [64 q][32 chunks of 4 cols] f32 (32 KB), chunk' = chunk ^ (q & 31)
+            float *cbf = reinterpret_cast<float *>(corr) + (long long)b * Nq * row_stride;
+#pragma unroll
+            for (int pass = 0; pass < 2; ++pass) {
+                if (wq == pass) {
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j)
+#pragma unroll
+                            for (int g = 0; g < 4; ++g) {
+                                const int q = 32 * j + r32;                 // local in this pass
+                                const int pch = 16 * wp + 8 * i + 2 * g + h;  // 4-column chunk
+                                u32x4 v;
+                                v[0] = __float_as_uint(acc[i][j][4 * g + 0] * scale);
+                                v[1] = __float_as_uint(acc[i][j][4 * g + 1] * scale);
+                                v[2] = __float_as_uint(acc[i][j][4 * g + 2] * scale);
+                                v[3] = __float_as_uint(acc[i][j][4 * g + 3] * scale);
+                                sT[q * 32 + (pch ^ (q & 31))] = v;
+                            }
+                }
+                __syncthreads();
+#pragma unroll
+                for (int it = 0; it < (64 * 32) / 256; ++it) {
+                    const int id = it * 256 + t;
+                    const int q = id >> 5, c = id & 31;
+                    const long long col = p0 + 4 * c;
+                    const long long gq = q0 + 64 * pass + q;
+                    if (gq < Nq && col < col_end)
+                        *reinterpret_cast<u32x4 *>(cbf + gq * row_stride + col) = sT[q * 32 + (c ^ (q & 31))];
+                }
+                __syncthreads();
+            }
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------- f32
+// Exact-f32 build on v_mfma_f32_32x32x2_f32 (a k-ordered fmaf chain, no xf32 on gfx950).
+// tile: 64 queries x 128 columns; wave w owns columns 32w..32w+31 and all 64 queries
+// (2 accumulators).  K is consumed 4 at a time: each lane reads 2 consecutive k
+// (8 bytes) per operand and feeds them to two MFMA steps; lane half h takes
+// k = 4t + 2h + u at step u (both operands use the same assignment).
+// LDS rows are 8-byte-slot XOR swizzled: slot' = slot ^ (row & m).
+constexpr int kFQ = 64, kFP = 128;
+
+__global__ __launch_bounds__(256, 1) void k_build_f32(const float *__restrict__ Q, const float *__restrict__ T,
+                                                      float *__restrict__ corr, long long Nq, int Cp,
+                                                      long long t_batch_rows, long long row_stride,
+                                                      long long col_begin, long long col_end, int nchunk,
+                                                      float scale) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int nsl = Cp / 2;                       // 8-byte slots per row
+    const int msk = (nsl >= 32 ? 32 : nsl) - 1;
+    u32x2 *sQ = reinterpret_cast<u32x2 *>(smem);
+    u32x2 *sT = sQ + kFQ * nsl;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int b = blockIdx.z;
+    const long long qtile = blockIdx.x / nchunk;
+    const int chunk = blockIdx.x % nchunk;
+    const long long q0 = qtile * kFQ;
+    const float *Qb = Q + (long long)b * Nq * Cp;
+    const float *Tb = T + (long long)b * t_batch_rows * Cp;
+
+    for (int id = t; id < kFQ * nsl; id += 256) {
+        const int row = id / nsl, s = id - row * nsl;
+        u32x2 v = {0u, 0u};
+        if (q0 + row < Nq) v = *reinterpret_cast<const u32x2 *>(Qb + (q0 + row) * Cp + 2 * s);
+        sQ[row * nsl + (s ^ (row & msk))] = v;
+    }
+    const long long ncol_tiles = (col_end - col_begin + kFP - 1) / kFP;
+    const int h = lane >> 5, r32 = lane & 31;
+
+    for (long long ct = chunk; ct < ncol_tiles; ct += nchunk) {
+        const long long p0 = col_begin + ct * kFP;
+        __syncthreads();
+        for (int id = t; id < kFP * nsl; id += 256) {
+            const int row = id / nsl, s = id - row * nsl;
+            sT[row * nsl + (s ^ (row & msk))] = *reinterpret_cast<const u32x2 *>(Tb + (p0 + row) * Cp + 2 * s);
+        }
+        __syncthreads();
+        f32x16 acc[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int k = 0; k < 16; ++k) acc[j][k] = 0.0f;
+        const int arow = 32 * w + r32;
+        for (int kt = 0; kt < Cp / 4; ++kt) {
+            const int s = 2 * kt + h;
+            const u32x2 av = sT[arow * nsl + (s ^ (arow & msk))];
+            u32x2 bv[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int row = 32 * j + r32;
+                bv[j] = sQ[row * nsl + (s ^ (row & msk))];
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(av[u]), __uint_as_float(bv[j][u]),
+                                                                  acc[j], 0, 0, 0);
+        }
+        __syncthreads();
+        // staging [64 q][32 chunks of 4 cols] f32 in sT, chunk' = chunk ^ (q & 31)
+        u32x4 *st = reinterpret_cast<u32x4 *>(sT);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int q = 32 * j + r32;
+                const int pch = 8 * w + 2 * g + h;
+                u32x4 v;
+                v[0] = __float_as_uint(acc[j][4 * g + 0] * scale);
+                v[1] = __float_as_uint(acc[j][4 * g + 1] * scale);
+                v[2] = __float_as_uint(acc[j][4 * g + 2] * scale);
+                v[3] = __float_as_uint(acc[j][4 * g + 3] * scale);
+                st[q * 32 + (pch ^ (q & 31))] = v;
+            }
+        __syncthreads();
+        float *cb = corr + (long long)b * Nq * row_stride;
+#pragma unroll
+        for (int it = 0; it < (kFQ * 32) / 256; ++it) {
+            const int id = it * 256 + t;
+            const int q = id >> 5, c = id & 31;
+            const long long col = p0 + 4 * c;
+            if (q0 + q < Nq && col < col_end)
+                *reinterpret_cast<u32x4 *>(cb + (q0 + q) * row_stride + col) = st[q * 32 + (c ^ (q & 31))];
+        }
+    }
+}
+
+}  // namespace dvc

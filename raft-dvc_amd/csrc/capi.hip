@@ -1,0 +1,312 @@
+// capi.hip -- the C ABI (include/dvccorr.h): validation, geometry, launches.
+//
+// Every entry point is stream-ordered on the caller's stream, allocates
+// nothing, never synchronises and reports failures as a status code plus a
+// thread-local message (the Python layer raises on it, as the reference's
+// pybind launchers raise on TORCH_CHECK, corr_otf_cuda.cu:51-54).
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "common.h"
+
+namespace dvc {
+__global__ void k_pool_fmap(const float *, float *, long long, int, int, int, int, int, int);
+template <typename T>
+__global__ void k_pack_rows(const float *, T *, int, int, long long, long long, int, int, long long, long long);
+__global__ void k_build_bf16(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long, long long, long long,
+                             long long, int, float, int);
+__global__ void k_build_f32(const float *, const float *, float *, long long, int, long long, long long, long long,
+                            long long, int, float);
+template <typename T>
+__global__ void k_corr_pool(T *, long long, long long, long long, int, int, long long, int, int, int, int);
+template <typename T, int R, bool WINBUF> __global__ void k_lookup_win(LookupArgs);
+template <typename T> __global__ void k_lookup_generic(LookupArgs);
+__global__ void k_sample3d(const float *, const float *, float *, int, int, int, int, int, long long, int);
+int fused_lookup(const void *packed_q, const void *packed_t, const float *coords, float *out, void *workspace, int B,
+                 long long Nq, int C, const dvc_layout &lay, int radius, int convention, int dtype, hipStream_t s,
+                 char *err, size_t errlen);
+size_t fused_workspace_bytes(int B, long long Nq, int L, int radius);
+}  // namespace dvc
+
+using namespace dvc;
+
+static thread_local char g_err[512] = "";
+
+static int fail(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+static int check_launch(const char *what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(DVC_ERR_LAUNCH, "%s: %s", what, hipGetErrorString(e));
+    return DVC_OK;
+}
+
+static inline long long ceil_div(long long a, long long b) { return (a + b - 1) / b; }
+static inline long long round_up(long long a, long long b) { return ceil_div(a, b) * b; }
+
+static int fill_lookup_args(LookupArgs &A, const dvc_layout &lay, const void *corr, const float *coords, float *out,
+                            int B, long long Nq, int radius, int convention) {
+    A.corr = corr; A.coords = coords; A.out = out;
+    A.Nq = Nq; A.q0 = 0; A.nq = Nq; A.row_stride = lay.row_stride; A.nqb = ceil_div(Nq, 64);
+    A.B = B; A.Ltot = lay.num_levels; A.l0 = 0; A.nl = lay.num_levels;
+    A.legacy = convention == DVC_LEGACY; A.r = radius;
+    const int n = 2 * radius + 1;
+    A.ach = n >= 3 ? 3 : n;
+    A.nach = (int)ceil_div(n, A.ach);
+    for (int l = 0; l < DVC_MAX_LEVELS; ++l) {
+        A.H[l] = lay.H[l]; A.W[l] = lay.W[l]; A.D[l] = lay.D[l]; A.Dp[l] = lay.Dp[l];
+        A.zero[l] = lay.zero_level[l]; A.off[l] = lay.offset[l];
+    }
+    return DVC_OK;
+}
+
+template <typename T>
+static void launch_lookup(const LookupArgs &A, unsigned blocks, hipStream_t s) {
+    switch (A.r) {
+    case 1: k_lookup_win<T, 1, false><<<blocks, 256, 0, s>>>(A); break;
+    case 2: k_lookup_win<T, 2, false><<<blocks, 256, 0, s>>>(A); break;
+    case 3: k_lookup_win<T, 3, false><<<blocks, 256, 0, s>>>(A); break;
+    case 4: k_lookup_win<T, 4, false><<<blocks, 256, 0, s>>>(A); break;
+    case 5: k_lookup_win<T, 5, false><<<blocks, 256, 0, s>>>(A); break;
+    case 6: k_lookup_win<T, 6, false><<<blocks, 256, 0, s>>>(A); break;
+    default: k_lookup_generic<T><<<blocks, 256, 0, s>>>(A); break;
+    }
+}
+
+extern "C" {
+
+const char *dvc_last_error(void) { return g_err; }
+const char *dvc_version(void) { return "dvccorr 0.1.0 (gfx950)"; }
+int dvc_abi_version(void) { return DVC_ABI_VERSION; }
+
+int dvc_layout_init(int H, int W, int D, int num_levels, int C, dvc_layout *out) {
+    if (!out) return fail(DVC_ERR_INVALID, "layout: null output");
+    if (H < 1 || W < 1 || D < 1 || C < 1)
+        return fail(DVC_ERR_INVALID, "layout: bad shape H=%d W=%d D=%d C=%d", H, W, D, C);
+    if (num_levels < 1 || num_levels > DVC_MAX_LEVELS)
+        return fail(DVC_ERR_INVALID, "layout: num_levels=%d outside [1, %d]", num_levels, DVC_MAX_LEVELS);
+    memset(out, 0, sizeof(*out));
+    out->num_levels = num_levels;
+    out->channels = C;
+    out->c_pad = (int)round_up(C, 32);
+    int h = H, w = W, d = D;
+    long long off = 0;
+    for (int l = 0; l < num_levels; ++l) {
+        if (l > 0) {
+            if (h < 2 || w < 2 || d < 2)   // avg_pool3d: "Output size is too small" (corr.py:138)
+                return fail(DVC_ERR_INVALID,
+                            "pyramid level %d cannot be pooled from (%d,%d,%d): avg_pool3d output size too small", l,
+                            h, w, d);
+            h /= 2; w /= 2; d /= 2;
+        }
+        out->H[l] = h; out->W[l] = w; out->D[l] = d;
+        out->Dp[l] = (int)round_up(d, 8);
+        out->zero_level[l] = (h == 1 || w == 1 || d == 1);
+        out->offset[l] = off;
+        out->level_elems[l] = (long long)h * w * out->Dp[l];
+        off += out->level_elems[l];
+    }
+    out->row_elems = off;
+    out->row_stride = round_up(off, 128);
+    return DVC_OK;
+}
+
+size_t dvc_pack_workspace_bytes(int B, int C, int H, int W, int D, int num_levels) {
+    dvc_layout lay;
+    if (dvc_layout_init(H, W, D, num_levels, C, &lay)) return 0;
+    size_t s = 0;
+    for (int l = 1; l < num_levels; ++l) s += (size_t)B * C * lay.H[l] * lay.W[l] * lay.D[l] * sizeof(float);
+    return s;
+}
+
+int dvc_pack_queries(const float *fmap1, void *packed, int B, int C, int64_t Nq, int dtype, void *stream) {
+    if (!fmap1 || !packed) return fail(DVC_ERR_INVALID, "pack_queries: null pointer");
+    if (B < 1 || C < 1 || Nq < 1) return fail(DVC_ERR_INVALID, "pack_queries: bad shape B=%d C=%d Nq=%lld", B, C,
+                                               (long long)Nq);
+    const int Cp = (int)round_up(C, 32);
+    hipStream_t s = (hipStream_t)stream;
+    dim3 grid((unsigned)ceil_div(Nq, 64), (unsigned)ceil_div(Cp, 64), (unsigned)B);
+    if (dtype == DVC_BF16)
+        k_pack_rows<bf16_t><<<grid, 256, 0, s>>>(fmap1, (bf16_t *)packed, C, Cp, (long long)C * Nq, Nq, 0, 0, 0, Nq);
+    else if (dtype == DVC_F32)
+        k_pack_rows<float><<<grid, 256, 0, s>>>(fmap1, (float *)packed, C, Cp, (long long)C * Nq, Nq, 0, 0, 0, Nq);
+    else
+        return fail(DVC_ERR_INVALID, "pack_queries: bad dtype %d", dtype);
+    return check_launch("pack_queries");
+}
+
+int dvc_pack_targets(const float *fmap2, void *packed, float *workspace, int B, int C, int H, int W, int D,
+                     int num_levels, int dtype, void *stream) {
+    dvc_layout lay;
+    int rc = dvc_layout_init(H, W, D, num_levels, C, &lay);
+    if (rc) return rc;
+    if (!fmap2 || !packed || (num_levels > 1 && !workspace)) return fail(DVC_ERR_INVALID, "pack_targets: null pointer");
+    if (B < 1) return fail(DVC_ERR_INVALID, "pack_targets: B=%d", B);
+    if (dtype != DVC_BF16 && dtype != DVC_F32) return fail(DVC_ERR_INVALID, "pack_targets: bad dtype %d", dtype);
+    hipStream_t s = (hipStream_t)stream;
+    const int Cp = lay.c_pad;
+    const size_t esz = dtype == DVC_BF16 ? 2 : 4;
+    if (hipMemsetAsync(packed, 0, (size_t)B * lay.row_stride * Cp * esz, s) != hipSuccess)
+        return fail(DVC_ERR_RUNTIME, "pack_targets: memset failed");
+    const float *src = fmap2;
+    float *ws = workspace;
+    for (int l = 0; l < num_levels; ++l) {
+        if (l > 0) {
+            const long long nd = (long long)lay.H[l] * lay.W[l] * lay.D[l];
+            const long long total = (long long)B * C * nd;
+            const unsigned blocks = (unsigned)std::min<long long>(ceil_div(total, 256), 65535LL * 4);
+            k_pool_fmap<<<blocks, 256, 0, s>>>(src, ws, (long long)B * C, lay.H[l - 1], lay.W[l - 1], lay.D[l - 1],
+                                               lay.H[l], lay.W[l], lay.D[l]);
+            if ((rc = check_launch("pool_fmap"))) return rc;
+            src = ws;
+            ws += (size_t)B * C * nd;
+        }
+        const long long npos = (long long)lay.H[l] * lay.W[l] * lay.D[l];
+        const long long nrows = lay.level_elems[l];
+        dim3 grid((unsigned)ceil_div(nrows, 64), (unsigned)ceil_div(Cp, 64), (unsigned)B);
+        if (dtype == DVC_BF16)
+            k_pack_rows<bf16_t><<<grid, 256, 0, s>>>(src, (bf16_t *)packed, C, Cp, (long long)C * npos, nrows,
+                                                     lay.D[l], lay.Dp[l], lay.offset[l], lay.row_stride);
+        else
+            k_pack_rows<float><<<grid, 256, 0, s>>>(src, (float *)packed, C, Cp, (long long)C * npos, nrows, lay.D[l],
+                                                    lay.Dp[l], lay.offset[l], lay.row_stride);
+        if ((rc = check_launch("pack_targets"))) return rc;
+    }
+    return DVC_OK;
+}
+
+int dvc_corr_build(const void *packed_q, const void *packed_t, void *corr, int B, int64_t Nq, int C, int H, int W,
+                   int D, int num_levels, int in_dtype, int store_dtype, int64_t col_begin, int64_t col_end,
+                   void *stream) {
+    dvc_layout lay;
+    int rc = dvc_layout_init(H, W, D, num_levels, C, &lay);
+    if (rc) return rc;
+    if (!packed_q || !packed_t || !corr) return fail(DVC_ERR_INVALID, "build: null pointer");
+    if (B < 1 || Nq < 1) return fail(DVC_ERR_INVALID, "build: B=%d Nq=%lld", B, (long long)Nq);
+    if (col_begin < 0 || col_begin % 128 || col_end <= col_begin || col_end > lay.row_stride || col_end % 4)
+        return fail(DVC_ERR_INVALID, "build: bad column range [%lld, %lld) for row_stride %lld", (long long)col_begin,
+                    (long long)col_end, lay.row_stride);
+    const int Cp = lay.c_pad;
+    if (Cp > 256) return fail(DVC_ERR_UNSUPPORTED, "build: C=%d > 256 not supported", C);
+    const float scale = 1.0f / sqrtf((float)C);   // corr / sqrt(C) (corr.py:165)
+    hipStream_t s = (hipStream_t)stream;
+    const long long ncol_tiles = ceil_div(col_end - col_begin, 128);
+    const int nchunk = (int)std::min<long long>(8, ncol_tiles);
+    if (in_dtype == DVC_BF16) {
+        if (store_dtype != DVC_BF16 && store_dtype != DVC_F32) return fail(DVC_ERR_INVALID, "build: bad store dtype");
+        const size_t lds = (size_t)128 * Cp * 2 + std::max<size_t>((size_t)128 * Cp * 2, 32768);
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void *)k_build_bf16, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr = true;
+        }
+        dim3 grid((unsigned)(ceil_div(Nq, 128) * nchunk), 1, (unsigned)B);
+        k_build_bf16<<<grid, 256, lds, s>>>((const bf16_t *)packed_q, (const bf16_t *)packed_t, (bf16_t *)corr, Nq, Cp,
+                                            lay.row_stride, lay.row_stride, col_begin, col_end, nchunk, scale,
+                                            store_dtype == DVC_F32);
+    } else if (in_dtype == DVC_F32) {
+        if (store_dtype != DVC_F32)
+            return fail(DVC_ERR_UNSUPPORTED, "build: float32 inputs need a float32 store");
+        const size_t lds = (size_t)64 * Cp * 4 + std::max<size_t>((size_t)128 * Cp * 4, 32768);
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void *)k_build_f32, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr = true;
+        }
+        dim3 grid((unsigned)(ceil_div(Nq, 64) * nchunk), 1, (unsigned)B);
+        k_build_f32<<<grid, 256, lds, s>>>((const float *)packed_q, (const float *)packed_t, (float *)corr, Nq, Cp,
+                                           lay.row_stride, lay.row_stride, col_begin, col_end, nchunk, scale);
+    } else {
+        return fail(DVC_ERR_INVALID, "build: bad input dtype %d", in_dtype);
+    }
+    return check_launch("corr_build");
+}
+
+int dvc_corr_pool(void *corr, int B, int64_t Nq, int H, int W, int D, int num_levels, int src_level,
+                  int store_dtype, void *stream) {
+    dvc_layout lay;
+    int rc = dvc_layout_init(H, W, D, num_levels, 1, &lay);
+    if (rc) return rc;
+    if (!corr) return fail(DVC_ERR_INVALID, "pool: null pointer");
+    if (src_level < 0 || src_level + 1 >= num_levels)
+        return fail(DVC_ERR_INVALID, "pool: src_level %d outside [0, %d)", src_level, num_levels - 1);
+    const int l = src_level;
+    const long long nrows = (long long)B * Nq;
+    const long long total = nrows * lay.H[l + 1] * lay.W[l + 1] * (lay.Dp[l + 1] / 4);
+    const unsigned blocks = (unsigned)std::min<long long>(ceil_div(total, 256), 16384);
+    hipStream_t s = (hipStream_t)stream;
+    if (store_dtype == DVC_BF16)
+        k_corr_pool<bf16_t><<<blocks, 256, 0, s>>>((bf16_t *)corr, nrows, lay.row_stride, lay.offset[l], lay.W[l],
+                                                   lay.Dp[l], lay.offset[l + 1], lay.H[l + 1], lay.W[l + 1],
+                                                   lay.D[l + 1], lay.Dp[l + 1]);
+    else if (store_dtype == DVC_F32)
+        k_corr_pool<float><<<blocks, 256, 0, s>>>((float *)corr, nrows, lay.row_stride, lay.offset[l], lay.W[l],
+                                                  lay.Dp[l], lay.offset[l + 1], lay.H[l + 1], lay.W[l + 1],
+                                                  lay.D[l + 1], lay.Dp[l + 1]);
+    else
+        return fail(DVC_ERR_INVALID, "pool: bad dtype %d", store_dtype);
+    return check_launch("corr_pool");
+}
+
+int dvc_corr_lookup(const void *corr, const float *coords, float *out, int B, int64_t Nq, int H, int W, int D,
+                    int num_levels, int radius, int convention, int store_dtype, void *stream) {
+    dvc_layout lay;
+    int rc = dvc_layout_init(H, W, D, num_levels, 1, &lay);
+    if (rc) return rc;
+    if (!corr || !coords || !out) return fail(DVC_ERR_INVALID, "lookup: null pointer");
+    if (B < 1 || Nq < 1) return fail(DVC_ERR_INVALID, "lookup: B=%d Nq=%lld", B, (long long)Nq);
+    if (radius < 0 || radius > 16) return fail(DVC_ERR_INVALID, "lookup: radius %d outside [0, 16]", radius);
+    if (convention != DVC_FIXED && convention != DVC_LEGACY)
+        return fail(DVC_ERR_INVALID, "lookup: bad convention %d", convention);
+    LookupArgs A;
+    fill_lookup_args(A, lay, corr, coords, out, B, Nq, radius, convention);
+    const long long items = (long long)A.nl * A.nach * B * A.nqb;
+    const unsigned blocks = (unsigned)ceil_div(items, 4);
+    hipStream_t s = (hipStream_t)stream;
+    if (store_dtype == DVC_BF16) launch_lookup<bf16_t>(A, blocks, s);
+    else if (store_dtype == DVC_F32) launch_lookup<float>(A, blocks, s);
+    else return fail(DVC_ERR_INVALID, "lookup: bad dtype %d", store_dtype);
+    return check_launch("corr_lookup");
+}
+
+size_t dvc_lookup_fused_workspace_bytes(int B, int64_t Nq, int num_levels, int radius) {
+    return fused_workspace_bytes(B, Nq, num_levels, radius);
+}
+
+int dvc_corr_lookup_fused(const void *packed_q, const void *packed_t, const float *coords, float *out,
+                          void *workspace, int B, int64_t Nq, int C, int H, int W, int D, int num_levels, int radius,
+                          int convention, int dtype, void *stream) {
+    dvc_layout lay;
+    int rc = dvc_layout_init(H, W, D, num_levels, C, &lay);
+    if (rc) return rc;
+    if (!packed_q || !packed_t || !coords || !out) return fail(DVC_ERR_INVALID, "lookup_fused: null pointer");
+    if (B < 1 || Nq < 1) return fail(DVC_ERR_INVALID, "lookup_fused: B=%d Nq=%lld", B, (long long)Nq);
+    if (radius < 0 || radius > 16) return fail(DVC_ERR_INVALID, "lookup_fused: radius %d outside [0, 16]", radius);
+    if (convention != DVC_FIXED && convention != DVC_LEGACY)
+        return fail(DVC_ERR_INVALID, "lookup_fused: bad convention %d", convention);
+    if (dtype != DVC_BF16 && dtype != DVC_F32) return fail(DVC_ERR_INVALID, "lookup_fused: bad dtype %d", dtype);
+    return fused_lookup(packed_q, packed_t, coords, out, workspace, B, Nq, C, lay, radius, convention, dtype,
+                        (hipStream_t)stream, g_err, sizeof(g_err));
+}
+
+int dvc_sample3d(const float *vol, const float *pts, float *out, int B, int C, int Hv, int Wv, int Dv, int64_t Nq,
+                 int convention, void *stream) {
+    if (!vol || !pts || !out) return fail(DVC_ERR_INVALID, "sample3d: null pointer");
+    if (B < 1 || C < 1 || Hv < 1 || Wv < 1 || Dv < 1 || Nq < 1)
+        return fail(DVC_ERR_INVALID, "sample3d: bad shape");
+    if (convention != DVC_FIXED && convention != DVC_LEGACY)
+        return fail(DVC_ERR_INVALID, "sample3d: bad convention %d", convention);
+    const long long n = (long long)B * Nq;
+    k_sample3d<<<(unsigned)ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(vol, pts, out, B, C, Hv, Wv, Dv, Nq,
+                                                                          convention == DVC_LEGACY);
+    return check_launch("sample3d");
+}
+
+}  // extern "C"

@@ -1,0 +1,107 @@
+// common.h -- shared device helpers for the gfx950 correlation kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dvccorr.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short bf16_t;   // storage type of one bf16 value
+
+namespace dvc {
+
+constexpr int kWave = 64;
+
+// Geometry of the correlation pyramid, passed by value to kernels.
+struct Geo {
+    int L;
+    int H[DVC_MAX_LEVELS], W[DVC_MAX_LEVELS], D[DVC_MAX_LEVELS], Dp[DVC_MAX_LEVELS];
+    int zero[DVC_MAX_LEVELS];
+    long long off[DVC_MAX_LEVELS];
+    long long row_stride;
+};
+
+__device__ __forceinline__ float bf16_bits_to_f32(unsigned int h) { return __uint_as_float(h << 16); }
+
+__device__ __forceinline__ bf16_t f32_to_bf16(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+
+// Arguments of the lookup kernels (materialised pyramid or fused window buffer).
+// A launch covers queries [q0, q0 + nq) of every batch element and levels
+// [l0, l0 + nl); out/coords are indexed with the full Nq and Ltot.
+struct LookupArgs {
+    const void *corr;        // pyramid rows [B][Nq][row_stride], or window buffer [B][nq][NB]
+    const float *coords;     // (B, 3, Nq)
+    float *out;              // (B, Ltot*n^3, Nq)
+    long long Nq, q0, nq, nqb, row_stride;
+    int B, Ltot, l0, nl, legacy, nach, ach, r;
+    int H[DVC_MAX_LEVELS], W[DVC_MAX_LEVELS], D[DVC_MAX_LEVELS], Dp[DVC_MAX_LEVELS], zero[DVC_MAX_LEVELS];
+    long long off[DVC_MAX_LEVELS];
+};
+
+template <typename T> struct StoreT;
+template <> struct StoreT<float> {
+    static __device__ __forceinline__ float load(const float *p) { return *p; }
+    static __device__ __forceinline__ void store(float *p, float v) { *p = v; }
+};
+template <> struct StoreT<bf16_t> {
+    static __device__ __forceinline__ float load(const bf16_t *p) { return bf16_bits_to_f32(*p); }
+    static __device__ __forceinline__ void store(bf16_t *p, float v) { *p = f32_to_bf16(v); }
+};
+
+// ---------------------------------------------------------------------------
+// Sampling-coordinate arithmetic of the reference, in float32, no FMA
+// contraction, IEEE division (reference src/core/corr.py:41-44 then
+// grid_sample's align_corners unnormalise): x -> 2x/(S-1) - 1 -> ((g+1)/2)*(S'-1).
+// Bit-identical to the CPU reference (checked by the oracle, see
+// oracle/corr_oracle.c header).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float norm_coord(float x, float snm1) {
+#pragma clang fp contract(off)
+    float t = 2.0f * x;
+    float u = t / snm1;
+    return u - 1.0f;
+}
+__device__ __forceinline__ float unnorm_coord(float g, float sum1) {
+#pragma clang fp contract(off)
+    float t = g + 1.0f;
+    float u = t / 2.0f;
+    return u * sum1;
+}
+__device__ __forceinline__ float roundtrip(float x, float snm1, float sum1) {
+    return unnorm_coord(norm_coord(x, snm1), sum1);
+}
+
+// Trilinear sample at grid_sample source indices (ix: W axis, iy: H axis,
+// iz: D axis) of one level in the padded row layout; out-of-range corners
+// contribute nothing (padding_mode='zeros').  Weight products and term order
+// follow grid_sample (tnw, tne, tsw, tse, bnw, bne, bsw, bse).
+template <typename T>
+__device__ __forceinline__ float tri_sample(const T *lvl, int Hl, int Wl, int Dl, int Dpl, float ix, float iy,
+                                            float iz) {
+#pragma clang fp contract(off)
+    if (!(fabsf(ix) < 1e7f) || !(fabsf(iy) < 1e7f) || !(fabsf(iz) < 1e7f)) return 0.0f;   // NaN/inf/huge: all OOB
+    const float fx = floorf(ix), fy = floorf(iy), fz = floorf(iz);
+    const int x0 = (int)fx, y0 = (int)fy, z0 = (int)fz;
+    const float wx1 = ix - fx, wx0 = (fx + 1.0f) - ix;
+    const float wy1 = iy - fy, wy0 = (fy + 1.0f) - iy;
+    const float wz1 = iz - fz, wz0 = (fz + 1.0f) - iz;
+    float acc = 0.0f;
+#pragma unroll
+    for (int cz = 0; cz < 2; ++cz)
+#pragma unroll
+        for (int cy = 0; cy < 2; ++cy)
+#pragma unroll
+            for (int cx = 0; cx < 2; ++cx) {
+                const int x = x0 + cx, y = y0 + cy, z = z0 + cz;
+                if (x < 0 || x >= Wl || y < 0 || y >= Hl || z < 0 || z >= Dl) continue;
+                const float w = ((cx ? wx1 : wx0) * (cy ? wy1 : wy0)) * (cz ? wz1 : wz0);
+                acc += StoreT<T>::load(lvl + ((long long)y * Wl + x) * Dpl + z) * w;
+            }
+    return acc;
+}
+
+}  // namespace dvc

@@ -1,0 +1,243 @@
+// fused.hip -- on-the-fly lookup without a correlation volume
+// (reference semantics: src/core/corr_otf.py:96-237, CorrBlockOnTheFly; CUDA design
+// reference: the integer-window "scatter" forward, src/core/cuda/corr_otf_cuda.cu:548-735).
+//
+// By linearity, sampling the correlation of the pooled pyramid equals the dot of
+// the query feature with the trilinearly sampled pooled target features, and the
+// trilinear sample of the correlation at window offsets only needs the dots at
+// the (2r+2)^3 integer window positions.  Per query chunk and level:
+//   stage 1 (k_fused_dots): dots[q][i][j][k] = scale * <Q[q], T_l[origin + (i,j,k)]>
+//            into a per-query dense window buffer (0 outside the level);
+//   stage 2 (k_lookup_win<float, R, WINBUF=true>, lookup.hip): the same window
+//            walk as the materialised lookup, reading the window buffer.
+// Memory is O(C * voxels) + one bounded window-buffer chunk, never O(N^2): this
+// is the path for the 1/2-encoder 256^3 configuration (128^3 feature map).
+// Legacy-convention levels with W != D (non-unit sample spacing) and radii
+// outside [1, 6] use k_fused_generic (per output, 8 corner dots).
+#include <algorithm>
+#include <stdio.h>
+
+#include "common.h"
+#include "lookup_common.h"
+
+namespace dvc {
+
+template <typename T, int R, bool WINBUF> __global__ void k_lookup_win(LookupArgs);
+
+constexpr long long kFusedChunk = 65536;   // queries per window-buffer chunk
+
+__host__ __device__ constexpr int win_nw(int R) { return 2 * R + 2; }
+__host__ __device__ constexpr int win_nwp(int R) { return (2 * R + 2 + 3) & ~3; }
+__host__ __device__ constexpr long long win_elems(int R) { return (long long)win_nw(R) * win_nw(R) * win_nwp(R); }
+
+template <typename T> struct Dot;
+template <> struct Dot<bf16_t> {
+    // 8 channels: one 16-byte chunk of each operand, v_dot2c_f32_bf16 x4
+    static __device__ __forceinline__ float chunk(const u32x4 &a, const u32x4 &b, float acc) {
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, a[i]), __builtin_bit_cast(bf16x2, b[i]),
+                                                  acc, false);
+        return acc;
+    }
+    static constexpr int kPerChunk = 8;
+};
+template <> struct Dot<float> {
+    static __device__ __forceinline__ float chunk(const u32x4 &a, const u32x4 &b, float acc) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc = __builtin_fmaf(__uint_as_float(a[i]), __uint_as_float(b[i]), acc);
+        return acc;
+    }
+    static constexpr int kPerChunk = 4;
+};
+
+// One wavefront per query; lanes stride over the (2r+2)^3 window positions.
+template <typename T, int R>
+__global__ __launch_bounds__(256) void k_fused_dots(const T *__restrict__ Q, const T *__restrict__ Tt,
+                                                    LookupArgs A, float *__restrict__ ws, int Cp,
+                                                    long long t_rows, float scale) {
+    constexpr int NW = win_nw(R), NWP = win_nwp(R);
+    constexpr long long NB = win_elems(R);
+    __shared__ u32x4 sq[4][64];   // one query row per wave (Cp <= 256 bf16 / 128 f32... see host check)
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const long long item = (long long)blockIdx.x * 4 + w;
+    if (item >= (long long)A.B * A.nq) return;
+    const int b = (int)(item / A.nq);
+    const long long qi = item - (long long)b * A.nq;
+    const long long q = A.q0 + qi;
+    const int l = A.l0;
+    const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
+    const int nck = Cp / Dot<T>::kPerChunk;   // 16-byte chunks per row
+    const T *qrow = Q + ((long long)b * A.Nq + q) * Cp;
+    if (lane < nck) sq[w][lane] = *reinterpret_cast<const u32x4 *>(qrow + lane * Dot<T>::kPerChunk);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS writes landed
+    float cy, cx, cz;
+    load_coords(A.coords, b, A.Nq, q, cy, cx, cz);
+    const float sc = (float)(1 << l);
+    WinAxes ax;
+    window_axes(cy / sc, cx / sc, cz / sc, Hl, Wl, Dl, A.legacy, ax);
+    const int ih = (int)ax.kh - R, iu = (int)ax.ku - R, iv = (int)ax.kv - R;
+    const T *Tb = Tt + ((long long)b * t_rows + A.off[l]) * Cp;
+    float *wq = ws + ((long long)b * A.nq + qi) * NB;
+    for (int p = lane; p < NW * NW * NWP; p += 64) {
+        const int k = p % NWP, ij = p / NWP;
+        const int j = ij % NW, i = ij / NW;
+        const int y = ih + i, x = iu + j, z = iv + k;
+        float acc = 0.0f;
+        if (k < NW && (unsigned)y < (unsigned)Hl && (unsigned)x < (unsigned)Wl && (unsigned)z < (unsigned)Dl) {
+            const T *trow = Tb + (((long long)y * Wl + x) * Dpl + z) * Cp;
+            for (int c = 0; c < nck; ++c)
+                acc = Dot<T>::chunk(*reinterpret_cast<const u32x4 *>(trow + c * Dot<T>::kPerChunk), sq[w][c], acc);
+            acc *= scale;
+        }
+        wq[p] = acc;
+    }
+}
+
+// Per-output fallback: any radius, legacy levels with W != D.
+template <typename T>
+__global__ __launch_bounds__(256) void k_fused_generic(const T *__restrict__ Q, const T *__restrict__ Tt,
+                                                       LookupArgs A, int Cp, long long t_rows, float scale) {
+    const int R = A.r, n = 2 * R + 1;
+    const long long n3 = (long long)n * n * n;
+    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long long)A.B * A.nq * n3) return;
+    const long long ch = gid % n3;            // channel fastest -> coalesced query row reads
+    const long long bq = gid / n3;
+    const int b = (int)(bq / A.nq);
+    const long long q = A.q0 + (bq - (long long)b * A.nq);
+    const int l = A.l0;
+    const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
+    float *o = A.out + (((long long)b * A.Ltot + l) * n3 + ch) * A.Nq + q;
+    if (A.zero[l]) { *o = 0.0f; return; }
+    const int e = (int)(ch % n), bb = (int)((ch / n) % n), a = (int)(ch / (n * n));
+    float cy, cx, cz;
+    load_coords(A.coords, b, A.Nq, q, cy, cx, cz);
+    const float sc = (float)(1 << l);
+    const float h1 = (float)(Hl - 1), w1 = (float)(Wl - 1), d1 = (float)(Dl - 1);
+    const float gh = norm_coord(cy / sc + (float)(a - R), h1);
+    const float gw = norm_coord(cx / sc + (float)(bb - R), w1);
+    const float gd = norm_coord(cz / sc + (float)(e - R), d1);
+    const float ix = unnorm_coord(A.legacy ? gd : gw, w1);
+    const float iy = unnorm_coord(gh, h1);
+    const float iz = unnorm_coord(A.legacy ? gw : gd, d1);
+    float acc = 0.0f;
+    if (fabsf(ix) < 1e7f && fabsf(iy) < 1e7f && fabsf(iz) < 1e7f) {
+#pragma clang fp contract(off)
+        const float fx = floorf(ix), fy = floorf(iy), fz = floorf(iz);
+        const int x0 = (int)fx, y0 = (int)fy, z0 = (int)fz;
+        const float wx[2] = {(fx + 1.0f) - ix, ix - fx};
+        const float wy[2] = {(fy + 1.0f) - iy, iy - fy};
+        const float wz[2] = {(fz + 1.0f) - iz, iz - fz};
+        const T *qrow = Q + ((long long)b * A.Nq + q) * Cp;
+        const T *Tb = Tt + ((long long)b * t_rows + A.off[l]) * Cp;
+        const int nck = Cp / Dot<T>::kPerChunk;
+        for (int cz = 0; cz < 2; ++cz)
+            for (int cyy = 0; cyy < 2; ++cyy)
+                for (int cxx = 0; cxx < 2; ++cxx) {
+                    const int x = x0 + cxx, y = y0 + cyy, z = z0 + cz;
+                    if (x < 0 || x >= Wl || y < 0 || y >= Hl || z < 0 || z >= Dl) continue;
+                    const T *trow = Tb + (((long long)y * Wl + x) * Dpl + z) * Cp;
+                    float d = 0.0f;
+                    for (int c = 0; c < nck; ++c)
+                        d = Dot<T>::chunk(*reinterpret_cast<const u32x4 *>(trow + c * Dot<T>::kPerChunk),
+                                          *reinterpret_cast<const u32x4 *>(qrow + c * Dot<T>::kPerChunk), d);
+                    const float wgt = (wx[cxx] * wy[cyy]) * wz[cz];
+                    acc += (d * scale) * wgt;
+                }
+    }
+    *o = acc;
+}
+
+size_t fused_workspace_bytes(int B, long long Nq, int L, int radius) {
+    (void)L;
+    if (radius < 1 || radius > 6) return 0;
+    return (size_t)B * std::min(Nq, kFusedChunk) * win_elems(radius) * sizeof(float);
+}
+
+template <typename T, int R>
+static int fused_level_win(const T *Q, const T *Tt, LookupArgs &A, float *ws, int Cp, long long t_rows, float scale,
+                           hipStream_t s) {
+    const long long waves = (long long)A.B * A.nq;
+    if (!A.zero[A.l0])   // a size-1 level samples all zeros: stage 2 writes them without a window
+        k_fused_dots<T, R><<<(unsigned)((waves + 3) / 4), 256, 0, s>>>(Q, Tt, A, ws, Cp, t_rows, scale);
+    A.corr = ws;
+    A.row_stride = win_elems(R);
+    const long long items = (long long)A.nach * A.B * A.nqb;
+    k_lookup_win<float, R, true><<<(unsigned)((items + 3) / 4), 256, 0, s>>>(A);
+    return 0;
+}
+
+template <typename T>
+static void fused_level(int R, const T *Q, const T *Tt, LookupArgs &A, float *ws, int Cp, long long t_rows,
+                        float scale, hipStream_t s) {
+    switch (R) {
+    case 1: fused_level_win<T, 1>(Q, Tt, A, ws, Cp, t_rows, scale, s); break;
+    case 2: fused_level_win<T, 2>(Q, Tt, A, ws, Cp, t_rows, scale, s); break;
+    case 3: fused_level_win<T, 3>(Q, Tt, A, ws, Cp, t_rows, scale, s); break;
+    case 4: fused_level_win<T, 4>(Q, Tt, A, ws, Cp, t_rows, scale, s); break;
+    case 5: fused_level_win<T, 5>(Q, Tt, A, ws, Cp, t_rows, scale, s); break;
+    default: fused_level_win<T, 6>(Q, Tt, A, ws, Cp, t_rows, scale, s); break;
+    }
+}
+
+int fused_lookup(const void *packed_q, const void *packed_t, const float *coords, float *out, void *workspace, int B,
+                 long long Nq, int C, const dvc_layout &lay, int radius, int convention, int dtype, hipStream_t s,
+                 char *err, size_t errlen) {
+    const int Cp = lay.c_pad;
+    if ((dtype == DVC_BF16 && Cp > 512) || (dtype == DVC_F32 && Cp > 256)) {
+        snprintf(err, errlen, "lookup_fused: C=%d too large", C);
+        return DVC_ERR_UNSUPPORTED;
+    }
+    const bool win_ok = radius >= 1 && radius <= 6;
+    if (win_ok && !workspace) {
+        snprintf(err, errlen, "lookup_fused: workspace required (%zu bytes)", fused_workspace_bytes(B, Nq, 0, radius));
+        return DVC_ERR_INVALID;
+    }
+    const float scale = 1.0f / sqrtf((float)C);
+    const int n = 2 * radius + 1;
+    const long long n3 = (long long)n * n * n;
+    LookupArgs A;
+    A.coords = coords; A.out = out; A.Nq = Nq; A.B = B; A.Ltot = lay.num_levels; A.nl = 1;
+    A.legacy = convention == DVC_LEGACY; A.r = radius;
+    A.ach = n >= 3 ? 3 : n;
+    A.nach = (n + A.ach - 1) / A.ach;
+    for (int l = 0; l < DVC_MAX_LEVELS; ++l) {
+        A.H[l] = lay.H[l]; A.W[l] = lay.W[l]; A.D[l] = lay.D[l]; A.Dp[l] = lay.Dp[l];
+        A.zero[l] = lay.zero_level[l]; A.off[l] = lay.offset[l];
+    }
+    for (long long q0 = 0; q0 < Nq; q0 += kFusedChunk) {
+        A.q0 = q0;
+        A.nq = std::min(kFusedChunk, Nq - q0);
+        A.nqb = (A.nq + 63) / 64;
+        for (int l = 0; l < lay.num_levels; ++l) {
+            A.l0 = l;
+            const bool generic = !win_ok || (A.legacy && lay.W[l] != lay.D[l]);
+            if (generic) {
+                const long long total = (long long)B * A.nq * n3;
+                if (dtype == DVC_BF16)
+                    k_fused_generic<bf16_t><<<(unsigned)((total + 255) / 256), 256, 0, s>>>(
+                        (const bf16_t *)packed_q, (const bf16_t *)packed_t, A, Cp, lay.row_stride, scale);
+                else
+                    k_fused_generic<float><<<(unsigned)((total + 255) / 256), 256, 0, s>>>(
+                        (const float *)packed_q, (const float *)packed_t, A, Cp, lay.row_stride, scale);
+            } else if (dtype == DVC_BF16) {
+                fused_level<bf16_t>(radius, (const bf16_t *)packed_q, (const bf16_t *)packed_t, A, (float *)workspace,
+                                    Cp, lay.row_stride, scale, s);
+            } else {
+                fused_level<float>(radius, (const float *)packed_q, (const float *)packed_t, A, (float *)workspace,
+                                   Cp, lay.row_stride, scale, s);
+            }
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) {
+                snprintf(err, errlen, "lookup_fused: %s", hipGetErrorString(e));
+                return DVC_ERR_LAUNCH;
+            }
+        }
+    }
+    return DVC_OK;
+}
+
+}  // namespace dvc

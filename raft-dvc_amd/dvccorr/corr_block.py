@@ -1,0 +1,197 @@
+"""Drop-in correlation blocks for RAFT-DVC on MI355X.
+
+Same constructor and call contract as the reference (zachtong/RAFT-DVC):
+
+    CorrBlock(fmap1, fmap2, num_levels=4, radius=4, legacy_wd_swap=False)   src/core/corr.py:116-139
+    CorrBlock.__call__(coords) -> (B, num_levels*(2r+1)**3, H, W, D) fp32    src/core/corr.py:169-208
+    CorrBlockOnTheFly(fmap1, fmap2, num_levels, radius, chunk_size,
+                      use_checkpoint)                                         src/core/corr_otf.py:51-94
+    bilinear_sampler_3d(vol, coords, legacy_wd_swap=False)                    src/core/corr.py:17-68
+    coords_grid_3d(batch, ht, wd, dp, device)                                 src/core/corr.py:71-99
+
+so RAFTDVC.forward (raft_dvc.py:369-450), the trainer and the evaluation
+scripts can use them unchanged.  The work is done by libdvccorr.so (gfx950
+HIP kernels): an MFMA GEMM builds every pyramid level against the pooled
+target features (equal to pooling the correlation, corr_otf.py:80-86), the
+lookup is a lane-per-query gather kernel, and the on-the-fly block never
+materialises the O(N^2) volume.
+
+Precision: fp32 feature maps build in exact f32 MFMA and store fp32
+(tolerance 1e-5 relative to the reference); `precision="bf16"` builds on
+bf16 MFMA and stores bf16 (tolerance 1e-2), halving the HBM traffic; the
+default follows the input dtype (fp16/bf16 inputs -> bf16), overridable with
+the DVCCORR_PRECISION environment variable.  Backward is not implemented yet.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional
+
+import torch
+
+from . import ops
+from ._lib import layout
+
+__all__ = ["CorrBlock", "CorrBlockFused", "CorrBlockOnTheFly", "bilinear_sampler_3d", "coords_grid_3d",
+           "make_corr_block", "resolve_precision"]
+
+
+def resolve_precision(fmap: torch.Tensor, precision: Optional[str]) -> str:
+    if precision is None:
+        precision = os.environ.get("DVCCORR_PRECISION") or None
+    if precision is None:
+        precision = "fp32" if fmap.dtype == torch.float32 else "bf16"
+    ops.dtype_code(precision)
+    return "bf16" if precision in ("bf16", "bfloat16") else "fp32"
+
+
+def _no_grad_guard(*ts: torch.Tensor) -> None:
+    if torch.is_grad_enabled() and any(t.requires_grad for t in ts):
+        raise NotImplementedError("dvccorr: backward through the correlation block is not implemented yet; "
+                                  "run under torch.no_grad() or detach the feature maps")
+
+
+def _check_fmaps(fmap1: torch.Tensor, fmap2: torch.Tensor) -> None:
+    if fmap1.ndim != 5:
+        raise ValueError(f"Expected 5D feature maps (B, C, H, W, D); got {fmap1.ndim}D")
+    if fmap1.shape != fmap2.shape:
+        raise ValueError(f"fmap1 and fmap2 must have matching shapes; got {tuple(fmap1.shape)} vs "
+                         f"{tuple(fmap2.shape)}")
+
+
+class CorrBlock:
+    """All-pairs 3-D correlation pyramid + radius-r trilinear lookup (materialised)."""
+
+    def __init__(self, fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int = 4, radius: int = 4,
+                 legacy_wd_swap: bool = False, *, precision: Optional[str] = None, build: str = "gemm"):
+        _check_fmaps(fmap1, fmap2)
+        _no_grad_guard(fmap1, fmap2)
+        self.num_levels = num_levels
+        self.radius = radius
+        self.legacy_wd_swap = legacy_wd_swap
+        B, C, H, W, D = fmap1.shape
+        self.shape = (B, C, H, W, D)
+        self._lay = layout(H, W, D, num_levels, C)      # RuntimeError where avg_pool3d would raise
+        self.precision = resolve_precision(fmap1, precision)
+        self._dt = ops.dtype_code(self.precision)
+        q = ops.pack_queries(fmap1.reshape(B, C, H * W * D), self._dt)
+        t = ops.pack_targets(fmap2, num_levels, self._dt)
+        if build == "gemm":       # every level from the pooled targets, one launch
+            self._corr = ops.build(q, t, C, H, W, D, num_levels, self._dt, self._dt)
+        elif build == "pool":     # the reference's op order: level 0 GEMM, then avg-pool the volume
+            corr = torch.empty((B, H * W * D, self._lay.row_stride), dtype=q.dtype, device=q.device)
+            ops.build(q, t, C, H, W, D, num_levels, self._dt, self._dt, 0, self._lay.level_elems[0], out=corr)
+            for l in range(num_levels - 1):
+                ops.pool(corr, H, W, D, num_levels, l, self._dt)
+            self._corr = corr
+        else:
+            raise ValueError(f"build must be 'gemm' or 'pool', got {build!r}")
+
+    @property
+    def corr_pyramid(self) -> List[torch.Tensor]:
+        """Zero-copy views shaped like the reference's list: (B*N, 1, H_l, W_l, D_l) per level."""
+        B, _, H, W, D = self.shape
+        flat = self._corr.reshape(B * H * W * D, self._lay.row_stride)
+        views = []
+        for l, (h, w, d) in enumerate(self._lay.levels()):
+            dp = self._lay.Dp[l]
+            off = self._lay.offset[l]
+            v = flat[:, off:off + h * w * dp].reshape(B * H * W * D, 1, h, w, dp)[..., :d]
+            views.append(v)
+        return views
+
+    def __call__(self, coords: torch.Tensor) -> torch.Tensor:
+        B, _, H, W, D = self.shape
+        if coords.ndim != 5 or tuple(coords.shape) != (B, 3, H, W, D):
+            raise ValueError(f"coords must be (B, 3, H, W, D) = {(B, 3, H, W, D)}; got {tuple(coords.shape)}")
+        out = ops.lookup(self._corr, coords.reshape(B, 3, H * W * D), H, W, D, self.num_levels, self.radius,
+                         self.legacy_wd_swap, self._dt)
+        return out.view(B, -1, H, W, D)
+
+
+class CorrBlockFused:
+    """On-the-fly lookup (no correlation volume), any sampler convention.
+
+    Keeps the packed fmap1 rows and the packed fmap2 pyramid (O(C * voxels));
+    each call computes the (2r+2)^3 window dots per query and interpolates them.
+    """
+
+    def __init__(self, fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int = 4, radius: int = 4,
+                 legacy_wd_swap: bool = False, *, precision: Optional[str] = None):
+        _check_fmaps(fmap1, fmap2)
+        _no_grad_guard(fmap1, fmap2)
+        self.num_levels = num_levels
+        self.radius = radius
+        self.legacy_wd_swap = legacy_wd_swap
+        B, C, H, W, D = fmap1.shape
+        self.shape = (B, C, H, W, D)
+        self._lay = layout(H, W, D, num_levels, C)
+        self.precision = resolve_precision(fmap1, precision)
+        self._dt = ops.dtype_code(self.precision)
+        self._q = ops.pack_queries(fmap1.reshape(B, C, H * W * D), self._dt)
+        self._t = ops.pack_targets(fmap2, num_levels, self._dt)
+        self._ws = ops.fused_workspace(B, H * W * D, num_levels, radius, fmap1.device)
+
+    def __call__(self, coords: torch.Tensor) -> torch.Tensor:
+        B, C, H, W, D = self.shape
+        if coords.ndim != 5 or tuple(coords.shape) != (B, 3, H, W, D):
+            raise ValueError(f"coords must be (B, 3, H, W, D) = {(B, 3, H, W, D)}; got {tuple(coords.shape)}")
+        out = ops.lookup_fused(self._q, self._t, coords.reshape(B, 3, H * W * D), C, H, W, D, self.num_levels,
+                               self.radius, self.legacy_wd_swap, self._dt, workspace=self._ws)
+        return out.view(B, -1, H, W, D)
+
+
+class CorrBlockOnTheFly(CorrBlockFused):
+    """Reference-signature on-the-fly block (corr_otf.py:51-94).
+
+    Like the reference it implements the LEGACY sampler convention
+    (corr_otf.py:227-234); chunk_size / use_checkpoint only shape the
+    reference's PyTorch memory use and are validated and ignored here.
+    """
+
+    def __init__(self, fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int = 4, radius: int = 4,
+                 chunk_size: int = 27, use_checkpoint: bool = True, *, precision: Optional[str] = None):
+        if fmap1.shape != fmap2.shape:
+            raise ValueError(f"fmap1 and fmap2 must have matching shapes; got {tuple(fmap1.shape)} vs "
+                             f"{tuple(fmap2.shape)}")
+        if fmap1.ndim != 5:
+            raise ValueError(f"Expected 5D feature maps (B, C, H, W, D); got {fmap1.ndim}D")
+        if chunk_size < 1:
+            raise ValueError(f"chunk_size must be >= 1; got {chunk_size}")
+        self.chunk_size = chunk_size
+        self.use_checkpoint = use_checkpoint
+        super().__init__(fmap1, fmap2, num_levels, radius, legacy_wd_swap=True, precision=precision)
+
+
+def bilinear_sampler_3d(vol: torch.Tensor, coords: torch.Tensor, legacy_wd_swap: bool = False) -> torch.Tensor:
+    """vol (B, C, H, W, D), coords (B, H', W', D', 3) in (h, w, d) -> (B, C, H', W', D')."""
+    if vol.ndim != 5 or coords.ndim != 5 or coords.shape[-1] != 3 or coords.shape[0] != vol.shape[0]:
+        raise ValueError(f"bad shapes vol {tuple(vol.shape)} coords {tuple(coords.shape)}")
+    B, C = vol.shape[:2]
+    out = ops.sample3d(vol, coords.reshape(B, -1, 3), legacy_wd_swap)
+    return out.view(B, C, *coords.shape[1:4])
+
+
+def coords_grid_3d(batch: int, ht: int, wd: int, dp: int, device: torch.device) -> torch.Tensor:
+    """Identity grid (B, 3, H, W, D), channel c = index along axis c (h, w, d)."""
+    axes = [torch.arange(s, device=device, dtype=torch.float32) for s in (ht, wd, dp)]
+    grid = torch.stack(torch.meshgrid(*axes, indexing="ij"), dim=0)
+    return grid.unsqueeze(0).expand(batch, 3, ht, wd, dp).contiguous()
+
+
+def make_corr_block(impl: str, fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int = 4, radius: int = 4,
+                    sampler_version: int = 2, **kw):
+    """The dispatch RAFTDVC.forward performs on config.corr_impl (raft_dvc.py:369-420), for the new impls.
+
+    impl "mi355x"        -> CorrBlock (materialised pyramid, fixed or legacy convention)
+    impl "mi355x_fused"  -> CorrBlockFused (on-the-fly, fixed or legacy convention)
+    """
+    if sampler_version not in (1, 2):
+        raise ValueError(f"Invalid corr_sampler_version: {sampler_version!r}. Must be 1 (legacy W<->D-swapped) "
+                         f"or 2 (fixed).")
+    legacy = sampler_version == 1
+    if impl == "mi355x":
+        return CorrBlock(fmap1, fmap2, num_levels, radius, legacy_wd_swap=legacy, **kw)
+    if impl == "mi355x_fused":
+        return CorrBlockFused(fmap1, fmap2, num_levels, radius, legacy_wd_swap=legacy, **kw)
+    raise ValueError(f"Invalid corr_impl for dvccorr: {impl!r}. Must be 'mi355x' or 'mi355x_fused'")

@@ -1,0 +1,144 @@
+"""Tensor-level wrappers over the C ABI.
+
+PyTorch supplies device memory and the current HIP stream; every call goes
+straight to libdvccorr.so (no CPU fallback).  Shapes follow include/dvccorr.h:
+
+    pack_queries(fmap1_slab (B, C, Nq) f32)            -> (B, Nq, Cp)          dtype
+    pack_targets(fmap2 (B, C, H, W, D) f32, L)         -> (B, row_stride, Cp)  dtype
+    build(q, t, ...)                                   -> (B, Nq, row_stride)  store dtype
+    pool(corr, ..., src_level)                         in place
+    lookup(corr, coords (B, 3, Nq) f32, ...)           -> (B, L*(2r+1)^3, Nq)  f32
+    lookup_fused(q, t, coords, ...)                    -> (B, L*(2r+1)^3, Nq)  f32
+    sample3d(vol (B, C, Hv, Wv, Dv), pts (B, Nq, 3))   -> (B, C, Nq)           f32
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import DVC_BF16, DVC_F32, DVC_FIXED, DVC_LEGACY, check, layout, lib
+
+_TORCH_DT = {DVC_F32: torch.float32, DVC_BF16: torch.bfloat16}
+
+
+def dtype_code(precision: str) -> int:
+    if precision in ("fp32", "float32", "f32"):
+        return DVC_F32
+    if precision in ("bf16", "bfloat16"):
+        return DVC_BF16
+    raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
+
+
+def _ptr(t: torch.Tensor) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(t: torch.Tensor) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _need_cuda(*ts: torch.Tensor) -> None:
+    for t in ts:
+        if not t.is_cuda:
+            raise RuntimeError("dvccorr runs on the MI355X only: got a CPU tensor (no CPU fallback)")
+
+
+def _f32c(t: torch.Tensor) -> torch.Tensor:
+    return t.to(torch.float32).contiguous()
+
+
+def pack_queries(fmap1_slab: torch.Tensor, dtype: int) -> torch.Tensor:
+    _need_cuda(fmap1_slab)
+    f = _f32c(fmap1_slab)
+    B, C, Nq = f.shape
+    Cp = (C + 31) // 32 * 32
+    out = torch.empty((B, Nq, Cp), dtype=_TORCH_DT[dtype], device=f.device)
+    check(lib().dvc_pack_queries(_ptr(f), _ptr(out), B, C, Nq, dtype, _stream(f)), "pack_queries")
+    return out
+
+
+def pack_targets(fmap2: torch.Tensor, num_levels: int, dtype: int) -> torch.Tensor:
+    _need_cuda(fmap2)
+    f = _f32c(fmap2)
+    B, C, H, W, D = f.shape
+    lay = layout(H, W, D, num_levels, C)
+    out = torch.empty((B, lay.row_stride, lay.c_pad), dtype=_TORCH_DT[dtype], device=f.device)
+    nws = lib().dvc_pack_workspace_bytes(B, C, H, W, D, num_levels)
+    ws = torch.empty((max(nws, 4) // 4,), dtype=torch.float32, device=f.device)
+    check(lib().dvc_pack_targets(_ptr(f), _ptr(out), _ptr(ws), B, C, H, W, D, num_levels, dtype, _stream(f)),
+          "pack_targets")
+    return out
+
+
+def build(packed_q: torch.Tensor, packed_t: torch.Tensor, C: int, H: int, W: int, D: int, num_levels: int,
+          in_dtype: int, store_dtype: int, col_begin: int = 0, col_end=None, out: torch.Tensor = None) -> torch.Tensor:
+    _need_cuda(packed_q, packed_t)
+    B, Nq, _ = packed_q.shape
+    lay = layout(H, W, D, num_levels, C)
+    col_end = lay.row_stride if col_end is None else col_end
+    if out is None:
+        out = torch.empty((B, Nq, lay.row_stride), dtype=_TORCH_DT[store_dtype], device=packed_q.device)
+    check(lib().dvc_corr_build(_ptr(packed_q), _ptr(packed_t), _ptr(out), B, Nq, C, H, W, D, num_levels, in_dtype,
+                               store_dtype, col_begin, col_end, _stream(packed_q)), "corr_build")
+    return out
+
+
+def pool(corr: torch.Tensor, H: int, W: int, D: int, num_levels: int, src_level: int, store_dtype: int) -> None:
+    _need_cuda(corr)
+    B, Nq, _ = corr.shape
+    check(lib().dvc_corr_pool(_ptr(corr), B, Nq, H, W, D, num_levels, src_level, store_dtype, _stream(corr)),
+          "corr_pool")
+
+
+def lookup(corr: torch.Tensor, coords: torch.Tensor, H: int, W: int, D: int, num_levels: int, radius: int,
+           legacy: bool, store_dtype: int, out: torch.Tensor = None) -> torch.Tensor:
+    _need_cuda(corr, coords)
+    B, Nq, _ = corr.shape
+    c = _f32c(coords)
+    n3 = (2 * radius + 1) ** 3
+    if out is None:
+        out = torch.empty((B, num_levels * n3, Nq), dtype=torch.float32, device=corr.device)
+    check(lib().dvc_corr_lookup(_ptr(corr), _ptr(c), _ptr(out), B, Nq, H, W, D, num_levels, radius,
+                                DVC_LEGACY if legacy else DVC_FIXED, store_dtype, _stream(corr)), "corr_lookup")
+    return out
+
+
+def lookup_fused(packed_q: torch.Tensor, packed_t: torch.Tensor, coords: torch.Tensor, C: int, H: int, W: int,
+                 D: int, num_levels: int, radius: int, legacy: bool, dtype: int, out: torch.Tensor = None,
+                 workspace: torch.Tensor = None) -> torch.Tensor:
+    _need_cuda(packed_q, packed_t, coords)
+    B, Nq, _ = packed_q.shape
+    c = _f32c(coords)
+    n3 = (2 * radius + 1) ** 3
+    if out is None:
+        out = torch.empty((B, num_levels * n3, Nq), dtype=torch.float32, device=packed_q.device)
+    nws = lib().dvc_lookup_fused_workspace_bytes(B, Nq, num_levels, radius)
+    if workspace is None or workspace.numel() * workspace.element_size() < nws:
+        workspace = torch.empty((max(nws, 4) // 4,), dtype=torch.float32, device=packed_q.device)
+    check(lib().dvc_corr_lookup_fused(_ptr(packed_q), _ptr(packed_t), _ptr(c), _ptr(out), _ptr(workspace), B, Nq, C,
+                                      H, W, D, num_levels, radius, DVC_LEGACY if legacy else DVC_FIXED, dtype,
+                                      _stream(packed_q)), "corr_lookup_fused")
+    return out
+
+
+def fused_workspace(B: int, Nq: int, num_levels: int, radius: int, device) -> torch.Tensor:
+    nws = lib().dvc_lookup_fused_workspace_bytes(B, Nq, num_levels, radius)
+    return torch.empty((max(nws, 4) // 4,), dtype=torch.float32, device=device)
+
+
+def sample3d(vol: torch.Tensor, pts: torch.Tensor, legacy: bool) -> torch.Tensor:
+    _need_cuda(vol, pts)
+    v = _f32c(vol)
+    p = _f32c(pts)
+    B, C, Hv, Wv, Dv = v.shape
+    Nq = p.numel() // (3 * B)
+    out = torch.empty((B, C, Nq), dtype=torch.float32, device=v.device)
+    check(lib().dvc_sample3d(_ptr(v), _ptr(p), _ptr(out), B, C, Hv, Wv, Dv, Nq,
+                             DVC_LEGACY if legacy else DVC_FIXED, _stream(v)), "sample3d")
+    return out
+
+
+__all__ = ["pack_queries", "pack_targets", "build", "pool", "lookup", "lookup_fused", "sample3d", "fused_workspace",
+           "dtype_code", "layout", "_lib"]

@@ -1,0 +1,144 @@
+"""Query-voxel sharding of the correlation block across the GPUs of one node.
+
+Rows of the correlation volume are independent: row q of every pyramid level
+depends only on fmap1[:, q] and all of fmap2, and the lookup of q only on
+those rows and coords[q].  So each rank owns a contiguous
+slab of H planes of the query volume:
+
+  * fmap2 is replicated once per forward with one RCCL all-gather of the
+    per-rank fmap2 slabs (each GPU receives (n-1)/n of fmap2 over its xGMI
+    links in parallel);
+  * each rank builds only its own rows of every level -- they never move
+    (64^3 at 1/4: 19.6 GB/GPU bf16 at n=8 instead of 157 GB);
+  * each lookup is shard-resident; gather_output=True additionally
+    all-gathers the lookup output for an unsharded consumer.
+
+Sharded results are bitwise equal to the single-GPU ones: the same kernels
+run on the same rows.  The reference has no distributed code; this is new
+design.  The per-rank compute is a pluggable backend (default: the HIP
+library) so the partitioning / collective logic is testable on CPU (gloo).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from . import ops
+from .corr_block import resolve_precision
+
+
+def slab_bounds(H: int, world: int, rank: int):
+    """Contiguous H-plane slab [h0, h1) of `rank` (sizes differ by at most one)."""
+    base, rem = divmod(H, world)
+    h0 = rank * base + min(rank, rem)
+    return h0, h0 + base + (1 if rank < rem else 0)
+
+
+def _world(group) -> int:
+    return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+
+
+def _rank(group) -> int:
+    return dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
+
+
+def gather_slabs(slab: torch.Tensor, H: int, group=None, dim: int = 2) -> torch.Tensor:
+    """All-gather H-slabs (split along `dim`) into the full tensor.  One collective."""
+    world = _world(group)
+    if world == 1:
+        return slab
+    maxh = -(-H // world)
+    pad = maxh - slab.shape[dim]
+    if pad:
+        shape = list(slab.shape)
+        shape[dim] = pad
+        slab = torch.cat([slab, slab.new_zeros(shape)], dim=dim)
+    slab = slab.contiguous()
+    buf = slab.new_empty((world,) + tuple(slab.shape))
+    try:
+        dist.all_gather_into_tensor(buf, slab, group=group)
+    except (RuntimeError, NotImplementedError, ValueError):
+        dist.all_gather(list(buf.unbind(0)), slab, group=group)
+    parts = []
+    for r in range(world):
+        h0, h1 = slab_bounds(H, world, r)
+        parts.append(buf[r].narrow(dim, 0, h1 - h0))
+    return torch.cat(parts, dim=dim)
+
+
+class HipRows:
+    """Default backend: this rank's query rows against the full target pyramid on the GPU."""
+
+    def __init__(self, q_flat: torch.Tensor, fmap2: torch.Tensor, num_levels: int, radius: int, legacy: bool,
+                 precision: str, impl: str, q_offset: int = 0):
+        B, C, H, W, D = fmap2.shape
+        self.dims = (C, H, W, D)
+        self.L, self.R, self.legacy, self.impl = num_levels, radius, legacy, impl
+        self.dt = ops.dtype_code(precision)
+        self.q = ops.pack_queries(q_flat, self.dt)
+        self.t = ops.pack_targets(fmap2, num_levels, self.dt)
+        if impl == "materialised":
+            self.corr = ops.build(self.q, self.t, C, H, W, D, num_levels, self.dt, self.dt)
+        elif impl == "fused":
+            self.ws = ops.fused_workspace(B, q_flat.shape[2], num_levels, radius, fmap2.device)
+        else:
+            raise ValueError(f"impl must be 'materialised' or 'fused', got {impl!r}")
+
+    def lookup(self, coords_flat: torch.Tensor) -> torch.Tensor:
+        C, H, W, D = self.dims
+        if self.impl == "materialised":
+            return ops.lookup(self.corr, coords_flat, H, W, D, self.L, self.R, self.legacy, self.dt)
+        return ops.lookup_fused(self.q, self.t, coords_flat, C, H, W, D, self.L, self.R, self.legacy, self.dt,
+                                workspace=self.ws)
+
+
+class ShardedCorrBlock:
+    """CorrBlock over this rank's H-slab of query voxels (fmap1 / coords slabs, full fmap2 gathered).
+
+    Args:
+        fmap1_slab, fmap2_slab: (B, C, h1-h0, W, D), this rank's slab_bounds(H) planes.
+        H: full H extent of the feature maps.
+        gather_output: all-gather every lookup output to the full (B, L*n^3, H, W, D).
+        backend: per-rank compute (default HipRows); see tests/test_sharded_gloo.py.
+    """
+
+    def __init__(self, fmap1_slab: torch.Tensor, fmap2_slab: torch.Tensor, H: int, num_levels: int = 4,
+                 radius: int = 4, legacy_wd_swap: bool = False, *, precision: Optional[str] = None,
+                 impl: str = "materialised", group=None, gather_output: bool = False, build_events=None,
+                 backend=HipRows):
+        if fmap1_slab.shape != fmap2_slab.shape or fmap1_slab.ndim != 5:
+            raise ValueError(f"slabs must be matching 5-D tensors; got {tuple(fmap1_slab.shape)} vs "
+                             f"{tuple(fmap2_slab.shape)}")
+        self.group = group
+        self.world, self.rank = _world(group), _rank(group)
+        h0, h1 = slab_bounds(H, self.world, self.rank)
+        B, C, Hs, W, D = fmap1_slab.shape
+        if Hs != h1 - h0:
+            raise ValueError(f"rank {self.rank} slab has {Hs} planes, slab_bounds gives {h1 - h0}")
+        self.H, self.h0, self.h1 = H, h0, h1
+        self.shape = (B, C, Hs, W, D)
+        self.num_levels, self.radius, self.legacy_wd_swap = num_levels, radius, legacy_wd_swap
+        self.gather_output = gather_output
+        precision = resolve_precision(fmap1_slab, precision)
+        stream = torch.cuda.current_stream(fmap1_slab.device) if fmap1_slab.is_cuda else None
+        if build_events is not None and stream is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        fmap2 = gather_slabs(fmap2_slab, H, group)           # the one data-path collective per forward
+        self.rows = backend(fmap1_slab.reshape(B, C, Hs * W * D), fmap2, num_levels, radius, legacy_wd_swap,
+                            precision, impl, q_offset=h0 * W * D)
+        if build_events is not None and stream is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record(stream)
+            build_events.append((e0, e1))
+
+    def __call__(self, coords_slab: torch.Tensor) -> torch.Tensor:
+        B, C, Hs, W, D = self.shape
+        if tuple(coords_slab.shape) != (B, 3, Hs, W, D):
+            raise ValueError(f"coords slab must be {(B, 3, Hs, W, D)}; got {tuple(coords_slab.shape)}")
+        out = self.rows.lookup(coords_slab.reshape(B, 3, Hs * W * D)).view(B, -1, Hs, W, D)
+        if self.gather_output:
+            out = gather_slabs(out, self.H, self.group)
+        return out

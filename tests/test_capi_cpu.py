@@ -1,0 +1,125 @@
+"""CPU: the C-ABI library loads, exports every declared symbol, and its host
+logic (geometry, validation, error mapping) behaves like the reference.
+No compute call is made (no GPU here)."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+from conftest import REPO
+
+
+def _header_functions():
+    txt = open(os.path.join(REPO, "include", "dvccorr.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(dvc_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    from dvccorr import _lib
+    L = _lib.lib()
+    declared = _header_functions()
+    assert len(declared) >= 13
+    for name in declared:
+        assert hasattr(L, name), name
+    assert set(declared) == set(_lib.EXPORTED)
+    assert L.dvc_abi_version() == 1
+    assert b"gfx950" in L.dvc_version()
+
+
+def test_library_is_gfx950_code_object():
+    from dvccorr import _lib
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+@pytest.mark.parametrize("shape,L,expect", [
+    ((32, 32, 32), 4, [(32, 32, 32), (16, 16, 16), (8, 8, 8), (4, 4, 4)]),
+    ((16, 16, 16), 4, [(16, 16, 16), (8, 8, 8), (4, 4, 4), (2, 2, 2)]),
+    ((8, 8, 8), 4, [(8, 8, 8), (4, 4, 4), (2, 2, 2), (1, 1, 1)]),
+    ((9, 7, 8), 3, [(9, 7, 8), (4, 3, 4), (2, 1, 2)]),
+    ((128, 128, 128), 2, [(128, 128, 128), (64, 64, 64)]),
+])
+def test_layout_geometry(shape, L, expect):
+    from dvccorr import layout
+    lay = layout(*shape, L, 128)
+    assert lay.levels() == expect
+    off = 0
+    for l, (h, w, d) in enumerate(expect):
+        assert lay.Dp[l] % 8 == 0 and lay.Dp[l] >= d
+        assert lay.offset[l] == off
+        assert lay.level_elems[l] == h * w * lay.Dp[l]
+        assert lay.zero_level[l] == int(min(h, w, d) == 1)
+        off += lay.level_elems[l]
+    assert lay.row_elems == off and lay.row_stride % 128 == 0 and lay.row_stride >= off
+    assert lay.c_pad == 128
+
+
+def test_layout_raises_where_reference_raises():
+    from dvccorr import layout
+    with pytest.raises(RuntimeError):
+        layout(8, 8, 2, 3)          # (4,4,1) cannot be pooled again (avg_pool3d error)
+    with pytest.raises(RuntimeError):
+        layout(8, 8, 8, 5)
+    layout(8, 8, 2, 2)
+
+
+def test_bf16_row_bytes_for_baseline_configs():
+    """pyramid elements N * P_L (unpadded) for configs #2-#4."""
+    from dvccorr import layout
+    for S, N, PL in ((16, 4096, 1.917e7), (32, 32768, 1.227e9), (64, 262144, 7.85e10)):
+        lay = layout(S, S, S, 4, 128)
+        unpadded = sum(h * w * d for (h, w, d) in lay.levels())
+        assert abs(N * unpadded - PL) / PL < 0.001
+        assert lay.row_elems <= 1.02 * unpadded     # z padding to 8 costs <= 2 %
+
+
+def test_validation_errors_without_gpu():
+    """Argument checks run before any HIP call and map to ValueError."""
+    from dvccorr import _lib
+    L = _lib.lib()
+    rc = L.dvc_corr_lookup(None, None, None, 1, 8, 2, 2, 2, 1, 4, 0, 0, None)
+    assert rc == _lib.DVC_ERR_INVALID
+    with pytest.raises(ValueError, match="null pointer"):
+        _lib.check(rc)
+    rc = L.dvc_corr_build(ctypes.c_void_p(16), ctypes.c_void_p(16), ctypes.c_void_p(16), 1, 8, 32, 8, 8, 8, 1,
+                          _lib.DVC_BF16, _lib.DVC_BF16, 64, 512, None)
+    assert rc == _lib.DVC_ERR_INVALID       # column range must start on a 128 boundary
+    rc = L.dvc_corr_lookup(ctypes.c_void_p(16), ctypes.c_void_p(16), ctypes.c_void_p(16), 1, 8, 8, 8, 8, 1, 4, 7,
+                           0, None)
+    assert rc == _lib.DVC_ERR_INVALID       # convention
+    assert L.dvc_lookup_fused_workspace_bytes(1, 100000, 2, 4) == 65536 * 10 * 10 * 12 * 4
+
+
+def test_product_path_refuses_cpu_tensors():
+    import dvccorr
+    f = torch.randn(1, 16, 8, 8, 8)
+    with pytest.raises(RuntimeError, match="MI355X"):
+        dvccorr.CorrBlock(f, f, 2, 4)
+    with pytest.raises(RuntimeError, match="MI355X"):
+        dvccorr.CorrBlockFused(f, f, 2, 4)
+
+
+def test_reference_style_argument_errors():
+    import dvccorr
+    f = torch.randn(1, 16, 8, 8, 8)
+    with pytest.raises(ValueError):
+        dvccorr.CorrBlock(f, torch.randn(1, 16, 8, 8, 4))
+    with pytest.raises(ValueError):
+        dvccorr.CorrBlockOnTheFly(f, f, chunk_size=0)
+    with pytest.raises(ValueError):
+        dvccorr.make_corr_block("mi355x", f, f, sampler_version=3)
+    with pytest.raises(NotImplementedError):
+        dvccorr.CorrBlock(f.requires_grad_(True), f)
+
+
+def test_coords_grid_matches_reference_fixture():
+    import numpy as np
+    import prng
+    import dvccorr
+    g = dvccorr.coords_grid_3d(2, 3, 4, 5, torch.device("cpu"))
+    np.testing.assert_array_equal(g.numpy(), prng.identity_coords(2, 3, 4, 5))

@@ -1,0 +1,236 @@
+"""GPU parity: the HIP path (through the C ABI) against the golden vectors and
+the CPU oracle.
+
+Tolerances (north_star): max|out - ref| / max|ref|
+  fp32 build + lookup     <= 1e-5
+  bf16-MFMA build         <= 1e-2
+"""
+from __future__ import annotations
+
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import prng
+from conftest import GOLDEN, corr_inputs, load_golden
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+FP32_TOL = 1e-5
+BF16_TOL = 1e-2
+CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "equiv_*.npz"))) + \
+    sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "edge_*.npz")))
+
+DEV = torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _no_grad():
+    with torch.no_grad():
+        yield
+
+
+def _gpu(*arrs):
+    return [torch.from_numpy(np.ascontiguousarray(a)).to(DEV) for a in arrs]
+
+
+def _rows(out: torch.Tensor, rows) -> np.ndarray:
+    B, Ch = out.shape[:2]
+    flat = out.reshape(B, Ch, -1).cpu().numpy()
+    N = flat.shape[2]
+    return np.stack([flat[r // N, :, r % N] for r in rows])
+
+
+def _blocks(kind, t1, t2, L, r, legacy, precision):
+    import dvccorr
+    if kind == "gemm":
+        return dvccorr.CorrBlock(t1, t2, L, r, legacy_wd_swap=legacy, precision=precision)
+    if kind == "pool":
+        return dvccorr.CorrBlock(t1, t2, L, r, legacy_wd_swap=legacy, precision=precision, build="pool")
+    return dvccorr.CorrBlockFused(t1, t2, L, r, legacy_wd_swap=legacy, precision=precision)
+
+
+@pytest.mark.parametrize("kind", ["gemm", "pool", "fused"])
+@pytest.mark.parametrize("case", CASES)
+def test_small_cases_fp32(case, kind):
+    g = load_golden(case + ".npz")
+    f1, f2, coords, L, r = corr_inputs(g)
+    t1, t2, tc = _gpu(f1, f2, coords)
+    for legacy, tag in ((False, "fixed"), (True, "legacy")):
+        out = _blocks(kind, t1, t2, L, r, legacy, "fp32")(tc)
+        assert out.shape == (f1.shape[0], L * (2 * r + 1) ** 3) + f1.shape[2:]
+        assert out.dtype == torch.float32 and out.is_contiguous()
+        e = orc.rel_err(_rows(out, g["rows"]), g[f"out_rows_{tag}"])
+        assert e <= FP32_TOL, (case, kind, tag, e)
+        full = orc.corr_lookup(f1, f2, coords, L, r, legacy)
+        e = orc.rel_err(out.cpu().numpy(), full)
+        assert e <= FP32_TOL, (case, kind, tag, "full", e)
+
+
+@pytest.mark.parametrize("kind", ["gemm", "fused"])
+@pytest.mark.parametrize("case", ["equiv_L4_r4", "edge_978_L3_r3", "cfg2"])
+def test_bf16_build(case, kind):
+    g = load_golden(case + ".npz")
+    f1, f2, coords, L, r = corr_inputs(g)
+    t1, t2, tc = _gpu(f1, f2, coords)
+    for legacy, tag in ((False, "fixed"), (True, "legacy")):
+        out = _blocks(kind, t1, t2, L, r, legacy, "bf16")(tc)
+        e = orc.rel_err(_rows(out, g["rows"]), g[f"out_rows_{tag}"])
+        assert e <= BF16_TOL, (case, kind, tag, e)
+
+
+@pytest.mark.parametrize("kind", ["gemm", "pool", "fused"])
+def test_cfg2_fp32_checksums(kind):
+    """Config #2 (16^3, C=128, L=4, r=4) fp32: sampled rows + full-output checksums."""
+    g = load_golden("cfg2.npz")
+    f1, f2, coords, L, r = corr_inputs(g)
+    t1, t2, tc = _gpu(f1, f2, coords)
+    out = _blocks(kind, t1, t2, L, r, False, "fp32")(tc)
+    assert orc.rel_err(_rows(out, g["rows"]), g["out_rows_fixed"]) <= FP32_TOL
+    o = out.double()
+    cs = g["checksum_fixed"]
+    assert abs(o.abs().max().item() - cs[3]) / cs[3] < FP32_TOL
+    assert abs((o * o).sum().item() - cs[2]) / cs[2] < 1e-6
+    sums = o.reshape(1, L, -1).sum(-1)[0].cpu().numpy()
+    np.testing.assert_allclose(sums, g["level_sums_fixed"], rtol=1e-4, atol=1e-3 * cs[3])
+
+
+@pytest.mark.parametrize("precision,tol", [("fp32", FP32_TOL), ("bf16", BF16_TOL)])
+def test_cfg3_rows(precision, tol):
+    """Config #3 (32^3, C=128, L=4, r=4): the bench workload, sampled rows vs the reference."""
+    import dvccorr
+    g = load_golden("cfg3.npz")
+    f1, f2, coords, L, r = corr_inputs(g)
+    t1, t2, tc = _gpu(f1, f2, coords)
+    blk = dvccorr.CorrBlock(t1, t2, L, r, precision=precision)
+    out = blk(tc)
+    for legacy, tag in ((False, "fixed"), (True, "legacy")):
+        if legacy:
+            blk.legacy_wd_swap = True
+            out = blk(tc)
+        e = orc.rel_err(_rows(out, g["rows"]), g[f"out_rows_{tag}"])
+        assert e <= tol, (precision, tag, e)
+    cs = g["checksum_fixed"]
+    if precision == "fp32":
+        blk.legacy_wd_swap = False
+        o = blk(tc).double()
+        assert abs((o * o).sum().item() - cs[2]) / cs[2] < 1e-5
+    # pyramid rows through the reference-shaped zero-copy views
+    pyr = blk.corr_pyramid
+    assert [tuple(p.shape[2:]) for p in pyr] == [(32, 32, 32), (16, 16, 16), (8, 8, 8), (4, 4, 4)]
+    prow = g["rows"][: g["pyr_rows"].shape[0]]
+    got = np.concatenate([p.reshape(p.shape[0], -1)[torch.from_numpy(prow).to(DEV)].float().cpu().numpy()
+                          for p in pyr], axis=1)
+    assert orc.rel_err(got, g["pyr_rows"]) <= tol
+
+
+def test_sampler_kats():
+    import dvccorr
+    g = load_golden("sampler_kat.npz")
+    v = torch.zeros(1, 1, 8, 12, 16, device=DEV)
+    v[0, 0, 3, 7, 11] = 1.0
+    q = torch.from_numpy(g["imp_queries"]).to(DEV)
+    np.testing.assert_array_equal(dvccorr.bilinear_sampler_3d(v, q).cpu().numpy(), g["imp_fixed"])
+    np.testing.assert_array_equal(dvccorr.bilinear_sampler_3d(v, q, legacy_wd_swap=True).cpu().numpy(),
+                                  g["imp_legacy"])
+    cube = torch.zeros(1, 1, 16, 16, 16, device=DEV)
+    cube[0, 0, 3, 7, 11] = 1.0
+    cq = torch.from_numpy(g["cube_queries"]).to(DEV)
+    np.testing.assert_array_equal(dvccorr.bilinear_sampler_3d(cube, cq, True).cpu().numpy(), g["cube_legacy"])
+    rv = torch.from_numpy(prng.normal(101, (1, 2, 9, 7, 8))).to(DEV)
+    pts = torch.from_numpy(g["rand_pts"]).to(DEV)
+    for leg, key in ((False, "rand_fixed"), (True, "rand_legacy")):
+        assert orc.rel_err(dvccorr.bilinear_sampler_3d(rv, pts, leg).cpu().numpy(), g[key]) <= 1e-6
+
+
+def test_peak_location():
+    """test_corr_sampler.py:74-105: the 9^3 window argmax sits at the true shift (fixed), drifts (legacy)."""
+    import dvccorr
+    g = load_golden("peak_shift.npz")
+    G, C = int(g["G"][0]), int(g["C"][0])
+    shift = tuple(int(s) for s in g["shift"])
+    f2 = prng.normal(int(g["seed"][0]), (1, C, G, G, G))
+    f1 = np.roll(f2, tuple(-s for s in shift), axis=(2, 3, 4)).copy()
+    t1, t2 = _gpu(f1, f2)
+    coords = dvccorr.coords_grid_3d(1, G, G, G, DEV)
+    for legacy, key in ((False, "out_fixed"), (True, "out_legacy")):
+        for kind in ("gemm", "fused"):
+            out = _blocks(kind, t1, t2, 1, 4, legacy, "fp32")(coords)
+            probes = np.stack([out[0, :, h, w, d].cpu().numpy() for (h, w, d) in g["probes"]])
+            assert orc.rel_err(probes, g[key]) <= FP32_TOL
+            offs = [tuple(int(i) - 4 for i in np.unravel_index(int(np.argmax(p)), (9, 9, 9))) for p in probes]
+            assert (offs == [shift] * 4) != legacy
+
+
+def test_zero_levels_and_errors():
+    import dvccorr
+    f = torch.randn(1, 8, 8, 8, 2, device=DEV)
+    with pytest.raises(RuntimeError):
+        dvccorr.CorrBlock(f, f, 3, 4)
+    blk = dvccorr.CorrBlock(f, f, 2, 2)
+    out = blk(dvccorr.coords_grid_3d(1, 8, 8, 2, DEV))
+    assert out[:, 125:].abs().max().item() == 0.0      # level 1 is (4,4,1): all zeros (corr.py:41-44)
+    assert out[:, :125].abs().max().item() > 0.0
+    with pytest.raises(ValueError):
+        blk(torch.zeros(1, 3, 8, 8, 3, device=DEV))
+
+
+def test_nonfinite_coords_give_zero():
+    """NaN / huge coordinates: every corner out of range in the reference -> 0 (no NaN leaks)."""
+    import dvccorr
+    f1 = torch.randn(1, 16, 8, 8, 8, device=DEV)
+    f2 = torch.randn(1, 16, 8, 8, 8, device=DEV)
+    c = dvccorr.coords_grid_3d(1, 8, 8, 8, DEV).clone()
+    c[0, 0, 1, 2, 3] = float("nan")
+    c[0, 1, 4, 4, 4] = 1e30
+    c[0, 2, 5, 5, 5] = -1e9
+    for kind in ("gemm", "fused"):
+        out = _blocks(kind, f1, f2, 2, 4, False, "fp32")(c)
+        assert torch.isfinite(out).all()
+        for (h, w, d) in ((1, 2, 3), (4, 4, 4), (5, 5, 5)):
+            assert out[0, :, h, w, d].abs().max().item() == 0.0
+        ref = orc.corr_lookup(f1.cpu().numpy(), f2.cpu().numpy(), c.cpu().numpy(), 2, 4, False)
+        assert orc.rel_err(out.cpu().numpy(), ref) <= FP32_TOL
+
+
+def test_plumbing_iterations():
+    """Config #1: the fmaps and per-iteration coords RAFTDVC fed the reference CorrBlock (64^3, 1/8, L=4)."""
+    import dvccorr
+    g = load_golden("plumbing.npz")
+    t1, t2 = _gpu(g["fmap1"], g["fmap2"])
+    for kind in ("gemm", "fused"):
+        blk = _blocks(kind, t1, t2, 4, 4, False, "fp32")
+        for it in range(g["coords"].shape[0]):
+            out = blk(_gpu(g["coords"][it])[0])
+            assert orc.rel_err(_rows(out, g["rows"]), g["out_rows"][it]) <= FP32_TOL, (kind, it)
+            cs = g["out_checksums"][it]
+            o = out.double()
+            assert abs((o * o).sum().item() - cs[2]) / cs[2] < 1e-5
+    # the reference-signature on-the-fly block is legacy-only, like corr_otf.py
+    otf = dvccorr.CorrBlockOnTheFly(t1, t2, 4, 4)
+    c0 = _gpu(g["coords"][0])[0]
+    ref_leg = dvccorr.CorrBlock(t1, t2, 4, 4, legacy_wd_swap=True)(c0)
+    assert orc.rel_err(otf(c0).cpu().numpy(), ref_leg.cpu().numpy()) <= FP32_TOL
+
+
+def test_determinism_and_linearity_at_cfg3():
+    """Size-independent properties at the bench size (bf16): bitwise determinism,
+    exact scaling by 2 (power-of-two scale commutes with every rounding)."""
+    import dvccorr
+    S = 32
+    f1 = torch.randn(1, 128, S, S, S, device=DEV)
+    f2 = torch.randn(1, 128, S, S, S, device=DEV)
+    c = torch.from_numpy(prng.flow_coords(77, 1, S, S, S, 2.0)).to(DEV)
+    blk = dvccorr.CorrBlock(f1, f2, 4, 4, precision="bf16")
+    a = blk(c)
+    b = blk(c)
+    assert torch.equal(a, b)
+    blk2 = dvccorr.CorrBlock(f1 * 2, f2, 4, 4, precision="bf16")
+    assert torch.equal(blk2(c), 2 * a)
+    # the fused path agrees with the materialised one at the bench size
+    fz = dvccorr.CorrBlockFused(f1, f2, 4, 4, precision="bf16")(c)
+    assert orc.rel_err(fz.cpu().numpy(), a.cpu().numpy()) <= BF16_TOL
