@@ -29,7 +29,7 @@
  *   packed targets [B][row_stride][c_pad] dtype; rows = level-concatenated target voxels
  *   corr pyramid   [B][Nq][row_stride]    store dtype; row q holds every level of query q:
  *                  level l voxel (y,x,z) at offset[l] + (y*W_l + x)*Dp_l + z, Dp_l = ceil8(D_l),
- *                  padding columns are 0.
+ *                  padding columns are 0; DVC_CORR_GUARD_BYTES of zeros before and after.
  * Nq is the number of query voxels per batch element; Nq == H*W*D for the
  * reference CorrBlock, Nq < H*W*D for one rank's query slab (sharded path).
  */
@@ -45,6 +45,12 @@ extern "C" {
 
 #define DVC_MAX_LEVELS 8
 #define DVC_ABI_VERSION 1
+/* The corr pyramid buffer passed to dvc_corr_lookup must be readable, and
+ * hold finite values (e.g. zeros), for DVC_CORR_GUARD_BYTES before its first
+ * row and after its last row: the lookup loads each window run from a clamped
+ * address without branching and cancels out-of-range elements with zero
+ * weights, so it may touch up to 2r+2 elements outside a row. */
+#define DVC_CORR_GUARD_BYTES 256
 
 typedef enum {
     DVC_OK = 0,

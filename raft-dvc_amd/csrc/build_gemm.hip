@@ -31,14 +31,16 @@ constexpr int kBQ = 128, kBP = 128;
 
 __device__ __forceinline__ int swz_mask(int nch) { return (nch >= 16 ? 16 : nch) - 1; }
 
+template <int NCH>
 __global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict__ Q, const bf16_t *__restrict__ T,
                                                        bf16_t *__restrict__ corr, long long Nq, int Cp,
                                                        long long t_batch_rows, long long row_stride,
                                                        long long col_begin, long long col_end, int nchunk,
                                                        float scale, int store_f32) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int nch = Cp / 8;                   // 16-byte chunks per row
-    const int msk = swz_mask(nch);
+    constexpr int nch = NCH;                  // 16-byte chunks per row (Cp / 8)
+    constexpr int msk = (NCH >= 16 ? 16 : NCH) - 1;
+    constexpr int PF = kBP * NCH / 256;       // prefetch chunks per thread for one target tile
     u32x4 *sQ = reinterpret_cast<u32x4 *>(smem);
     u32x4 *sT = sQ + kBQ * nch;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -61,14 +63,35 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict_
     const int wp = w & 1, wq = w >> 1;
     const int h = lane >> 5, r32 = lane & 31;
 
+    // register prefetch of the next target tile: its global loads fly while the
+    // current tile's MFMAs and epilogue run
+    u32x4 pf[PF];
+    if (chunk < ncol_tiles) {
+        const long long p0 = col_begin + (long long)chunk * kBP;
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+            const int id = i * 256 + t;
+            pf[i] = *reinterpret_cast<const u32x4 *>(Tb + (p0 + id / nch) * Cp + (id % nch) * 8);
+        }
+    }
     for (long long ct = chunk; ct < ncol_tiles; ct += nchunk) {
         const long long p0 = col_begin + ct * kBP;
-        __syncthreads();   // previous staging image fully stored / sQ written
-        for (int id = t; id < kBP * nch; id += 256) {
-            const int row = id / nch, c = id - row * nch;
-            sT[row * nch + (c ^ (row & msk))] = *reinterpret_cast<const u32x4 *>(Tb + (p0 + row) * Cp + c * 8);
+        __syncthreads();   // previous staging image fully read / sQ written
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+            const int id = i * 256 + t;
+            const int row = id / nch, c = id % nch;
+            sT[row * nch + (c ^ (row & msk))] = pf[i];
         }
         __syncthreads();
+        if (ct + nchunk < ncol_tiles) {
+            const long long pn = p0 + (long long)nchunk * kBP;
+#pragma unroll
+            for (int i = 0; i < PF; ++i) {
+                const int id = i * 256 + t;
+                pf[i] = *reinterpret_cast<const u32x4 *>(Tb + (pn + id / nch) * Cp + (id % nch) * 8);
+            }
+        }
 
         f32x16 acc[2][2];
 #pragma unroll
@@ -78,7 +101,8 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict_
 #pragma unroll
                 for (int k = 0; k < 16; ++k) acc[i][j][k] = 0.0f;
 
-        for (int ks = 0; ks < Cp / 16; ++ks) {
+#pragma unroll
+        for (int ks = 0; ks < NCH / 2; ++ks) {
             const int c = 2 * ks + h;
             bf16x8 a[2], bq[2];
 #pragma unroll
@@ -262,5 +286,14 @@ __global__ __launch_bounds__(256, 1) void k_build_f32(const float *__restrict__ 
         }
     }
 }
+
+template __global__ void k_build_bf16<4>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long, long long,
+                                         long long, long long, int, float, int);
+template __global__ void k_build_bf16<8>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long, long long,
+                                         long long, long long, int, float, int);
+template __global__ void k_build_bf16<16>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+                                          long long, long long, long long, int, float, int);
+template __global__ void k_build_bf16<32>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+                                          long long, long long, long long, int, float, int);
 
 }  // namespace dvc

@@ -15,6 +15,7 @@ namespace dvc {
 __global__ void k_pool_fmap(const float *, float *, long long, int, int, int, int, int, int);
 template <typename T>
 __global__ void k_pack_rows(const float *, T *, int, int, long long, long long, int, int, long long, long long);
+template <int NCH>
 __global__ void k_build_bf16(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long, long long, long long,
                              long long, int, float, int);
 __global__ void k_build_f32(const float *, const float *, float *, long long, int, long long, long long, long long,
@@ -63,6 +64,7 @@ static int fill_lookup_args(LookupArgs &A, const dvc_layout &lay, const void *co
     for (int l = 0; l < DVC_MAX_LEVELS; ++l) {
         A.H[l] = lay.H[l]; A.W[l] = lay.W[l]; A.D[l] = lay.D[l]; A.Dp[l] = lay.Dp[l];
         A.zero[l] = lay.zero_level[l]; A.off[l] = lay.offset[l];
+        A.generic[l] = l < lay.num_levels && A.legacy && lay.W[l] != lay.D[l];
     }
     return DVC_OK;
 }
@@ -202,15 +204,20 @@ int dvc_corr_build(const void *packed_q, const void *packed_t, void *corr, int B
     if (in_dtype == DVC_BF16) {
         if (store_dtype != DVC_BF16 && store_dtype != DVC_F32) return fail(DVC_ERR_INVALID, "build: bad store dtype");
         const size_t lds = (size_t)128 * Cp * 2 + std::max<size_t>((size_t)128 * Cp * 2, 32768);
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute((const void *)k_build_bf16, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            attr = true;
-        }
         dim3 grid((unsigned)(ceil_div(Nq, 128) * nchunk), 1, (unsigned)B);
-        k_build_bf16<<<grid, 256, lds, s>>>((const bf16_t *)packed_q, (const bf16_t *)packed_t, (bf16_t *)corr, Nq, Cp,
-                                            lay.row_stride, lay.row_stride, col_begin, col_end, nchunk, scale,
-                                            store_dtype == DVC_F32);
+        auto launch = [&](auto kern) {
+            (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            kern<<<grid, 256, lds, s>>>((const bf16_t *)packed_q, (const bf16_t *)packed_t, (bf16_t *)corr, Nq, Cp,
+                                        lay.row_stride, lay.row_stride, col_begin, col_end, nchunk, scale,
+                                        store_dtype == DVC_F32);
+        };
+        switch (Cp / 8) {
+        case 4: launch(k_build_bf16<4>); break;
+        case 8: launch(k_build_bf16<8>); break;
+        case 16: launch(k_build_bf16<16>); break;
+        case 32: launch(k_build_bf16<32>); break;
+        default: return fail(DVC_ERR_UNSUPPORTED, "build: C=%d not supported on the bf16 path", C);
+        }
     } else if (in_dtype == DVC_F32) {
         if (store_dtype != DVC_F32)
             return fail(DVC_ERR_UNSUPPORTED, "build: float32 inputs need a float32 store");
@@ -267,13 +274,25 @@ int dvc_corr_lookup(const void *corr, const float *coords, float *out, int B, in
         return fail(DVC_ERR_INVALID, "lookup: bad convention %d", convention);
     LookupArgs A;
     fill_lookup_args(A, lay, corr, coords, out, B, Nq, radius, convention);
+    if (store_dtype != DVC_BF16 && store_dtype != DVC_F32) return fail(DVC_ERR_INVALID, "lookup: bad dtype %d", store_dtype);
     const long long items = (long long)A.nl * A.nach * B * A.nqb;
     const unsigned blocks = (unsigned)ceil_div(items, 4);
     hipStream_t s = (hipStream_t)stream;
     if (store_dtype == DVC_BF16) launch_lookup<bf16_t>(A, blocks, s);
-    else if (store_dtype == DVC_F32) launch_lookup<float>(A, blocks, s);
-    else return fail(DVC_ERR_INVALID, "lookup: bad dtype %d", store_dtype);
-    return check_launch("corr_lookup");
+    else launch_lookup<float>(A, blocks, s);
+    if ((rc = check_launch("corr_lookup"))) return rc;
+    if (radius >= 1 && radius <= 6) {   // legacy levels with W != D: per-output kernel, one launch per level
+        for (int l = 0; l < lay.num_levels; ++l) {
+            if (!A.generic[l] || A.zero[l]) continue;
+            LookupArgs G = A;
+            G.l0 = l; G.nl = 1;
+            const unsigned gb = (unsigned)ceil_div((long long)G.nach * B * G.nqb, 4);
+            if (store_dtype == DVC_BF16) k_lookup_generic<bf16_t><<<gb, 256, 0, s>>>(G);
+            else k_lookup_generic<float><<<gb, 256, 0, s>>>(G);
+            if ((rc = check_launch("corr_lookup_generic"))) return rc;
+        }
+    }
+    return DVC_OK;
 }
 
 size_t dvc_lookup_fused_workspace_bytes(int B, int64_t Nq, int num_levels, int radius) {

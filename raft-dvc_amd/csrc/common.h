@@ -39,6 +39,7 @@ struct LookupArgs {
     long long Nq, q0, nq, nqb, row_stride;
     int B, Ltot, l0, nl, legacy, nach, ach, r;
     int H[DVC_MAX_LEVELS], W[DVC_MAX_LEVELS], D[DVC_MAX_LEVELS], Dp[DVC_MAX_LEVELS], zero[DVC_MAX_LEVELS];
+    int generic[DVC_MAX_LEVELS];   // level handled by a separate per-output launch (legacy, W != D)
     long long off[DVC_MAX_LEVELS];
 };
 

@@ -32,13 +32,15 @@ __host__ __device__ constexpr long long win_elems(int R) { return (long long)win
 
 template <typename T> struct Dot;
 template <> struct Dot<bf16_t> {
-    // 8 channels: one 16-byte chunk of each operand, v_dot2c_f32_bf16 x4
+    // 8 channels: one 16-byte chunk of each operand, unpacked to f32 and FMA'd
+    // (hipcc 7.2 miscompiles __builtin_amdgcn_fdot2_f32_bf16 on vector elements here:
+    // it re-used element 0 -- caught by tests/test_gpu_parity.py::test_bf16_build).
     static __device__ __forceinline__ float chunk(const u32x4 &a, const u32x4 &b, float acc) {
-        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, a[i]), __builtin_bit_cast(bf16x2, b[i]),
-                                                  acc, false);
+        for (int i = 0; i < 4; ++i) {
+            acc = __builtin_fmaf(__uint_as_float(a[i] << 16), __uint_as_float(b[i] << 16), acc);
+            acc = __builtin_fmaf(__uint_as_float(a[i] & 0xffff0000u), __uint_as_float(b[i] & 0xffff0000u), acc);
+        }
         return acc;
     }
     static constexpr int kPerChunk = 8;
@@ -207,6 +209,7 @@ int fused_lookup(const void *packed_q, const void *packed_t, const float *coords
     for (int l = 0; l < DVC_MAX_LEVELS; ++l) {
         A.H[l] = lay.H[l]; A.W[l] = lay.W[l]; A.D[l] = lay.D[l]; A.Dp[l] = lay.Dp[l];
         A.zero[l] = lay.zero_level[l]; A.off[l] = lay.offset[l];
+        A.generic[l] = 0;   // the fused path routes these levels to k_fused_generic itself
     }
     for (long long q0 = 0; q0 < Nq; q0 += kFusedChunk) {
         A.q0 = q0;

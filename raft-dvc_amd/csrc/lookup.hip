@@ -8,12 +8,17 @@
 // the pair of H-planes (a, a+1) row by row along the W axis and holds four
 // runs of 2r+2 values along the contiguous D axis in registers ("scatter form":
 // every output is a weighted sum of 8 window values; each window value is
-// loaded once per plane pair instead of once per output).  Runs are fetched as
-// aligned 16-byte chunks and shifted into place with v_cndmask/v_alignbyte.
+// loaded once per plane pair instead of once per output).  Runs are fetched with
+// hardware-unaligned 16-byte loads straight at the window start, and the next
+// column's runs are prefetched while the current one is interpolated.
 //
 // Sampling weights are the reference's float32 arithmetic per axis and offset
-// (normalise by (S-1), unnormalise, floor, corner weights; see common.h), and
-// the 8 weights are formed in grid_sample's product order.  Levels with a
+// (normalise by (S-1), unnormalise, floor, corner weights; see common.h).  The
+// trilinear sum is evaluated separably (z-lerp of each run, then the 4 bilinear
+// (y, x) weights): the same value as grid_sample's 8-term sum up to float32
+// rounding.  Zero padding is folded into the axis weights, so run loads never
+// branch: every load reads a clamped, valid address and out-of-range corners
+// get weight 0.  Levels with a
 // size-1 axis return 0 (the reference divides by S-1 = 0 there).  The legacy
 // convention (W<->D swapped grid channels) maps onto the same walk on levels
 // with W == D; other legacy levels take the generic per-output path.
@@ -26,56 +31,61 @@
 
 namespace dvc {
 
-// --- contiguous run loaders: v[j] = row[z0 + j], 0 outside [0, Dp) or if !ok -------------
+// --- contiguous run loaders: v[j] = row[j], j < NW, read with hardware-unaligned
+// 16-byte loads (gfx950 global loads accept any 2-byte-aligned address).  The
+// caller guarantees the NW elements are readable (clamped addresses + the
+// DVC_CORR_GUARD_BYTES guards); out-of-range elements are cancelled by zero weights.
 template <int NW>
-__device__ __forceinline__ void load_run(const bf16_t *row, bool ok, int z0, int Dp, float (&v)[NW]) {
-    constexpr int NCH = (7 + NW + 7) / 8;
-    const int za = z0 & ~7;
-    const int s = z0 - za;
-    unsigned w[4 * NCH];
+__device__ __forceinline__ void load_run(const bf16_t *row, float (&v)[NW]) {
+    constexpr int ND = NW / 2;            // NW is even: 2R+2
+    unsigned w[ND];
+    int i = 0;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-        const int zc = za + 8 * c;
-        u32x4 x = {0u, 0u, 0u, 0u};
-        if (ok && zc >= 0 && zc < Dp) x = *reinterpret_cast<const u32x4 *>(row + zc);
-        w[4 * c + 0] = x[0]; w[4 * c + 1] = x[1]; w[4 * c + 2] = x[2]; w[4 * c + 3] = x[3];
+    for (; i + 4 <= ND; i += 4) {
+        u32x4 x;
+        __builtin_memcpy(&x, row + 2 * i, 16);
+        w[i] = x[0]; w[i + 1] = x[1]; w[i + 2] = x[2]; w[i + 3] = x[3];
     }
-    // barrel shift by s>>1 words; masks instead of selects keep w[] in registers
-    // (a select between two array elements would become a dynamic index)
-    const unsigned m2 = 0u - (unsigned)((s >> 2) & 1), m1 = 0u - (unsigned)((s >> 1) & 1);
+    if constexpr (ND % 4 >= 2) {
+        u32x2 x;
+        __builtin_memcpy(&x, row + 2 * (ND & ~3), 8);
+        w[ND & ~3] = x[0]; w[(ND & ~3) + 1] = x[1];
+    }
+    if constexpr (ND % 2 == 1) {
+        unsigned x;
+        __builtin_memcpy(&x, row + 2 * (ND - 1), 4);
+        w[ND - 1] = x;
+    }
 #pragma unroll
-    for (int i = 0; i < 4 * NCH - 2; ++i) w[i] ^= (w[i] ^ w[i + 2]) & m2;
-#pragma unroll
-    for (int i = 0; i < 4 * NCH - 1; ++i) w[i] ^= (w[i] ^ w[i + 1]) & m1;
-    const unsigned bs = (unsigned)(s & 1) * 2u;
-#pragma unroll
-    for (int i = 0; i < (NW + 1) / 2; ++i) {
-        const unsigned o = __builtin_amdgcn_alignbyte(w[i + 1], w[i], bs);
-        v[2 * i] = __uint_as_float(o << 16);
-        if (2 * i + 1 < NW) v[2 * i + 1] = __uint_as_float(o & 0xffff0000u);
+    for (int j = 0; j < ND; ++j) {
+        v[2 * j] = __uint_as_float(w[j] << 16);
+        v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
     }
 }
 
 template <int NW>
-__device__ __forceinline__ void load_run(const float *row, bool ok, int z0, int Dp, float (&v)[NW]) {
-    constexpr int NCH = (3 + NW + 3) / 4;
-    const int za = z0 & ~3;
-    const int s = z0 - za;
-    unsigned w[4 * NCH];
+__device__ __forceinline__ void load_run(const float *row, float (&v)[NW]) {
+    int i = 0;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-        const int zc = za + 4 * c;
-        u32x4 x = {0u, 0u, 0u, 0u};
-        if (ok && zc >= 0 && zc < Dp) x = *reinterpret_cast<const u32x4 *>(row + zc);
-        w[4 * c + 0] = x[0]; w[4 * c + 1] = x[1]; w[4 * c + 2] = x[2]; w[4 * c + 3] = x[3];
+    for (; i + 4 <= NW; i += 4) {
+        u32x4 x;
+        __builtin_memcpy(&x, row + i, 16);
+        v[i] = __uint_as_float(x[0]); v[i + 1] = __uint_as_float(x[1]);
+        v[i + 2] = __uint_as_float(x[2]); v[i + 3] = __uint_as_float(x[3]);
     }
-    const unsigned m2 = 0u - (unsigned)((s >> 1) & 1), m1 = 0u - (unsigned)(s & 1);
+    if constexpr (NW % 4 >= 2) {
+        u32x2 x;
+        __builtin_memcpy(&x, row + (NW & ~3), 8);
+        v[NW & ~3] = __uint_as_float(x[0]); v[(NW & ~3) + 1] = __uint_as_float(x[1]);
+    }
+}
+
+// z-axis lerp of one run: zl[v] = R[v] * wz0[v] + R[v+1] * wz1[v]
+template <int NW>
+__device__ __forceinline__ void zlerp(const float (&r)[NW], const float (&w0)[NW - 1], const float (&w1)[NW - 1],
+                                      float (&zl)[NW - 1]) {
 #pragma unroll
-    for (int i = 0; i < 4 * NCH - 2; ++i) w[i] ^= (w[i] ^ w[i + 2]) & m2;
-#pragma unroll
-    for (int i = 0; i < 4 * NCH - 1; ++i) w[i] ^= (w[i] ^ w[i + 1]) & m1;
-#pragma unroll
-    for (int j = 0; j < NW; ++j) v[j] = __uint_as_float(w[j]);
+    for (int v = 0; v < NW - 1; ++v) zl[v] = __builtin_fmaf(r[v + 1], w1[v], r[v] * w0[v]);
 }
 
 // --- per-output path: any radius, any convention (also legacy non-cubic levels) ---------
@@ -147,18 +157,21 @@ __global__ __launch_bounds__(256) void k_lookup_win(LookupArgs A) {
     float cy = 0.f, cx = 0.f, cz = 0.f;
     if (active) load_coords(A.coords, it.b, Nq, q, cy, cx, cz);
     const float sc = (float)(1 << l);
-    if (!WINBUF && A.legacy && Wl != Dl) {   // wave-uniform; the fused path handles these itself
-        const T *lvl = reinterpret_cast<const T *>(A.corr) +
-                       ((long long)it.b * Nq + (active ? q : 0)) * A.row_stride + A.off[l];
-        lookup_generic<T>(lvl, Hl, Wl, Dl, Dpl, R, a0, a1, cy / sc, cx / sc, cz / sc, 1, active, outp, Nq);
-        return;
-    }
+    if (A.generic[l]) return;   // legacy level with W != D: k_lookup_generic covers it (wave-uniform)
     WinAxes ax;
     window_axes(cy / sc, cx / sc, cz / sc, Hl, Wl, Dl, A.legacy, ax);
+    const int ih = (int)ax.kh - R, iu = (int)ax.ku - R, iv = (int)ax.kv - R;
+    // D-axis weights with the zero padding folded in: a corner outside [0, Dl)
+    // gets weight 0, so the (finite) value loaded there never contributes.
     float wv0[n], wv1[n];
 #pragma unroll
-    for (int t = 0; t < n; ++t) axis_weights(ax.pv, ax.kv, t - R, ax.vn, ax.vu, wv0[t], wv1[t]);
-    const int ih = (int)ax.kh - R, iu = (int)ax.ku - R, iv = (int)ax.kv - R;
+    for (int t = 0; t < n; ++t) {
+        axis_weights(ax.pv, ax.kv, t - R, ax.vn, ax.vu, wv0[t], wv1[t]);
+        if (!WINBUF) {
+            wv0[t] = (unsigned)(iv + t) < (unsigned)Dl ? wv0[t] : 0.0f;
+            wv1[t] = (unsigned)(iv + t + 1) < (unsigned)Dl ? wv1[t] : 0.0f;
+        }
+    }
     const T *lvl;
     if (WINBUF)
         lvl = reinterpret_cast<const T *>(A.corr) + ((long long)it.b * A.nq + (active ? it.qi : 0)) * A.row_stride;
@@ -167,51 +180,72 @@ __global__ __launch_bounds__(256) void k_lookup_win(LookupArgs A) {
               A.off[l];
     const long long rs = WINBUF ? NWP : Dpl;                        // run (row) stride
     const long long ps = WINBUF ? NW * NWP : (long long)Wl * Dpl;   // plane stride
-    const int rz0 = WINBUF ? 0 : iv;
-    const int rdp = WINBUF ? NWP : Dpl;
-    const int xb = WINBUF ? 0 : iu;
+    // run start inside the row, clamped so every load stays inside [-NW, Dp + NW) of
+    // a real row (the guards cover the two ends of the buffer)
+    const int rz0 = WINBUF ? 0 : min(max(iv, -NW), Dpl);
     const long long chstep_u = A.legacy ? 1 : n;   // output-channel step per U (W-axis) offset
     const long long chstep_v = A.legacy ? n : 1;   // ... per V (D-axis) offset
     for (int a = a0; a < a1; ++a) {
         float wy0, wy1;
         axis_weights(ax.ph, ax.kh, a - R, ax.hs, ax.hs, wy0, wy1);
         const int y0 = ih + a;
-        const bool y0ok = WINBUF || (unsigned)y0 < (unsigned)Hl;
-        const bool y1ok = WINBUF || (unsigned)(y0 + 1) < (unsigned)Hl;
-        const T *r0 = lvl + (WINBUF ? (long long)a : (long long)y0) * ps;
-        const T *r1 = r0 + ps;
-        float A0[NW], B0[NW];
+        int yc0 = y0, yc1 = y0 + 1;
+        if (!WINBUF) {
+            wy0 = (unsigned)y0 < (unsigned)Hl ? wy0 : 0.0f;
+            wy1 = (unsigned)(y0 + 1) < (unsigned)Hl ? wy1 : 0.0f;
+            yc0 = min(max(y0, 0), Hl - 1);
+            yc1 = min(max(y0 + 1, 0), Hl - 1);
+        } else {
+            yc0 = a; yc1 = a + 1;
+        }
+        const T *r0 = lvl + (long long)yc0 * ps + rz0;
+        const T *r1 = lvl + (long long)yc1 * ps + rz0;
+        auto xrow = [&](int u) -> long long {   // clamped W-axis row of window column u
+            if (WINBUF) return (long long)u * rs;
+            return (long long)min(max(iu + u, 0), Wl - 1) * rs;
+        };
+        float zA0[n], zB0[n];
+        float nA[NW], nB[NW];
         {
-            const bool xok = WINBUF || (unsigned)iu < (unsigned)Wl;
-            load_run<NW>(r0 + (long long)xb * rs, y0ok && xok, rz0, rdp, A0);
-            load_run<NW>(r1 + (long long)xb * rs, y1ok && xok, rz0, rdp, B0);
+            float rA[NW], rB[NW];
+            load_run<NW>(r0 + xrow(0), rA);
+            load_run<NW>(r1 + xrow(0), rB);
+            load_run<NW>(r0 + xrow(1), nA);     // prefetch column 1
+            load_run<NW>(r1 + xrow(1), nB);
+            zlerp<NW>(rA, wv0, wv1, zA0);
+            zlerp<NW>(rB, wv0, wv1, zB0);
         }
         float *oa = outp + (long long)(a * n * n) * Nq;
 #pragma unroll 1
         for (int u = 0; u < n; ++u) {
-            float A1[NW], B1[NW];
-            const int x = xb + u + 1;
-            const bool xok = WINBUF || (unsigned)x < (unsigned)Wl;
-            load_run<NW>(r0 + (long long)x * rs, y0ok && xok, rz0, rdp, A1);
-            load_run<NW>(r1 + (long long)x * rs, y1ok && xok, rz0, rdp, B1);
+            float cA[NW], cB[NW];
+#pragma unroll
+            for (int j = 0; j < NW; ++j) { cA[j] = nA[j]; cB[j] = nB[j]; }
+            if (u + 2 <= n) {                   // prefetch column u + 2
+                load_run<NW>(r0 + xrow(u + 2), nA);
+                load_run<NW>(r1 + xrow(u + 2), nB);
+            }
+            float zA1[n], zB1[n];
+            zlerp<NW>(cA, wv0, wv1, zA1);
+            zlerp<NW>(cB, wv0, wv1, zB1);
             float wx0, wx1;
             axis_weights(ax.pu, ax.ku, u - R, ax.un, ax.uu, wx0, wx1);
+            if (!WINBUF) {
+                wx0 = (unsigned)(iu + u) < (unsigned)Wl ? wx0 : 0.0f;
+                wx1 = (unsigned)(iu + u + 1) < (unsigned)Wl ? wx1 : 0.0f;
+            }
             const float p00 = wx0 * wy0, p10 = wx1 * wy0, p01 = wx0 * wy1, p11 = wx1 * wy1;
             float *ou = oa + u * chstep_u * Nq;
 #pragma unroll
             for (int v = 0; v < n; ++v) {
-                float acc = A0[v] * (p00 * wv0[v]);                  // tnw
-                acc = __builtin_fmaf(A1[v], p10 * wv0[v], acc);      // tne
-                acc = __builtin_fmaf(B0[v], p01 * wv0[v], acc);      // tsw
-                acc = __builtin_fmaf(B1[v], p11 * wv0[v], acc);      // tse
-                acc = __builtin_fmaf(A0[v + 1], p00 * wv1[v], acc);  // bnw
-                acc = __builtin_fmaf(A1[v + 1], p10 * wv1[v], acc);  // bne
-                acc = __builtin_fmaf(B0[v + 1], p01 * wv1[v], acc);  // bsw
-                acc = __builtin_fmaf(B1[v + 1], p11 * wv1[v], acc);  // bse
+                float acc = p00 * zA0[v];
+                acc = __builtin_fmaf(p10, zA1[v], acc);
+                acc = __builtin_fmaf(p01, zB0[v], acc);
+                acc = __builtin_fmaf(p11, zB1[v], acc);
                 if (active) ou[v * chstep_v * Nq] = ax.dead ? 0.0f : acc;
             }
 #pragma unroll
-            for (int j = 0; j < NW; ++j) { A0[j] = A1[j]; B0[j] = B1[j]; }
+            for (int j = 0; j < n; ++j) { zA0[j] = zA1[j]; zB0[j] = zB1[j]; }
         }
     }
 }

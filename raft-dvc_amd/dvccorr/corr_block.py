@@ -79,7 +79,7 @@ class CorrBlock:
         if build == "gemm":       # every level from the pooled targets, one launch
             self._corr = ops.build(q, t, C, H, W, D, num_levels, self._dt, self._dt)
         elif build == "pool":     # the reference's op order: level 0 GEMM, then avg-pool the volume
-            corr = torch.empty((B, H * W * D, self._lay.row_stride), dtype=q.dtype, device=q.device)
+            corr = ops.alloc_corr(B, H * W * D, self._lay.row_stride, self._dt, q.device, zero=True)
             ops.build(q, t, C, H, W, D, num_levels, self._dt, self._dt, 0, self._lay.level_elems[0], out=corr)
             for l in range(num_levels - 1):
                 ops.pool(corr, H, W, D, num_levels, l, self._dt)

@@ -72,6 +72,21 @@ def pack_targets(fmap2: torch.Tensor, num_levels: int, dtype: int) -> torch.Tens
     return out
 
 
+GUARD_BYTES = 256   # DVC_CORR_GUARD_BYTES
+
+
+def alloc_corr(B: int, Nq: int, row_stride: int, store_dtype: int, device, zero: bool = False) -> torch.Tensor:
+    """(B, Nq, row_stride) corr buffer with zeroed DVC_CORR_GUARD_BYTES guards on both sides."""
+    dt = _TORCH_DT[store_dtype]
+    g = GUARD_BYTES // torch.tensor([], dtype=dt).element_size()
+    n = B * Nq * row_stride
+    buf = (torch.zeros if zero else torch.empty)((n + 2 * g,), dtype=dt, device=device)
+    if not zero:
+        buf[:g].zero_()
+        buf[g + n:].zero_()
+    return buf[g:g + n].view(B, Nq, row_stride)
+
+
 def build(packed_q: torch.Tensor, packed_t: torch.Tensor, C: int, H: int, W: int, D: int, num_levels: int,
           in_dtype: int, store_dtype: int, col_begin: int = 0, col_end=None, out: torch.Tensor = None) -> torch.Tensor:
     _need_cuda(packed_q, packed_t)
@@ -79,7 +94,7 @@ def build(packed_q: torch.Tensor, packed_t: torch.Tensor, C: int, H: int, W: int
     lay = layout(H, W, D, num_levels, C)
     col_end = lay.row_stride if col_end is None else col_end
     if out is None:
-        out = torch.empty((B, Nq, lay.row_stride), dtype=_TORCH_DT[store_dtype], device=packed_q.device)
+        out = alloc_corr(B, Nq, lay.row_stride, store_dtype, packed_q.device)
     check(lib().dvc_corr_build(_ptr(packed_q), _ptr(packed_t), _ptr(out), B, Nq, C, H, W, D, num_levels, in_dtype,
                                store_dtype, col_begin, col_end, _stream(packed_q)), "corr_build")
     return out
