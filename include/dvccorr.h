@@ -126,6 +126,10 @@ int dvc_corr_lookup_fused(const void *packed_q, const void *packed_t, const floa
 int dvc_sample3d(const float *vol, const float *pts, float *out, int B, int C, int Hv, int Wv, int Dv, int64_t Nq,
                  int convention, void *stream);
 
+/* Kernel-variant knob for A/B timing (process-wide, not thread-safe):
+ *   "lookup_variant" 0 = unaligned 16-byte run loads, 1 = aligned chunks + v_perm shifter. */
+int dvc_set_tuning(const char *key, int value);
+
 const char *dvc_last_error(void);
 const char *dvc_version(void);
 int dvc_abi_version(void);

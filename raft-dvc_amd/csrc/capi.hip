@@ -7,6 +7,7 @@
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "common.h"
@@ -22,7 +23,7 @@ __global__ void k_build_f32(const float *, const float *, float *, long long, in
                             long long, int, float);
 template <typename T>
 __global__ void k_corr_pool(T *, long long, long long, long long, int, int, long long, int, int, int, int);
-template <typename T, int R, bool WINBUF> __global__ void k_lookup_win(LookupArgs);
+template <typename T, int R, bool WINBUF, bool ALIGNED> __global__ void k_lookup_win(LookupArgs);
 template <typename T> __global__ void k_lookup_generic(LookupArgs);
 __global__ void k_sample3d(const float *, const float *, float *, int, int, int, int, int, long long, int);
 int fused_lookup(const void *packed_q, const void *packed_t, const float *coords, float *out, void *workspace, int B,
@@ -69,22 +70,49 @@ static int fill_lookup_args(LookupArgs &A, const dvc_layout &lay, const void *co
     return DVC_OK;
 }
 
-template <typename T>
-static void launch_lookup(const LookupArgs &A, unsigned blocks, hipStream_t s) {
+// Lookup kernel variant: 0 = unaligned 16-byte run loads (default), 1 = aligned
+// chunks + v_perm shifter.  DVCCORR_LOOKUP_VARIANT overrides (read once, for A/B timing).
+static int g_lookup_variant = -1;
+static int lookup_variant() {
+    if (g_lookup_variant < 0) {
+        const char *e = getenv("DVCCORR_LOOKUP_VARIANT");
+        g_lookup_variant = e ? atoi(e) : 0;
+    }
+    return g_lookup_variant;
+}
+
+template <typename T, bool AL>
+static void launch_lookup_v(const LookupArgs &A, unsigned blocks, hipStream_t s) {
     switch (A.r) {
-    case 1: k_lookup_win<T, 1, false><<<blocks, 256, 0, s>>>(A); break;
-    case 2: k_lookup_win<T, 2, false><<<blocks, 256, 0, s>>>(A); break;
-    case 3: k_lookup_win<T, 3, false><<<blocks, 256, 0, s>>>(A); break;
-    case 4: k_lookup_win<T, 4, false><<<blocks, 256, 0, s>>>(A); break;
-    case 5: k_lookup_win<T, 5, false><<<blocks, 256, 0, s>>>(A); break;
-    case 6: k_lookup_win<T, 6, false><<<blocks, 256, 0, s>>>(A); break;
+    case 1: k_lookup_win<T, 1, false, AL><<<blocks, 256, 0, s>>>(A); break;
+    case 2: k_lookup_win<T, 2, false, AL><<<blocks, 256, 0, s>>>(A); break;
+    case 3: k_lookup_win<T, 3, false, AL><<<blocks, 256, 0, s>>>(A); break;
+    case 4: k_lookup_win<T, 4, false, AL><<<blocks, 256, 0, s>>>(A); break;
+    case 5: k_lookup_win<T, 5, false, AL><<<blocks, 256, 0, s>>>(A); break;
+    case 6: k_lookup_win<T, 6, false, AL><<<blocks, 256, 0, s>>>(A); break;
     default: k_lookup_generic<T><<<blocks, 256, 0, s>>>(A); break;
     }
+}
+
+template <typename T>
+static void launch_lookup(const LookupArgs &A, unsigned blocks, hipStream_t s) {
+    if (lookup_variant() == 1) launch_lookup_v<T, true>(A, blocks, s);
+    else launch_lookup_v<T, false>(A, blocks, s);
 }
 
 extern "C" {
 
 const char *dvc_last_error(void) { return g_err; }
+
+int dvc_set_tuning(const char *key, int value) {
+    if (!key) return fail(DVC_ERR_INVALID, "set_tuning: null key");
+    if (!strcmp(key, "lookup_variant")) {
+        if (value < 0 || value > 1) return fail(DVC_ERR_INVALID, "set_tuning: lookup_variant %d", value);
+        g_lookup_variant = value;
+        return DVC_OK;
+    }
+    return fail(DVC_ERR_INVALID, "set_tuning: unknown key '%s'", key);
+}
 const char *dvc_version(void) { return "dvccorr 0.1.0 (gfx950)"; }
 int dvc_abi_version(void) { return DVC_ABI_VERSION; }
 

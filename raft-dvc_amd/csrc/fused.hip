@@ -22,7 +22,7 @@
 
 namespace dvc {
 
-template <typename T, int R, bool WINBUF> __global__ void k_lookup_win(LookupArgs);
+template <typename T, int R, bool WINBUF, bool ALIGNED> __global__ void k_lookup_win(LookupArgs);
 
 constexpr long long kFusedChunk = 65536;   // queries per window-buffer chunk
 
@@ -168,7 +168,7 @@ static int fused_level_win(const T *Q, const T *Tt, LookupArgs &A, float *ws, in
     A.corr = ws;
     A.row_stride = win_elems(R);
     const long long items = (long long)A.nach * A.B * A.nqb;
-    k_lookup_win<float, R, true><<<(unsigned)((items + 3) / 4), 256, 0, s>>>(A);
+    k_lookup_win<float, R, true, false><<<(unsigned)((items + 3) / 4), 256, 0, s>>>(A);
     return 0;
 }
 

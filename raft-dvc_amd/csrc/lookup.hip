@@ -80,6 +80,61 @@ __device__ __forceinline__ void load_run(const float *row, float (&v)[NW]) {
     }
 }
 
+// Aligned variant: the run [z0, z0 + NW) is fetched as aligned 16-byte chunks
+// covering it and shifted into place with v_perm / v_alignbyte (1 op per word per
+// stage, no data-dependent array index).
+__device__ __forceinline__ unsigned sel_word(unsigned hi, unsigned lo, unsigned sel) {
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+template <int NW>
+__device__ __forceinline__ void load_run_al(const bf16_t *row, int z0, float (&v)[NW]) {
+    constexpr int NCH = (7 + NW + 7) / 8;
+    const int za = z0 & ~7;
+    const unsigned s = (unsigned)(z0 - za);
+    unsigned w[4 * NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const u32x4 x = *reinterpret_cast<const u32x4 *>(row + za + 8 * c);
+        w[4 * c + 0] = x[0]; w[4 * c + 1] = x[1]; w[4 * c + 2] = x[2]; w[4 * c + 3] = x[3];
+    }
+    const unsigned sA = (s & 4) ? 0x07060504u : 0x03020100u;
+    const unsigned sB = (s & 2) ? 0x07060504u : 0x03020100u;
+    constexpr int ND = NW / 2;
+#pragma unroll
+    for (int i = 0; i < ND + 2; ++i) w[i] = sel_word(w[i + 2], w[i], sA);
+#pragma unroll
+    for (int i = 0; i < ND + 1; ++i) w[i] = sel_word(w[i + 1], w[i], sB);
+    const unsigned bs = (s & 1) * 2u;
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+        const unsigned o = __builtin_amdgcn_alignbyte(w[j + 1], w[j], bs);
+        v[2 * j] = __uint_as_float(o << 16);
+        v[2 * j + 1] = __uint_as_float(o & 0xffff0000u);
+    }
+}
+
+template <int NW>
+__device__ __forceinline__ void load_run_al(const float *row, int z0, float (&v)[NW]) {
+    constexpr int NCH = (3 + NW + 3) / 4;
+    const int za = z0 & ~3;
+    const unsigned s = (unsigned)(z0 - za);
+    unsigned w[4 * NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const u32x4 x = *reinterpret_cast<const u32x4 *>(row + za + 4 * c);
+        w[4 * c + 0] = x[0]; w[4 * c + 1] = x[1]; w[4 * c + 2] = x[2]; w[4 * c + 3] = x[3];
+    }
+    const unsigned sA = (s & 2) ? 0x07060504u : 0x03020100u;
+    const unsigned sB = (s & 1) ? 0x07060504u : 0x03020100u;
+#pragma unroll
+    for (int i = 0; i < NW + 1; ++i) w[i] = sel_word(w[i + 2], w[i], sA);
+#pragma unroll
+    for (int i = 0; i < NW; ++i) w[i] = sel_word(w[i + 1], w[i], sB);
+#pragma unroll
+    for (int j = 0; j < NW; ++j) v[j] = __uint_as_float(w[j]);
+}
+
 // z-axis lerp of one run: zl[v] = R[v] * wz0[v] + R[v+1] * wz1[v]
 template <int NW>
 __device__ __forceinline__ void zlerp(const float (&r)[NW], const float (&w0)[NW - 1], const float (&w1)[NW - 1],
@@ -136,7 +191,7 @@ __global__ __launch_bounds__(256) void k_lookup_generic(LookupArgs A) {
                       outp, Nq);
 }
 
-template <typename T, int R, bool WINBUF>
+template <typename T, int R, bool WINBUF, bool ALIGNED>
 __global__ __launch_bounds__(256) void k_lookup_win(LookupArgs A) {
     constexpr int n = 2 * R + 1, NW = 2 * R + 2, NWP = (NW + 3) & ~3;
     constexpr long long n3 = (long long)n * n * n;
@@ -198,8 +253,12 @@ __global__ __launch_bounds__(256) void k_lookup_win(LookupArgs A) {
         } else {
             yc0 = a; yc1 = a + 1;
         }
-        const T *r0 = lvl + (long long)yc0 * ps + rz0;
-        const T *r1 = lvl + (long long)yc1 * ps + rz0;
+        const T *r0 = lvl + (long long)yc0 * ps + (ALIGNED ? 0 : rz0);
+        const T *r1 = lvl + (long long)yc1 * ps + (ALIGNED ? 0 : rz0);
+        auto run = [&](const T *p, float (&dst)[NW]) {
+            if constexpr (ALIGNED) load_run_al<NW>(p, rz0, dst);
+            else load_run<NW>(p, dst);
+        };
         auto xrow = [&](int u) -> long long {   // clamped W-axis row of window column u
             if (WINBUF) return (long long)u * rs;
             return (long long)min(max(iu + u, 0), Wl - 1) * rs;
@@ -208,10 +267,10 @@ __global__ __launch_bounds__(256) void k_lookup_win(LookupArgs A) {
         float nA[NW], nB[NW];
         {
             float rA[NW], rB[NW];
-            load_run<NW>(r0 + xrow(0), rA);
-            load_run<NW>(r1 + xrow(0), rB);
-            load_run<NW>(r0 + xrow(1), nA);     // prefetch column 1
-            load_run<NW>(r1 + xrow(1), nB);
+            run(r0 + xrow(0), rA);
+            run(r1 + xrow(0), rB);
+            run(r0 + xrow(1), nA);     // prefetch column 1
+            run(r1 + xrow(1), nB);
             zlerp<NW>(rA, wv0, wv1, zA0);
             zlerp<NW>(rB, wv0, wv1, zB0);
         }
@@ -222,8 +281,8 @@ __global__ __launch_bounds__(256) void k_lookup_win(LookupArgs A) {
 #pragma unroll
             for (int j = 0; j < NW; ++j) { cA[j] = nA[j]; cB[j] = nB[j]; }
             if (u + 2 <= n) {                   // prefetch column u + 2
-                load_run<NW>(r0 + xrow(u + 2), nA);
-                load_run<NW>(r1 + xrow(u + 2), nB);
+                run(r0 + xrow(u + 2), nA);
+                run(r1 + xrow(u + 2), nB);
             }
             float zA1[n], zB1[n];
             zlerp<NW>(cA, wv0, wv1, zA1);
@@ -250,18 +309,19 @@ __global__ __launch_bounds__(256) void k_lookup_win(LookupArgs A) {
     }
 }
 
-#define DVC_LOOKUP_INST(T, R)                                            \
-    template __global__ void k_lookup_win<T, R, false>(LookupArgs);
+#define DVC_LOOKUP_INST(T, R)                                              \
+    template __global__ void k_lookup_win<T, R, false, false>(LookupArgs); \
+    template __global__ void k_lookup_win<T, R, false, true>(LookupArgs);
 DVC_LOOKUP_INST(float, 1) DVC_LOOKUP_INST(float, 2) DVC_LOOKUP_INST(float, 3)
 DVC_LOOKUP_INST(float, 4) DVC_LOOKUP_INST(float, 5) DVC_LOOKUP_INST(float, 6)
 DVC_LOOKUP_INST(bf16_t, 1) DVC_LOOKUP_INST(bf16_t, 2) DVC_LOOKUP_INST(bf16_t, 3)
 DVC_LOOKUP_INST(bf16_t, 4) DVC_LOOKUP_INST(bf16_t, 5) DVC_LOOKUP_INST(bf16_t, 6)
-template __global__ void k_lookup_win<float, 1, true>(LookupArgs);
-template __global__ void k_lookup_win<float, 2, true>(LookupArgs);
-template __global__ void k_lookup_win<float, 3, true>(LookupArgs);
-template __global__ void k_lookup_win<float, 4, true>(LookupArgs);
-template __global__ void k_lookup_win<float, 5, true>(LookupArgs);
-template __global__ void k_lookup_win<float, 6, true>(LookupArgs);
+template __global__ void k_lookup_win<float, 1, true, false>(LookupArgs);
+template __global__ void k_lookup_win<float, 2, true, false>(LookupArgs);
+template __global__ void k_lookup_win<float, 3, true, false>(LookupArgs);
+template __global__ void k_lookup_win<float, 4, true, false>(LookupArgs);
+template __global__ void k_lookup_win<float, 5, true, false>(LookupArgs);
+template __global__ void k_lookup_win<float, 6, true, false>(LookupArgs);
 template __global__ void k_lookup_generic<float>(LookupArgs);
 template __global__ void k_lookup_generic<bf16_t>(LookupArgs);
 

@@ -22,7 +22,7 @@ MAX_LEVELS = 8
 EXPORTED = (
     "dvc_layout_init", "dvc_pack_workspace_bytes", "dvc_pack_queries", "dvc_pack_targets", "dvc_corr_build",
     "dvc_corr_pool", "dvc_corr_lookup", "dvc_lookup_fused_workspace_bytes", "dvc_corr_lookup_fused",
-    "dvc_sample3d", "dvc_last_error", "dvc_version", "dvc_abi_version",
+    "dvc_sample3d", "dvc_set_tuning", "dvc_last_error", "dvc_version", "dvc_abi_version",
 )
 
 
@@ -74,6 +74,7 @@ def lib() -> ctypes.CDLL:
         "dvc_lookup_fused_workspace_bytes": (sz, [i32, i64, i32, i32]),
         "dvc_corr_lookup_fused": (i32, [vp, vp, vp, vp, vp, i32, i64, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
         "dvc_sample3d": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i64, i32, vp]),
+        "dvc_set_tuning": (i32, [ctypes.c_char_p, i32]),
         "dvc_last_error": (ctypes.c_char_p, []),
         "dvc_version": (ctypes.c_char_p, []),
         "dvc_abi_version": (i32, []),
@@ -97,6 +98,10 @@ def check(rc: int, what: str = "") -> None:
     if rc == DVC_ERR_UNSUPPORTED:
         raise NotImplementedError(msg)
     raise DvcError(msg)
+
+
+def set_tuning(key: str, value: int) -> None:
+    check(lib().dvc_set_tuning(key.encode(), int(value)), "set_tuning")
 
 
 def layout(H: int, W: int, D: int, num_levels: int, C: int = 1) -> Layout:

@@ -234,3 +234,23 @@ def test_determinism_and_linearity_at_cfg3():
     # the fused path agrees with the materialised one at the bench size
     fz = dvccorr.CorrBlockFused(f1, f2, 4, 4, precision="bf16")(c)
     assert orc.rel_err(fz.cpu().numpy(), a.cpu().numpy()) <= BF16_TOL
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_lookup_variants(variant):
+    """Both lookup load strategies (unaligned runs / aligned chunks + v_perm) reproduce the golden rows."""
+    import dvccorr
+    from dvccorr import _lib
+    _lib.set_tuning("lookup_variant", variant)
+    try:
+        for case, prec, tol in (("edge_978_L3_r3", "fp32", FP32_TOL), ("edge_965_L2_r4", "fp32", FP32_TOL),
+                                ("cfg2", "fp32", FP32_TOL), ("cfg2", "bf16", BF16_TOL)):
+            g = load_golden(case + ".npz")
+            f1, f2, coords, L, r = corr_inputs(g)
+            t1, t2, tc = _gpu(f1, f2, coords)
+            for legacy, tag in ((False, "fixed"), (True, "legacy")):
+                out = dvccorr.CorrBlock(t1, t2, L, r, legacy_wd_swap=legacy, precision=prec)(tc)
+                e = orc.rel_err(_rows(out, g["rows"]), g[f"out_rows_{tag}"])
+                assert e <= tol, (variant, case, prec, tag, e)
+    finally:
+        _lib.set_tuning("lookup_variant", 0)

@@ -1,0 +1,35 @@
+#!/usr/bin/env python3
+"""Minimal workload for rocprofv3 counter passes: one build + `reps` lookups."""
+import argparse
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "raft-dvc_amd"))
+import dvccorr  # noqa: E402
+from dvccorr import _lib  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--size", type=int, default=32)
+ap.add_argument("--levels", type=int, default=4)
+ap.add_argument("--precision", default="bf16")
+ap.add_argument("--reps", type=int, default=4)
+ap.add_argument("--variant", type=int, default=0)
+ap.add_argument("--impl", default="materialised")
+a = ap.parse_args()
+_lib.set_tuning("lookup_variant", a.variant)
+dev = torch.device("cuda:0")
+S = a.size
+g = torch.Generator(device="cpu").manual_seed(7)
+f1 = torch.randn(1, 128, S, S, S, generator=g).to(dev)
+f2 = torch.randn(1, 128, S, S, S, generator=g).to(dev)
+c = (dvccorr.coords_grid_3d(1, S, S, S, torch.device("cpu")) + (torch.rand(1, 3, S, S, S, generator=g) * 4 - 2)).to(dev)
+with torch.no_grad():
+    cls = dvccorr.CorrBlock if a.impl == "materialised" else dvccorr.CorrBlockFused
+    blk = cls(f1, f2, a.levels, 4, precision=a.precision)
+    for _ in range(a.reps):
+        out = blk(c)
+torch.cuda.synchronize()
+print("ok", float(out.abs().sum()))
