@@ -298,6 +298,8 @@ int dvc_corr_lookup(const void *corr, const float *coords, float *out, int B, in
     if (!corr || !coords || !out) return fail(DVC_ERR_INVALID, "lookup: null pointer");
     if (B < 1 || Nq < 1) return fail(DVC_ERR_INVALID, "lookup: B=%d Nq=%lld", B, (long long)Nq);
     if (radius < 0 || radius > 16) return fail(DVC_ERR_INVALID, "lookup: radius %d outside [0, 16]", radius);
+    if ((long long)Nq * (2 * radius + 1) * (2 * radius + 1) * 4 >= (1LL << 31))
+        return fail(DVC_ERR_UNSUPPORTED, "lookup: Nq=%lld too large for 32-bit output offsets", (long long)Nq);
     if (convention != DVC_FIXED && convention != DVC_LEGACY)
         return fail(DVC_ERR_INVALID, "lookup: bad convention %d", convention);
     LookupArgs A;

@@ -194,6 +194,10 @@ int fused_lookup(const void *packed_q, const void *packed_t, const float *coords
         return DVC_ERR_UNSUPPORTED;
     }
     const bool win_ok = radius >= 1 && radius <= 6;
+    if ((long long)Nq * (2 * radius + 1) * (2 * radius + 1) * 4 >= (1LL << 31)) {
+        snprintf(err, errlen, "lookup_fused: Nq=%lld too large for 32-bit output offsets", Nq);
+        return DVC_ERR_UNSUPPORTED;
+    }
     if (win_ok && !workspace) {
         snprintf(err, errlen, "lookup_fused: workspace required (%zu bytes)", fused_workspace_bytes(B, Nq, 0, radius));
         return DVC_ERR_INVALID;

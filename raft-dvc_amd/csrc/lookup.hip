@@ -135,6 +135,70 @@ __device__ __forceinline__ void load_run_al(const float *row, int z0, float (&v)
     for (int j = 0; j < NW; ++j) v[j] = __uint_as_float(w[j]);
 }
 
+// Raw run containers: the prefetched runs stay packed (bf16: NW/2 dwords) until the
+// z-lerp consumes them, halving the registers the prefetch needs.
+template <typename T, int NW> struct Raw;
+template <int NW> struct Raw<bf16_t, NW> {
+    static constexpr int K = NW / 2;
+    unsigned w[K];
+    __device__ __forceinline__ void load(const bf16_t *row) {
+        int i = 0;
+#pragma unroll
+        for (; i + 4 <= K; i += 4) {
+            u32x4 x;
+            __builtin_memcpy(&x, row + 2 * i, 16);
+            w[i] = x[0]; w[i + 1] = x[1]; w[i + 2] = x[2]; w[i + 3] = x[3];
+        }
+        if constexpr (K % 4 >= 2) {
+            u32x2 x;
+            __builtin_memcpy(&x, row + 2 * (K & ~3), 8);
+            w[K & ~3] = x[0]; w[(K & ~3) + 1] = x[1];
+        }
+        if constexpr (K % 2 == 1) {
+            unsigned x;
+            __builtin_memcpy(&x, row + 2 * (K - 1), 4);
+            w[K - 1] = x;
+        }
+    }
+    __device__ __forceinline__ void load_al(const bf16_t *row, int z0) {
+        constexpr int NCH = (7 + NW + 7) / 8;
+        const int za = z0 & ~7;
+        const unsigned s = (unsigned)(z0 - za);
+        unsigned t[4 * NCH];
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const u32x4 x = *reinterpret_cast<const u32x4 *>(row + za + 8 * c);
+            t[4 * c + 0] = x[0]; t[4 * c + 1] = x[1]; t[4 * c + 2] = x[2]; t[4 * c + 3] = x[3];
+        }
+        const unsigned sA = (s & 4) ? 0x07060504u : 0x03020100u;
+        const unsigned sB = (s & 2) ? 0x07060504u : 0x03020100u;
+#pragma unroll
+        for (int i = 0; i < K + 2; ++i) t[i] = sel_word(t[i + 2], t[i], sA);
+#pragma unroll
+        for (int i = 0; i < K + 1; ++i) t[i] = sel_word(t[i + 1], t[i], sB);
+        const unsigned bs = (s & 1) * 2u;
+#pragma unroll
+        for (int j = 0; j < K; ++j) w[j] = __builtin_amdgcn_alignbyte(t[j + 1], t[j], bs);
+    }
+    __device__ __forceinline__ float get(int j) const {
+        return (j & 1) ? __uint_as_float(w[j >> 1] & 0xffff0000u) : __uint_as_float(w[j >> 1] << 16);
+    }
+};
+template <int NW> struct Raw<float, NW> {
+    float w[NW];
+    __device__ __forceinline__ void load(const float *row) { load_run<NW>(row, w); }
+    __device__ __forceinline__ void load_al(const float *row, int z0) { load_run_al<NW>(row, z0, w); }
+    __device__ __forceinline__ float get(int j) const { return w[j]; }
+};
+
+// z-axis lerp of a raw run: zl[v] = R[v] * wz0[v] + R[v+1] * wz1[v]
+template <typename T, int NW>
+__device__ __forceinline__ void zlerp_raw(const Raw<T, NW> &r, const float (&w0)[NW - 1], const float (&w1)[NW - 1],
+                                          float (&zl)[NW - 1]) {
+#pragma unroll
+    for (int v = 0; v < NW - 1; ++v) zl[v] = __builtin_fmaf(r.get(v + 1), w1[v], r.get(v) * w0[v]);
+}
+
 // z-axis lerp of one run: zl[v] = R[v] * wz0[v] + R[v+1] * wz1[v]
 template <int NW>
 __device__ __forceinline__ void zlerp(const float (&r)[NW], const float (&w0)[NW - 1], const float (&w1)[NW - 1],
@@ -238,73 +302,111 @@ __global__ __launch_bounds__(256) void k_lookup_win(LookupArgs A) {
     // run start inside the row, clamped so every load stays inside [-NW, Dp + NW) of
     // a real row (the guards cover the two ends of the buffer)
     const int rz0 = WINBUF ? 0 : min(max(iv, -NW), Dpl);
-    const long long chstep_u = A.legacy ? 1 : n;   // output-channel step per U (W-axis) offset
-    const long long chstep_v = A.legacy ? n : 1;   // ... per V (D-axis) offset
-    for (int a = a0; a < a1; ++a) {
-        float wy0, wy1;
-        axis_weights(ax.ph, ax.kh, a - R, ax.hs, ax.hs, wy0, wy1);
-        const int y0 = ih + a;
-        int yc0 = y0, yc1 = y0 + 1;
+    const int chstep_u = A.legacy ? 1 : n;   // output-channel step per U (W-axis) offset
+    const int chstep_v = A.legacy ? n : 1;   // ... per V (D-axis) offset
+    float *obase = A.out + ((long long)it.b * A.Ltot + l) * n3 * Nq;   // wave-uniform
+    const int q4 = (int)((active ? q : 0) * 4);
+    // H-planes of this a-chunk: window planes a0 .. a1 (np = a1 - a0 + 1 <= ACH + 1).
+    // Column-outer walk: every run (plane, column) is loaded once per wave; the
+    // z-lerped runs of the previous column are kept for all planes of the chunk.
+    constexpr int ACH = 3, NP = ACH + 1;
+    const int np = a1 - a0 + 1;
+    float wy0[ACH], wy1[ACH];
+    const T *pl[NP];
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+        const int a = min(a0 + i, n - 1);
+        axis_weights(ax.ph, ax.kh, a - R, ax.hs, ax.hs, wy0[i], wy1[i]);
         if (!WINBUF) {
-            wy0 = (unsigned)y0 < (unsigned)Hl ? wy0 : 0.0f;
-            wy1 = (unsigned)(y0 + 1) < (unsigned)Hl ? wy1 : 0.0f;
-            yc0 = min(max(y0, 0), Hl - 1);
-            yc1 = min(max(y0 + 1, 0), Hl - 1);
-        } else {
-            yc0 = a; yc1 = a + 1;
+            wy0[i] = (unsigned)(ih + a) < (unsigned)Hl ? wy0[i] : 0.0f;
+            wy1[i] = (unsigned)(ih + a + 1) < (unsigned)Hl ? wy1[i] : 0.0f;
         }
-        const T *r0 = lvl + (long long)yc0 * ps + (ALIGNED ? 0 : rz0);
-        const T *r1 = lvl + (long long)yc1 * ps + (ALIGNED ? 0 : rz0);
-        auto run = [&](const T *p, float (&dst)[NW]) {
-            if constexpr (ALIGNED) load_run_al<NW>(p, rz0, dst);
-            else load_run<NW>(p, dst);
-        };
-        auto xrow = [&](int u) -> long long {   // clamped W-axis row of window column u
-            if (WINBUF) return (long long)u * rs;
-            return (long long)min(max(iu + u, 0), Wl - 1) * rs;
-        };
-        float zA0[n], zB0[n];
-        float nA[NW], nB[NW];
-        {
-            float rA[NW], rB[NW];
-            run(r0 + xrow(0), rA);
-            run(r1 + xrow(0), rB);
-            run(r0 + xrow(1), nA);     // prefetch column 1
-            run(r1 + xrow(1), nB);
-            zlerp<NW>(rA, wv0, wv1, zA0);
-            zlerp<NW>(rB, wv0, wv1, zB0);
+    }
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        const int wp = min(a0 + i, n);   // window plane index (0 .. 2R+1)
+        const int y = WINBUF ? wp : min(max(ih + wp, 0), Hl - 1);
+        pl[i] = lvl + (long long)y * ps + (ALIGNED ? 0 : rz0);
+    }
+    auto col = [&](int u) -> long long {   // clamped W-axis row of window column u
+        if (WINBUF) return (long long)u * rs;
+        return (long long)min(max(iu + u, 0), Wl - 1) * rs;
+    };
+    auto run = [&](const T *p, Raw<T, NW> &dst) {
+        if constexpr (ALIGNED) dst.load_al(p, rz0);
+        else dst.load(p);
+    };
+    float zp[NP][n];          // z-lerped runs of the previous column, per plane
+    Raw<T, NW> nx[NP];        // prefetched runs of the next column (packed)
+    {
+        const long long c0 = col(0);
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+            if (i < np) {
+                Raw<T, NW> r;
+                run(pl[i] + c0, r);
+                zlerp_raw<T, NW>(r, wv0, wv1, zp[i]);
+            }
         }
-        float *oa = outp + (long long)(a * n * n) * Nq;
+        const long long c1 = col(1);
+#pragma unroll
+        for (int i = 0; i < NP; ++i)
+            if (i < np) run(pl[i] + c1, nx[i]);
+    }
 #pragma unroll 1
-        for (int u = 0; u < n; ++u) {
-            float cA[NW], cB[NW];
+    for (int u = 0; u < n; ++u) {
+        Raw<T, NW> cur[NP];
 #pragma unroll
-            for (int j = 0; j < NW; ++j) { cA[j] = nA[j]; cB[j] = nB[j]; }
-            if (u + 2 <= n) {                   // prefetch column u + 2
-                run(r0 + xrow(u + 2), nA);
-                run(r1 + xrow(u + 2), nB);
-            }
-            float zA1[n], zB1[n];
-            zlerp<NW>(cA, wv0, wv1, zA1);
-            zlerp<NW>(cB, wv0, wv1, zB1);
-            float wx0, wx1;
-            axis_weights(ax.pu, ax.ku, u - R, ax.un, ax.uu, wx0, wx1);
-            if (!WINBUF) {
-                wx0 = (unsigned)(iu + u) < (unsigned)Wl ? wx0 : 0.0f;
-                wx1 = (unsigned)(iu + u + 1) < (unsigned)Wl ? wx1 : 0.0f;
-            }
-            const float p00 = wx0 * wy0, p10 = wx1 * wy0, p01 = wx0 * wy1, p11 = wx1 * wy1;
-            float *ou = oa + u * chstep_u * Nq;
+        for (int i = 0; i < NP; ++i) cur[i] = nx[i];
+        if (u + 2 <= n) {                       // prefetch column u + 2
+            const long long cn = col(u + 2);
 #pragma unroll
-            for (int v = 0; v < n; ++v) {
-                float acc = p00 * zA0[v];
-                acc = __builtin_fmaf(p10, zA1[v], acc);
-                acc = __builtin_fmaf(p01, zB0[v], acc);
-                acc = __builtin_fmaf(p11, zB1[v], acc);
-                if (active) ou[v * chstep_v * Nq] = ax.dead ? 0.0f : acc;
-            }
+            for (int i = 0; i < NP; ++i)
+                if (i < np) run(pl[i] + cn, nx[i]);
+        }
+        float wx0, wx1;
+        axis_weights(ax.pu, ax.ku, u - R, ax.un, ax.uu, wx0, wx1);
+        if (!WINBUF) {
+            wx0 = (unsigned)(iu + u) < (unsigned)Wl ? wx0 : 0.0f;
+            wx1 = (unsigned)(iu + u + 1) < (unsigned)Wl ? wx1 : 0.0f;
+        }
+        // planes in order: once plane i's current column is lerped, output row
+        // a0 + i - 1 (planes i-1, i) is complete and plane i-1's previous column retires
+        float zc_prev[n];
 #pragma unroll
-            for (int j = 0; j < n; ++j) { zA0[j] = zA1[j]; zB0[j] = zB1[j]; }
+        for (int i = 0; i < NP; ++i) {
+            if (i < np) {
+                float zc[n];
+                zlerp_raw<T, NW>(cur[i], wv0, wv1, zc);
+                if (i >= 1) {
+                    const int a = a0 + i - 1;
+                    const float p00 = wx0 * wy0[i - 1], p10 = wx1 * wy0[i - 1];
+                    const float p01 = wx0 * wy1[i - 1], p11 = wx1 * wy1[i - 1];
+                    // buffer stores: scalar descriptor per output row a, scalar channel
+                    // offset, one 32-bit per-lane offset (q * 4)
+                    const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(
+                        obase + (long long)a * n * n * Nq, (short)0, (int)(n * n * Nq * 4), 0x00020000);
+#pragma unroll
+                    for (int v = 0; v < n; ++v) {
+                        float acc = p00 * zp[i - 1][v];
+                        acc = __builtin_fmaf(p10, zc_prev[v], acc);
+                        acc = __builtin_fmaf(p01, zp[i][v], acc);
+                        acc = __builtin_fmaf(p11, zc[v], acc);
+                        const int soff = (int)((u * chstep_u + v * chstep_v) * Nq * 4);
+                        if (active)
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ax.dead ? 0.0f : acc), rs_out, q4,
+                                                                  soff, 0);
+                    }
+#pragma unroll
+                    for (int v = 0; v < n; ++v) zp[i - 1][v] = zc_prev[v];
+                }
+#pragma unroll
+                for (int v = 0; v < n; ++v) zc_prev[v] = zc[v];
+                if (i == np - 1) {
+#pragma unroll
+                    for (int v = 0; v < n; ++v) zp[i][v] = zc[v];
+                }
+            }
         }
     }
 }

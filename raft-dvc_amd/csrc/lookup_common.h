@@ -13,7 +13,8 @@ struct Item {
 
 // item = ((l * nach + ac) * B + b) * nqb + qb, one wavefront each (4 per block).
 __device__ __forceinline__ bool decode_item(const LookupArgs &A, Item &it) {
-    const long long item = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    // wave-uniform by construction; readfirstlane lets the compiler keep it in SGPRs
+    const long long item = (long long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const long long bq = (long long)A.B * A.nqb;
     const long long per_l = (long long)A.nach * bq;
     if (item >= per_l * A.nl) return false;
