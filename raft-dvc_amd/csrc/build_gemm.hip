@@ -29,14 +29,29 @@ namespace dvc {
 // bf16 staging image).  Rows are 16-byte-chunk XOR swizzled: chunk' = chunk ^ (row & m).
 constexpr int kBQ = 128, kBP = 128;
 
+// Prefetch load hidden from hipcc's waitcnt bookkeeping (see the loop below): the
+// compiler cannot carry store counts across the loop back-edge and would otherwise
+// drain every epilogue store (s_waitcnt vmcnt(0)) before the next tile's LDS write.
+__device__ __forceinline__ void asm_load16(u32x4 &dst, const void *p) {
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(p) : "memory");
+}
+// After the counted wait: make every prefetch register opaque at this point so no
+// consumer is scheduled above the wait (guide 5.7, form (ii)).
+template <int PF> struct PfTouch {
+    static __device__ __forceinline__ void touch(u32x4 (&pf)[PF]) {
+#pragma unroll
+        for (int i = 0; i < PF; ++i) asm volatile("" : "+v"(pf[i]));
+    }
+};
+
 __device__ __forceinline__ int swz_mask(int nch) { return (nch >= 16 ? 16 : nch) - 1; }
 
-template <int NCH>
+template <int NCH, bool STORE_F32>
 __global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict__ Q, const bf16_t *__restrict__ T,
                                                        bf16_t *__restrict__ corr, long long Nq, int Cp,
                                                        long long t_batch_rows, long long row_stride,
                                                        long long col_begin, long long col_end, int nchunk,
-                                                       float scale, int store_f32) {
+                                                       float scale) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int nch = NCH;                  // 16-byte chunks per row (Cp / 8)
     constexpr int msk = (NCH >= 16 ? 16 : NCH) - 1;
@@ -65,17 +80,30 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict_
 
     // register prefetch of the next target tile: its global loads fly while the
     // current tile's MFMAs and epilogue run
+    static_assert(PF == 4 || PF == 8 || PF == 16 || PF == 2, "prefetch depth");
     u32x4 pf[PF];
     if (chunk < ncol_tiles) {
         const long long p0 = col_begin + (long long)chunk * kBP;
 #pragma unroll
         for (int i = 0; i < PF; ++i) {
             const int id = i * 256 + t;
-            pf[i] = *reinterpret_cast<const u32x4 *>(Tb + (p0 + id / nch) * Cp + (id % nch) * 8);
+            asm_load16(pf[i], Tb + (p0 + id / nch) * Cp + (id % nch) * 8);
         }
     }
+    // vector-memory ops issued after the prefetch in one iteration: the epilogue stores
+    constexpr int NSTORE = STORE_F32 ? 16 : 8;
+    bool first = true;
     for (long long ct = chunk; ct < ncol_tiles; ct += nchunk) {
         const long long p0 = col_begin + ct * kBP;
+        // wait for this tile's prefetch only: NSTORE younger stores may stay in flight
+        if (first) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(%c0)" ::"i"(NSTORE) : "memory");
+        }
+        first = false;
+        __builtin_amdgcn_sched_barrier(0);
+        PfTouch<PF>::touch(pf);
         __syncthreads();   // previous staging image fully read / sQ written
 #pragma unroll
         for (int i = 0; i < PF; ++i) {
@@ -84,12 +112,14 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict_
             sT[row * nch + (c ^ (row & msk))] = pf[i];
         }
         __syncthreads();
-        if (ct + nchunk < ncol_tiles) {
-            const long long pn = p0 + (long long)nchunk * kBP;
+        {   // unconditional (the last iteration re-reads its own tile): a branch here would
+            // make the compiler drain every store before the next tile's LDS write
+            const long long cn = ct + nchunk < ncol_tiles ? ct + nchunk : ct;
+            const long long pn = col_begin + cn * kBP;
 #pragma unroll
             for (int i = 0; i < PF; ++i) {
                 const int id = i * 256 + t;
-                pf[i] = *reinterpret_cast<const u32x4 *>(Tb + (pn + id / nch) * Cp + (id % nch) * 8);
+                asm_load16(pf[i], Tb + (pn + id / nch) * Cp + (id % nch) * 8);
             }
         }
 
@@ -123,7 +153,7 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict_
         }
         __syncthreads();   // sT reads done: reuse as staging
 
-        if (!store_f32) {
+        if constexpr (!STORE_F32) {
             // staging [128 q][16 chunks of 8 cols] bf16, chunk' = chunk ^ (q & 15)
             u32x2 *st = reinterpret_cast<u32x2 *>(sT);
 #pragma unroll
@@ -142,16 +172,20 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict_
                         st[(q * 16 + (pch ^ (q & 15))) * 2 + h] = v;
                     }
             __syncthreads();
-            bf16_t *cb = corr + (long long)b * Nq * row_stride;
+            // branch-free buffer stores of the tile: rows past Nq fall outside num_records
+            // and columns past col_end get an out-of-range offset, so the hardware drops
+            // them; no branch keeps the compiler's counted vmcnt for the prefetch exact
+            const long long nrow = Nq - q0 < kBQ ? Nq - q0 : kBQ;
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                corr + ((long long)b * Nq + q0) * row_stride + p0, (short)0,
+                (int)(nrow * row_stride * (long long)sizeof(bf16_t)), 0x00020000);
 #pragma unroll
             for (int it = 0; it < (kBQ * 16) / 256; ++it) {
                 const int id = it * 256 + t;
                 const int q = id >> 4, c = id & 15;
-                const long long col = p0 + 8 * c;
-                if (q0 + q < Nq && col < col_end) {
-                    const u32x4 v = sT[q * 16 + (c ^ (q & 15))];
-                    *reinterpret_cast<u32x4 *>(cb + (q0 + q) * row_stride + col) = v;
-                }
+                const u32x4 v = sT[q * 16 + (c ^ (q & 15))];
+                const int off = (p0 + 8 * c < col_end) ? (int)(q * row_stride * 2 + c * 16) : 0x7ffffff0;
+                __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
             }
         } else {
             // float32 store of a bf16-input build: two passes of 64 queries each,
@@ -177,14 +211,18 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict_
                             }
                 }
                 __syncthreads();
+                {
+                    const long long qb0 = q0 + 64 * pass;
+                    const long long nrow = Nq - qb0 < 64 ? (Nq - qb0 > 0 ? Nq - qb0 : 0) : 64;
+                    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                        cbf + qb0 * row_stride + p0, (short)0, (int)(nrow * row_stride * 4), 0x00020000);
 #pragma unroll
-                for (int it = 0; it < (64 * 32) / 256; ++it) {
-                    const int id = it * 256 + t;
-                    const int q = id >> 5, c = id & 31;
-                    const long long col = p0 + 4 * c;
-                    const long long gq = q0 + 64 * pass + q;
-                    if (gq < Nq && col < col_end)
-                        *reinterpret_cast<u32x4 *>(cbf + gq * row_stride + col) = sT[q * 32 + (c ^ (q & 31))];
+                    for (int it = 0; it < (64 * 32) / 256; ++it) {
+                        const int id = it * 256 + t;
+                        const int q = id >> 5, c = id & 31;
+                        const int off = (p0 + 4 * c < col_end) ? (int)(q * row_stride * 4 + c * 16) : 0x7ffffff0;
+                        __builtin_amdgcn_raw_buffer_store_b128(sT[q * 32 + (c ^ (q & 31))], rs, off, 0, 0);
+                    }
                 }
                 __syncthreads();
             }
@@ -275,25 +313,34 @@ __global__ __launch_bounds__(256, 1) void k_build_f32(const float *__restrict__ 
                 st[q * 32 + (pch ^ (q & 31))] = v;
             }
         __syncthreads();
-        float *cb = corr + (long long)b * Nq * row_stride;
+        const long long nrow = Nq - q0 < kFQ ? Nq - q0 : kFQ;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            corr + ((long long)b * Nq + q0) * row_stride + p0, (short)0, (int)(nrow * row_stride * 4), 0x00020000);
 #pragma unroll
         for (int it = 0; it < (kFQ * 32) / 256; ++it) {
             const int id = it * 256 + t;
             const int q = id >> 5, c = id & 31;
-            const long long col = p0 + 4 * c;
-            if (q0 + q < Nq && col < col_end)
-                *reinterpret_cast<u32x4 *>(cb + (q0 + q) * row_stride + col) = st[q * 32 + (c ^ (q & 31))];
+            const int off = (p0 + 4 * c < col_end) ? (int)(q * row_stride * 4 + c * 16) : 0x7ffffff0;
+            __builtin_amdgcn_raw_buffer_store_b128(st[q * 32 + (c ^ (q & 31))], rs, off, 0, 0);
         }
     }
 }
 
-template __global__ void k_build_bf16<4>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long, long long,
-                                         long long, long long, int, float, int);
-template __global__ void k_build_bf16<8>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long, long long,
-                                         long long, long long, int, float, int);
-template __global__ void k_build_bf16<16>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
-                                          long long, long long, long long, int, float, int);
-template __global__ void k_build_bf16<32>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
-                                          long long, long long, long long, int, float, int);
+template __global__ void k_build_bf16<4, false>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+                                                 long long, long long, long long, int, float);
+template __global__ void k_build_bf16<4, true>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+                                                long long, long long, long long, int, float);
+template __global__ void k_build_bf16<8, false>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+                                                 long long, long long, long long, int, float);
+template __global__ void k_build_bf16<8, true>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+                                                long long, long long, long long, int, float);
+template __global__ void k_build_bf16<16, false>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+                                                 long long, long long, long long, int, float);
+template __global__ void k_build_bf16<16, true>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+                                                long long, long long, long long, int, float);
+template __global__ void k_build_bf16<32, false>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+                                                 long long, long long, long long, int, float);
+template __global__ void k_build_bf16<32, true>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+                                                long long, long long, long long, int, float);
 
 }  // namespace dvc

@@ -16,9 +16,9 @@ namespace dvc {
 __global__ void k_pool_fmap(const float *, float *, long long, int, int, int, int, int, int);
 template <typename T>
 __global__ void k_pack_rows(const float *, T *, int, int, long long, long long, int, int, long long, long long);
-template <int NCH>
+template <int NCH, bool STORE_F32>
 __global__ void k_build_bf16(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long, long long, long long,
-                             long long, int, float, int);
+                             long long, int, float);
 __global__ void k_build_f32(const float *, const float *, float *, long long, int, long long, long long, long long,
                             long long, int, float);
 template <typename T>
@@ -236,14 +236,14 @@ int dvc_corr_build(const void *packed_q, const void *packed_t, void *corr, int B
         auto launch = [&](auto kern) {
             (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             kern<<<grid, 256, lds, s>>>((const bf16_t *)packed_q, (const bf16_t *)packed_t, (bf16_t *)corr, Nq, Cp,
-                                        lay.row_stride, lay.row_stride, col_begin, col_end, nchunk, scale,
-                                        store_dtype == DVC_F32);
+                                        lay.row_stride, lay.row_stride, col_begin, col_end, nchunk, scale);
         };
+        const bool f32s = store_dtype == DVC_F32;
         switch (Cp / 8) {
-        case 4: launch(k_build_bf16<4>); break;
-        case 8: launch(k_build_bf16<8>); break;
-        case 16: launch(k_build_bf16<16>); break;
-        case 32: launch(k_build_bf16<32>); break;
+        case 4: f32s ? launch(k_build_bf16<4, true>) : launch(k_build_bf16<4, false>); break;
+        case 8: f32s ? launch(k_build_bf16<8, true>) : launch(k_build_bf16<8, false>); break;
+        case 16: f32s ? launch(k_build_bf16<16, true>) : launch(k_build_bf16<16, false>); break;
+        case 32: f32s ? launch(k_build_bf16<32, true>) : launch(k_build_bf16<32, false>); break;
         default: return fail(DVC_ERR_UNSUPPORTED, "build: C=%d not supported on the bf16 path", C);
         }
     } else if (in_dtype == DVC_F32) {
