@@ -127,7 +127,8 @@ int dvc_sample3d(const float *vol, const float *pts, float *out, int B, int C, i
                  int convention, void *stream);
 
 /* Kernel-variant knob for A/B timing (process-wide, not thread-safe):
- *   "lookup_variant" 0 = unaligned 16-byte run loads, 1 = aligned chunks + v_perm shifter. */
+ *   "lookup_variant" 0 = unaligned 16-byte run loads, 1 = aligned chunks + v_perm shifter;
+ *   "lookup_ablate"  diagnostics only, invalidates outputs: 1 = skip stores, 2 = skip loads. */
 int dvc_set_tuning(const char *key, int value);
 
 const char *dvc_last_error(void);

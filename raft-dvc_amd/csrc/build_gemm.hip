@@ -78,6 +78,19 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict_
     const int wp = w & 1, wq = w >> 1;
     const int h = lane >> 5, r32 = lane & 31;
 
+    // the query-tile MFMA operands never change across column tiles: keep them in
+    // registers (halves the per-tile LDS read traffic)
+    __syncthreads();
+    bf16x8 bq[2][NCH / 2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < NCH / 2; ++ks) {
+            const int row = 64 * wq + 32 * j + r32;
+            const int c = 2 * ks + h;
+            bq[j][ks] = __builtin_bit_cast(bf16x8, sQ[row * nch + (c ^ (row & msk))]);
+        }
+
     // register prefetch of the next target tile: its global loads fly while the
     // current tile's MFMAs and epilogue run
     static_assert(PF == 4 || PF == 8 || PF == 16 || PF == 2, "prefetch depth");
@@ -134,22 +147,17 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict_
 #pragma unroll
         for (int ks = 0; ks < NCH / 2; ++ks) {
             const int c = 2 * ks + h;
-            bf16x8 a[2], bq[2];
+            bf16x8 a[2];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 const int row = 64 * wp + 32 * i + r32;
                 a[i] = __builtin_bit_cast(bf16x8, sT[row * nch + (c ^ (row & msk))]);
             }
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int row = 64 * wq + 32 * j + r32;
-                bq[j] = __builtin_bit_cast(bf16x8, sQ[row * nch + (c ^ (row & msk))]);
-            }
-#pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], bq[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], bq[j][ks], acc[i][j], 0, 0, 0);
         }
         __syncthreads();   // sT reads done: reuse as staging
 

@@ -35,6 +35,8 @@ size_t fused_workspace_bytes(int B, long long Nq, int L, int radius);
 using namespace dvc;
 
 static thread_local char g_err[512] = "";
+static int g_lookup_variant = -1;   // tuning knobs (dvc_set_tuning)
+static int g_lookup_ablate = 0;
 
 static int fail(int code, const char *fmt, ...) {
     va_list ap;
@@ -67,12 +69,13 @@ static int fill_lookup_args(LookupArgs &A, const dvc_layout &lay, const void *co
         A.zero[l] = lay.zero_level[l]; A.off[l] = lay.offset[l];
         A.generic[l] = l < lay.num_levels && A.legacy && lay.W[l] != lay.D[l];
     }
+    A.ablate = g_lookup_ablate;
     return DVC_OK;
 }
 
 // Lookup kernel variant: 0 = unaligned 16-byte run loads (default), 1 = aligned
 // chunks + v_perm shifter.  DVCCORR_LOOKUP_VARIANT overrides (read once, for A/B timing).
-static int g_lookup_variant = -1;
+
 static int lookup_variant() {
     if (g_lookup_variant < 0) {
         const char *e = getenv("DVCCORR_LOOKUP_VARIANT");
@@ -109,6 +112,10 @@ int dvc_set_tuning(const char *key, int value) {
     if (!strcmp(key, "lookup_variant")) {
         if (value < 0 || value > 1) return fail(DVC_ERR_INVALID, "set_tuning: lookup_variant %d", value);
         g_lookup_variant = value;
+        return DVC_OK;
+    }
+    if (!strcmp(key, "lookup_ablate")) {   // diagnostics only (outputs become invalid)
+        g_lookup_ablate = value;
         return DVC_OK;
     }
     return fail(DVC_ERR_INVALID, "set_tuning: unknown key '%s'", key);

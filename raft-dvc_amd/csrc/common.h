@@ -40,6 +40,7 @@ struct LookupArgs {
     int B, Ltot, l0, nl, legacy, nach, ach, r;
     int H[DVC_MAX_LEVELS], W[DVC_MAX_LEVELS], D[DVC_MAX_LEVELS], Dp[DVC_MAX_LEVELS], zero[DVC_MAX_LEVELS];
     int generic[DVC_MAX_LEVELS];   // level handled by a separate per-output launch (legacy, W != D)
+    int ablate;                    // diagnostics only: 1 = skip output stores, 2 = skip run loads
     long long off[DVC_MAX_LEVELS];
 };
 

@@ -207,7 +207,7 @@ int fused_lookup(const void *packed_q, const void *packed_t, const float *coords
     const long long n3 = (long long)n * n * n;
     LookupArgs A;
     A.coords = coords; A.out = out; A.Nq = Nq; A.B = B; A.Ltot = lay.num_levels; A.nl = 1;
-    A.legacy = convention == DVC_LEGACY; A.r = radius;
+    A.legacy = convention == DVC_LEGACY; A.r = radius; A.ablate = 0;
     A.ach = n >= 3 ? 3 : n;
     A.nach = (n + A.ach - 1) / A.ach;
     for (int l = 0; l < DVC_MAX_LEVELS; ++l) {

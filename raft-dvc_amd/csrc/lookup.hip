@@ -332,10 +332,16 @@ __global__ __launch_bounds__(256) void k_lookup_win(LookupArgs A) {
         if (WINBUF) return (long long)u * rs;
         return (long long)min(max(iu + u, 0), Wl - 1) * rs;
     };
+    const bool no_loads = (A.ablate & 2) != 0;   // diagnostics: time everything but the gathers
     auto run = [&](const T *p, Raw<T, NW> &dst) {
+        if (no_loads) {
+            dst = Raw<T, NW>{};
+            return;
+        }
         if constexpr (ALIGNED) dst.load_al(p, rz0);
         else dst.load(p);
     };
+    const bool no_stores = (A.ablate & 1) != 0;
     float zp[NP][n];          // z-lerped runs of the previous column, per plane
     Raw<T, NW> nx[NP];        // prefetched runs of the next column (packed)
     {
@@ -393,9 +399,12 @@ __global__ __launch_bounds__(256) void k_lookup_win(LookupArgs A) {
                         acc = __builtin_fmaf(p01, zp[i][v], acc);
                         acc = __builtin_fmaf(p11, zc[v], acc);
                         const int soff = (int)((u * chstep_u + v * chstep_v) * Nq * 4);
-                        if (active)
+                        if (no_stores) {
+                            asm volatile("" ::"v"(acc));   // keep the value live
+                        } else if (active) {
                             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ax.dead ? 0.0f : acc), rs_out, q4,
                                                                   soff, 0);
+                        }
                     }
 #pragma unroll
                     for (int v = 0; v < n; ++v) zp[i - 1][v] = zc_prev[v];

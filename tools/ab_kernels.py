@@ -25,6 +25,7 @@ ap.add_argument("--precision", default="bf16")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--reps", type=int, default=12)
 ap.add_argument("--variants", default="0,1")
+ap.add_argument("--ablate", default="", help="comma list of lookup_ablate values to time (diagnostics)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 S, L, R = a.size, a.levels, a.radius
@@ -56,6 +57,25 @@ with torch.no_grad():
             torch.cuda.synchronize()
             res[v].append(e0.elapsed_time(e1) / a.reps)
             outs[v] = out
+if a.ablate:
+    abl = {}
+    with torch.no_grad():
+        for v in [int(x) for x in a.ablate.split(",")]:
+            _lib.set_tuning("lookup_variant", variants[0])
+            _lib.set_tuning("lookup_ablate", v)
+            ts = []
+            for _ in range(a.rounds):
+                blk(c)
+                torch.cuda.synchronize()
+                e0.record()
+                for _ in range(a.reps):
+                    blk(c)
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1) / a.reps)
+            abl[v] = statistics.median(ts)
+        _lib.set_tuning("lookup_ablate", 0)
+    print(json.dumps({"ablate_ms": abl}))
 base = outs[variants[0]]
 summary = {"size": S, "precision": a.precision, "build_ms_median": statistics.median(bres),
            "variants": {v: {"median_ms": statistics.median(t), "min_ms": min(t),
