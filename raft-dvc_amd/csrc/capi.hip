@@ -25,6 +25,7 @@ template <typename T>
 __global__ void k_corr_pool(T *, long long, long long, long long, int, int, long long, int, int, int, int);
 template <typename T, int R, bool WINBUF, bool ALIGNED> __global__ void k_lookup_win(LookupArgs);
 template <typename T> __global__ void k_lookup_generic(LookupArgs);
+template <typename T, int R, bool NT> __global__ void k_lookup_tile(LookupArgs);
 __global__ void k_sample3d(const float *, const float *, float *, int, int, int, int, int, long long, int);
 int fused_lookup(const void *packed_q, const void *packed_t, const float *coords, float *out, void *workspace, int B,
                  long long Nq, int C, const dvc_layout &lay, int radius, int convention, int dtype, hipStream_t s,
@@ -37,6 +38,7 @@ using namespace dvc;
 static thread_local char g_err[512] = "";
 static int g_lookup_variant = -1;   // tuning knobs (dvc_set_tuning)
 static int g_lookup_ablate = 0;
+static int g_lookup_nt = 0;          // nontemporal output stores in the tile kernel
 
 static int fail(int code, const char *fmt, ...) {
     va_list ap;
@@ -73,15 +75,37 @@ static int fill_lookup_args(LookupArgs &A, const dvc_layout &lay, const void *co
     return DVC_OK;
 }
 
-// Lookup kernel variant: 0 = unaligned 16-byte run loads (default), 1 = aligned
-// chunks + v_perm shifter.  DVCCORR_LOOKUP_VARIANT overrides (read once, for A/B timing).
+// Lookup kernel variant: 2 = LDS-staged tile kernel (default, lookup_tile.hip),
+// 0 = lane-per-query walk with unaligned 16-byte run loads, 1 = the same walk with
+// aligned chunks + v_perm shifter.  DVCCORR_LOOKUP_VARIANT overrides (read once).
 
 static int lookup_variant() {
     if (g_lookup_variant < 0) {
         const char *e = getenv("DVCCORR_LOOKUP_VARIANT");
-        g_lookup_variant = e ? atoi(e) : 0;
+        g_lookup_variant = e ? atoi(e) : 2;
     }
     return g_lookup_variant;
+}
+
+// The tile kernel addresses one tile's 64 rows through a buffer descriptor with
+// 32-bit offsets; wider rows take the walk.
+static bool tile_ok(const LookupArgs &A, size_t esz) {
+    return A.r >= 1 && A.r <= 6 && (long long)64 * A.row_stride * (long long)esz < (1LL << 31) - 4096;
+}
+
+template <typename T, bool NT>
+static void launch_tile_nt(const LookupArgs &A, hipStream_t s) {
+    const unsigned blocks = (unsigned)(A.B * A.nqb);
+    const unsigned threads = 64u * (unsigned)((2 * A.r + 3) / 3);
+    switch (A.r) {
+    case 1: k_lookup_tile<T, 1, NT><<<blocks, threads, 0, s>>>(A); break;
+    case 2: k_lookup_tile<T, 2, NT><<<blocks, threads, 0, s>>>(A); break;
+    case 3: k_lookup_tile<T, 3, NT><<<blocks, threads, 0, s>>>(A); break;
+    case 4: k_lookup_tile<T, 4, NT><<<blocks, threads, 0, s>>>(A); break;
+    case 5: k_lookup_tile<T, 5, NT><<<blocks, threads, 0, s>>>(A); break;
+    case 6: k_lookup_tile<T, 6, NT><<<blocks, threads, 0, s>>>(A); break;
+    default: break;
+    }
 }
 
 template <typename T, bool AL>
@@ -99,8 +123,15 @@ static void launch_lookup_v(const LookupArgs &A, unsigned blocks, hipStream_t s)
 
 template <typename T>
 static void launch_lookup(const LookupArgs &A, unsigned blocks, hipStream_t s) {
-    if (lookup_variant() == 1) launch_lookup_v<T, true>(A, blocks, s);
-    else launch_lookup_v<T, false>(A, blocks, s);
+    const int v = lookup_variant();
+    if (v == 2 && tile_ok(A, sizeof(T))) {
+        if (g_lookup_nt) launch_tile_nt<T, true>(A, s);
+        else launch_tile_nt<T, false>(A, s);
+    } else if (v == 1) {
+        launch_lookup_v<T, true>(A, blocks, s);
+    } else {
+        launch_lookup_v<T, false>(A, blocks, s);
+    }
 }
 
 extern "C" {
@@ -110,8 +141,12 @@ const char *dvc_last_error(void) { return g_err; }
 int dvc_set_tuning(const char *key, int value) {
     if (!key) return fail(DVC_ERR_INVALID, "set_tuning: null key");
     if (!strcmp(key, "lookup_variant")) {
-        if (value < 0 || value > 1) return fail(DVC_ERR_INVALID, "set_tuning: lookup_variant %d", value);
+        if (value < 0 || value > 2) return fail(DVC_ERR_INVALID, "set_tuning: lookup_variant %d", value);
         g_lookup_variant = value;
+        return DVC_OK;
+    }
+    if (!strcmp(key, "lookup_nt")) {
+        g_lookup_nt = value != 0;
         return DVC_OK;
     }
     if (!strcmp(key, "lookup_ablate")) {   // diagnostics only (outputs become invalid)

@@ -236,9 +236,10 @@ def test_determinism_and_linearity_at_cfg3():
     assert orc.rel_err(fz.cpu().numpy(), a.cpu().numpy()) <= BF16_TOL
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 def test_lookup_variants(variant):
-    """Both lookup load strategies (unaligned runs / aligned chunks + v_perm) reproduce the golden rows."""
+    """Every lookup kernel (lane-per-query walk with unaligned runs / aligned chunks + v_perm, and the
+    LDS-staged tile kernel) reproduces the golden rows."""
     import dvccorr
     from dvccorr import _lib
     _lib.set_tuning("lookup_variant", variant)
@@ -253,4 +254,40 @@ def test_lookup_variants(variant):
                 e = orc.rel_err(_rows(out, g["rows"]), g[f"out_rows_{tag}"])
                 assert e <= tol, (variant, case, prec, tag, e)
     finally:
-        _lib.set_tuning("lookup_variant", 0)
+        _lib.set_tuning("lookup_variant", 2)
+
+
+@pytest.mark.parametrize("shape,L,r", [((9, 7, 5), 2, 1), ((12, 10, 16), 3, 2), ((16, 16, 16), 4, 3),
+                                       ((20, 13, 24), 3, 4), ((32, 32, 32), 4, 4), ((24, 26, 28), 2, 5),
+                                       ((30, 28, 40), 2, 6), ((40, 36, 33), 3, 4)])
+def test_tile_kernel_matches_walk(shape, L, r):
+    """The LDS-staged tile kernel (variant 2) is bit-identical to the lane-per-query walk (variant 0):
+    same per-axis weights, same separable summation order.  Ragged tiles (Nq % 64 != 0), non-cubic and
+    odd sizes, D padding, every radius the kernel is instantiated for, both conventions, both store
+    dtypes, wide flows that leave the volume, and NaN / huge coordinates."""
+    import dvccorr
+    from dvccorr import _lib
+    H, W, D = shape
+    g = torch.Generator(device="cpu").manual_seed(H * 1000 + W * 10 + D + r)
+    f1 = torch.randn(1, 32, H, W, D, generator=g).to(DEV)
+    f2 = torch.randn(1, 32, H, W, D, generator=g).to(DEV)
+    base = dvccorr.coords_grid_3d(1, H, W, D, torch.device("cpu"))
+    c = base + (torch.rand(1, 3, H, W, D, generator=g) * 2 - 1) * (r + 6)
+    c.view(3, -1)[:, 5] = float("nan")
+    c.view(3, -1)[1, 17] = 1e30
+    c.view(3, -1)[2, 23] = -float("inf")
+    c = c.to(DEV)
+    try:
+        for prec in ("bf16", "fp32"):
+            for legacy in (False, True):
+                blk = dvccorr.CorrBlock(f1, f2, L, r, legacy_wd_swap=legacy, precision=prec)
+                outs = []
+                for v in (0, 2):
+                    _lib.set_tuning("lookup_variant", v)
+                    outs.append(blk(c))
+                torch.cuda.synchronize()
+                assert torch.isfinite(outs[1]).all(), (prec, legacy)
+                assert torch.equal(outs[0], outs[1]), (shape, L, r, prec, legacy,
+                                                        float((outs[0] - outs[1]).abs().max()))
+    finally:
+        _lib.set_tuning("lookup_variant", 2)
