@@ -12,6 +12,8 @@
 
 #include "common.h"
 
+#include <type_traits>
+
 namespace dvc {
 __global__ void k_pool_fmap(const float *, float *, long long, int, int, int, int, int, int);
 template <typename T>
@@ -25,7 +27,7 @@ template <typename T>
 __global__ void k_corr_pool(T *, long long, long long, long long, int, int, long long, int, int, int, int);
 template <typename T, int R, bool WINBUF, bool ALIGNED> __global__ void k_lookup_win(LookupArgs);
 template <typename T> __global__ void k_lookup_generic(LookupArgs);
-template <typename T, int R, bool NT> __global__ void k_lookup_tile(LookupArgs);
+template <typename T, int R, bool NT, int ABL> __global__ void k_lookup_tile(LookupArgs);
 __global__ void k_sample3d(const float *, const float *, float *, int, int, int, int, int, long long, int);
 int fused_lookup(const void *packed_q, const void *packed_t, const float *coords, float *out, void *workspace, int B,
                  long long Nq, int C, const dvc_layout &lay, int radius, int convention, int dtype, hipStream_t s,
@@ -38,7 +40,9 @@ using namespace dvc;
 static thread_local char g_err[512] = "";
 static int g_lookup_variant = -1;   // tuning knobs (dvc_set_tuning)
 static int g_lookup_ablate = 0;
-static int g_lookup_nt = 0;          // nontemporal output stores in the tile kernel
+static int g_lookup_nt = 1;          // nontemporal output stores in the tile kernel
+static int g_lookup_order = 1;       // tile kernel level order (LookupArgs::order)
+static int g_lookup_ldpol = 0;       // tile kernel load cache policy (LookupArgs::ldpol)
 
 static int fail(int code, const char *fmt, ...) {
     va_list ap;
@@ -72,6 +76,8 @@ static int fill_lookup_args(LookupArgs &A, const dvc_layout &lay, const void *co
         A.generic[l] = l < lay.num_levels && A.legacy && lay.W[l] != lay.D[l];
     }
     A.ablate = g_lookup_ablate;
+    A.order = g_lookup_order;
+    A.ldpol = g_lookup_ldpol;
     return DVC_OK;
 }
 
@@ -97,13 +103,21 @@ template <typename T, bool NT>
 static void launch_tile_nt(const LookupArgs &A, hipStream_t s) {
     const unsigned blocks = (unsigned)(A.B * A.nqb);
     const unsigned threads = 64u * (unsigned)((2 * A.r + 3) / 3);
+    if constexpr (std::is_same<T, bf16_t>::value && NT) {
+        if (A.r == 4 && A.ablate >= 1 && A.ablate <= 3) {   // diagnostics only
+            if (A.ablate == 1) k_lookup_tile<T, 4, NT, 1><<<blocks, threads, 0, s>>>(A);
+            else if (A.ablate == 2) k_lookup_tile<T, 4, NT, 2><<<blocks, threads, 0, s>>>(A);
+            else k_lookup_tile<T, 4, NT, 3><<<blocks, threads, 0, s>>>(A);
+            return;
+        }
+    }
     switch (A.r) {
-    case 1: k_lookup_tile<T, 1, NT><<<blocks, threads, 0, s>>>(A); break;
-    case 2: k_lookup_tile<T, 2, NT><<<blocks, threads, 0, s>>>(A); break;
-    case 3: k_lookup_tile<T, 3, NT><<<blocks, threads, 0, s>>>(A); break;
-    case 4: k_lookup_tile<T, 4, NT><<<blocks, threads, 0, s>>>(A); break;
-    case 5: k_lookup_tile<T, 5, NT><<<blocks, threads, 0, s>>>(A); break;
-    case 6: k_lookup_tile<T, 6, NT><<<blocks, threads, 0, s>>>(A); break;
+    case 1: k_lookup_tile<T, 1, NT, 0><<<blocks, threads, 0, s>>>(A); break;
+    case 2: k_lookup_tile<T, 2, NT, 0><<<blocks, threads, 0, s>>>(A); break;
+    case 3: k_lookup_tile<T, 3, NT, 0><<<blocks, threads, 0, s>>>(A); break;
+    case 4: k_lookup_tile<T, 4, NT, 0><<<blocks, threads, 0, s>>>(A); break;
+    case 5: k_lookup_tile<T, 5, NT, 0><<<blocks, threads, 0, s>>>(A); break;
+    case 6: k_lookup_tile<T, 6, NT, 0><<<blocks, threads, 0, s>>>(A); break;
     default: break;
     }
 }
@@ -147,6 +161,15 @@ int dvc_set_tuning(const char *key, int value) {
     }
     if (!strcmp(key, "lookup_nt")) {
         g_lookup_nt = value != 0;
+        return DVC_OK;
+    }
+    if (!strcmp(key, "lookup_order")) {
+        g_lookup_order = value != 0;
+        return DVC_OK;
+    }
+    if (!strcmp(key, "lookup_ldpol")) {
+        if (value < 0 || value > 3) return fail(DVC_ERR_INVALID, "set_tuning: lookup_ldpol %d", value);
+        g_lookup_ldpol = value;
         return DVC_OK;
     }
     if (!strcmp(key, "lookup_ablate")) {   // diagnostics only (outputs become invalid)

@@ -41,6 +41,8 @@ struct LookupArgs {
     int H[DVC_MAX_LEVELS], W[DVC_MAX_LEVELS], D[DVC_MAX_LEVELS], Dp[DVC_MAX_LEVELS], zero[DVC_MAX_LEVELS];
     int generic[DVC_MAX_LEVELS];   // level handled by a separate per-output launch (legacy, W != D)
     int ablate;                    // diagnostics only: 1 = skip output stores, 2 = skip run loads
+    int order;                     // tile kernel: 1 = odd tiles walk the levels coarse-to-fine
+    int ldpol;                     // tile kernel: cache-policy bits of the plane loads
     long long off[DVC_MAX_LEVELS];
 };
 

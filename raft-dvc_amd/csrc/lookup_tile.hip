@@ -29,6 +29,8 @@
 #include "common.h"
 #include "lookup_common.h"
 
+#include <type_traits>
+
 namespace dvc {
 
 template <typename T, int R> struct TileCfg {
@@ -74,11 +76,22 @@ __device__ __forceinline__ void lds_run(const unsigned char *base, int addr, con
     for (int i = 0; i < NW; ++i) v[i] = p[i];
 }
 
-template <typename T, int R, bool NT>
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// z-lerped run of one window column: zl[v] = fma(R[v+1], w1[v], R[v] * w0[v]), v < n,
+// kept as n/2 pairs (packed-f32 math, same per-element rounding) plus a tail.
+template <int n> struct ZRun {
+    f32x2 p[n / 2];
+    float t;
+};
+
+// ABL (diagnostics only, never the product path): 1 = skip output stores, 2 = skip loads.
+template <typename T, int R, bool NT, int ABL>
 __global__ __launch_bounds__(64 * ((2 * R + 3) / 3), 2) void k_lookup_tile(LookupArgs A) {
     using C = TileCfg<T, R>;
-    constexpr int n = C::n, NW = C::NW, ES = C::ES, CE = C::CE;
+    constexpr int n = C::n, NW = C::NW, ES = C::ES, CE = C::CE, NP = n / 2;
     constexpr long long n3 = (long long)n * n * n;
+    constexpr int NU_LAST = n - C::COLS * (C::NWAVES - 1);   // output columns of the last wave
     __shared__ __attribute__((aligned(16))) unsigned char smem[C::LDS];
     __shared__ int tab[3][64];   // per query of the tile: ih, cs, za (element units)
 
@@ -99,7 +112,7 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3), 2) void k_lookup_tile(Looku
     float cy = 0.f, cx = 0.f, cz = 0.f;
     if (active) load_coords(A.coords, b, Nq, q, cy, cx, cz);
 
-    // tile rows as one buffer: loads past the valid rows / out-of-range planes return 0
+    // the tile's rows as one buffer: offsets past its valid rows (or negative) read 0
     const T *tile_rows = reinterpret_cast<const T *>(A.corr) + ((long long)b * Nq + A.q0 + qt) * A.row_stride;
     // (readfirstlane: keep the descriptor in SGPRs, no waterfall loops around the loads)
     const unsigned long long trp = (unsigned long long)tile_rows;
@@ -108,33 +121,43 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3), 2) void k_lookup_tile(Looku
     const int nrec = __builtin_amdgcn_readfirstlane((int)((long long)nvalid * A.row_stride * ES));
     const __amdgpu_buffer_rsrc_t rs_in = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(((unsigned long long)trhi << 32) | trlo), (short)0, nrec, 0x00020000);
-    const int q4 = (int)(active ? q * 4 : 0);
+    // output lane offset; lanes past the tile's end store out of the descriptor's range (dropped)
+    const int q4 = active ? (int)(q * 4) : 0x7ffffff0;
+    const int chstep_u = A.legacy ? 1 : n;       // output-channel step per U (W-axis) offset
+    const int chstep_v = A.legacy ? n : 1;       // ... per V (D-axis) offset
+    const int u0 = wave * C::COLS;               // this wave's output columns u0 .. u0 + NU - 1
+    const int ldpol = A.ldpol;
 
-    // output columns of this wave: u = u0 .. u0 + nu - 1; window columns u0 .. u0 + nu
-    const int u0 = wave * C::COLS;
-    const int nu = min(C::COLS, n - u0);
+    // store of output (row a, column u, offset v) of this lane's query
+    auto out_rsrc = [&](float *obase, int a, int u) {
+        return __builtin_amdgcn_make_buffer_rsrc(obase + ((long long)a * n * n + (long long)u * chstep_u) * Nq,
+                                                 (short)0, (int)(n * n * Nq * 4), 0x00020000);
+    };
+    auto store = [&](__amdgpu_buffer_rsrc_t rs, int v, float val) {
+        if constexpr ((ABL & 1) != 0) asm volatile("" ::"v"(val));
+        else __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val), rs, q4, (int)(v * chstep_v * Nq * 4),
+                                                   NT ? 2 : 0);
+    };
 
-    for (int l = A.l0; l < A.l0 + A.nl; ++l) {
+    auto level = [&](int l, auto nu_c) {
+        constexpr int NU = decltype(nu_c)::value;
         float *obase = A.out + ((long long)b * A.Ltot + l) * n3 * Nq;   // wave-uniform
-        const int chstep_u = A.legacy ? 1 : n;
-        const int chstep_v = A.legacy ? n : 1;
-        if (A.zero[l] || A.generic[l]) {
-            if (A.zero[l]) {
-                for (int a = 0; a < n; ++a) {
-                    const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(
-                        obase + (long long)a * n * n * Nq, (short)0, (int)(n * n * Nq * 4), 0x00020000);
-                    for (int uu = 0; uu < nu; ++uu)
-                        for (int v = 0; v < n; ++v)
-                            if (active) __builtin_amdgcn_raw_buffer_store_b32(
-                                0u, rs_out, q4, (int)(((u0 + uu) * chstep_u + v * chstep_v) * Nq * 4), NT ? 2 : 0);
+        if (A.zero[l]) {
+            for (int a = 0; a < n; ++a)
+#pragma unroll
+                for (int uu = 0; uu < NU; ++uu) {
+                    const __amdgpu_buffer_rsrc_t rs = out_rsrc(obase, a, u0 + uu);
+#pragma unroll
+                    for (int v = 0; v < n; ++v) store(rs, v, 0.0f);
                 }
-            }
-            continue;   // generic (legacy, W != D) levels: k_lookup_generic
+            return;
         }
         const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
         const float sc = (float)(1 << l);
         WinAxes ax;
         window_axes(cy / sc, cx / sc, cz / sc, Hl, Wl, Dl, A.legacy, ax);
+        // (a NaN / huge coordinate moves the window far outside the level: every
+        //  weight below is then folded to 0 and the output is 0, as the reference's)
         const int ih = (int)ax.kh - R, iu = (int)ax.ku - R, iv = (int)ax.kv - R;
         const int NC = min(NW, Wl);
         const int ZW = min(Dpl, C::ZWMAX);
@@ -153,35 +176,43 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3), 2) void k_lookup_tile(Looku
             wv0[t] = (unsigned)(iv + t) < (unsigned)Dl ? wv0[t] : 0.0f;
             wv1[t] = (unsigned)(iv + t + 1) < (unsigned)Dl ? wv1[t] : 0.0f;
         }
-        float wx0[C::COLS], wx1[C::COLS];
+        f32x2 w0p[NP], w1p[NP];
 #pragma unroll
-        for (int uu = 0; uu < C::COLS; ++uu) {
-            const int u = min(u0 + uu, n - 1);
+        for (int i = 0; i < NP; ++i) {
+            w0p[i] = f32x2{wv0[2 * i], wv0[2 * i + 1]};
+            w1p[i] = f32x2{wv1[2 * i], wv1[2 * i + 1]};
+        }
+        float wx0[NU], wx1[NU];
+#pragma unroll
+        for (int uu = 0; uu < NU; ++uu) {
+            const int u = u0 + uu;
             axis_weights(ax.pu, ax.ku, u - R, ax.un, ax.uu, wx0[uu], wx1[uu]);
             wx0[uu] = (unsigned)(iu + u) < (unsigned)Wl ? wx0[uu] : 0.0f;
             wx1[uu] = (unsigned)(iu + u + 1) < (unsigned)Wl ? wx1[uu] : 0.0f;
         }
         // LDS read offsets (bytes, relative to a slot) of this lane's window columns
         const int rz = min(max(iv - za, -NW), ZW);
-        int coff[C::COLS + 1];
+        int coff[NU + 1];
 #pragma unroll
-        for (int k = 0; k <= C::COLS; ++k) {
+        for (int k = 0; k <= NU; ++k) {
             const int cl = min(max(iu + u0 + k - cs, 0), NC - 1);
             coff[k] = lane * SQ + (cl * ZW + rz) * ES;
         }
 
         __syncthreads();   // previous level's LDS reads are done; table free
         if (wave == 0) {
-            tab[0][lane] = active ? ih : -(1 << 20);
+            tab[0][lane] = active ? min(max(ih, -2 * NW), Hl) : -2 * NW;
             tab[1][lane] = cs;
             tab[2][lane] = za;
         }
         __syncthreads();
 
-        // this thread's chunks of every plane: (query j, column c, z-chunk k)
-        // packed per chunk: LDS offset / 8 (low 16 bits, 0xffff = no chunk) | (ih_j + 0x4000) << 16
-        int gofs[C::MAXCH];
-        unsigned pk[C::MAXCH];
+        // this thread's chunks of every plane: (query j, column c, z-chunk k).  voff =
+        // byte offset of the chunk in window plane 0; window plane wp adds wp * plane_bytes.
+        // Planes outside the level read finite neighbouring data or 0 (negative offsets
+        // fail the range check): their weights are 0, so only finiteness matters.
+        int voff[C::MAXCH];
+        unsigned lo8[C::MAXCH];   // LDS offset / 8 of the chunk (0xffff: no chunk)
 #pragma unroll
         for (int k = 0; k < C::MAXCH; ++k) {
             const int idx = tid + k * C::THREADS;
@@ -191,107 +222,118 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3), 2) void k_lookup_tile(Looku
             const int zc = rem - c * ZC;
             const bool ok = idx < nch;
             const int jj = ok ? j : 0;
-            const int ihj = ok ? min(max(tab[0][jj], -2 * NW), Hl) : -2 * NW;   // clamping keeps y out of range
-            const unsigned lo = ok ? (unsigned)(jj * SQ + (c * ZW + zc * CE) * ES) >> 3 : 0xffffu;
-            pk[k] = lo | ((unsigned)(ihj + 0x4000) << 16);
-            gofs[k] = (int)(((long long)jj * A.row_stride + A.off[l] + (long long)(tab[1][jj] + c) * Dpl + tab[2][jj] +
-                             zc * CE) * ES);
+            lo8[k] = ok ? (unsigned)(jj * SQ + (c * ZW + zc * CE) * ES) >> 3 : 0xffffu;
+            voff[k] = ok ? (int)(((long long)jj * A.row_stride + A.off[l] + (long long)tab[0][jj] * Wl * Dpl +
+                                  (long long)(tab[1][jj] + c) * Dpl + tab[2][jj] + zc * CE) * ES)
+                         : 0x7ff00000;
         }
         auto load_plane = [&](int wp, u32x4 (&st)[C::MAXCH]) {
 #pragma unroll
             for (int k = 0; k < C::MAXCH; ++k) {
-                const int y = (int)(pk[k] >> 16) - 0x4000 + wp;
-                const int off = (unsigned)y < (unsigned)Hl ? gofs[k] + y * plane_bytes : 0x7fffffff - 64;
-                st[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, off, 0, 0));
+                if constexpr ((ABL & 2) != 0) st[k] = u32x4{(unsigned)k, 0, 0, 0};
+                else if (ldpol == 2) st[k] = __builtin_bit_cast(
+                    u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, voff[k] + wp * plane_bytes, 0, 2));
+                else st[k] = __builtin_bit_cast(
+                    u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, voff[k] + wp * plane_bytes, 0, 0));
             }
         };
         auto write_plane = [&](int slot, const u32x4 (&st)[C::MAXCH]) {
             unsigned char *sb = smem + C::GUARD + slot * C::SLOT;
 #pragma unroll
             for (int k = 0; k < C::MAXCH; ++k) {
-                const unsigned lo16 = pk[k] & 0xffffu;
-                if (lo16 != 0xffffu) {
+                if (lo8[k] != 0xffffu) {
                     u32x2 lo = {st[k][0], st[k][1]}, hi = {st[k][2], st[k][3]};
-                    *reinterpret_cast<u32x2 *>(sb + lo16 * 8) = lo;
-                    *reinterpret_cast<u32x2 *>(sb + lo16 * 8 + 8) = hi;
+                    *reinterpret_cast<u32x2 *>(sb + lo8[k] * 8) = lo;
+                    *reinterpret_cast<u32x2 *>(sb + lo8[k] * 8 + 8) = hi;
                 }
             }
         };
-        auto lerp_col = [&](const unsigned char *sb, int addr, float (&zl)[n]) {
+        auto lerp_col = [&](int slot, int k, ZRun<n> &z) {
             float r[NW];
-            lds_run<NW>(sb, addr, (const T *)nullptr, r);
+            lds_run<NW>(smem + C::GUARD + slot * C::SLOT, coff[k], (const T *)nullptr, r);
 #pragma unroll
-            for (int v = 0; v < n; ++v) zl[v] = __builtin_fmaf(r[v + 1], wv1[v], r[v] * wv0[v]);
+            for (int i = 0; i < NP; ++i)
+                z.p[i] = __builtin_elementwise_fma(f32x2{r[2 * i + 1], r[2 * i + 2]}, w1p[i],
+                                                   f32x2{r[2 * i], r[2 * i + 1]} * w0p[i]);
+            z.t = __builtin_fmaf(r[n], wv1[n - 1], r[n - 1] * wv0[n - 1]);
         };
 
-        u32x4 st[C::MAXCH];
-        float zp[C::COLS + 1][n];
-        load_plane(0, st);
-        write_plane(0, st);
-        load_plane(1, st);
+        // staged planes: plane p + 2 is loaded into st[p & 1] two rows before it is written
+        u32x4 st[2][C::MAXCH];
+        ZRun<n> zp[NU + 1];       // z-lerped columns of the lower plane of the current row
+        load_plane(0, st[0]);
+        load_plane(1, st[1]);
+        write_plane(0, st[0]);
+        load_plane(2, st[0]);
         __syncthreads();          // plane 0 in slot 0
 #pragma unroll
-        for (int k = 0; k <= C::COLS; ++k)
-            if (k <= nu) lerp_col(smem + C::GUARD, coff[k], zp[k]);
-        write_plane(1, st);
+        for (int k = 0; k <= NU; ++k) lerp_col(0, k, zp[k]);
+        write_plane(1, st[1]);
         __syncthreads();          // plane 1 in slot 1
-#pragma unroll 1
+#pragma unroll
         for (int a = 0; a < n; ++a) {
-            const bool more = a + 2 < NW;
-            if (more) load_plane(a + 2, st);             // in flight during this row
+            if (a + 3 < NW) load_plane(a + 3, st[(a + 1) & 1]);   // in flight for two rows
             float wy0, wy1;
             axis_weights(ax.ph, ax.kh, a - R, ax.hs, ax.hs, wy0, wy1);
             wy0 = (unsigned)(ih + a) < (unsigned)Hl ? wy0 : 0.0f;
             wy1 = (unsigned)(ih + a + 1) < (unsigned)Hl ? wy1 : 0.0f;
-            const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(
-                obase + (long long)a * n * n * Nq, (short)0, (int)(n * n * Nq * 4), 0x00020000);
-            const unsigned char *sb = smem + C::GUARD + ((a + 1) & 1) * C::SLOT;
             // column by column: once window column k of plane a+1 is lerped, output
             // column k-1 is complete and plane a's column k-1 retires
-            float zprev[n];
+            ZRun<n> zprev;
 #pragma unroll
-            for (int k = 0; k <= C::COLS; ++k) {
-                if (k <= nu) {
-                    float zcur[n];
-                    lerp_col(sb, coff[k], zcur);
-                    if (k >= 1) {
-                        const int uu = k - 1;
-                        const float p00 = wx0[uu] * wy0, p10 = wx1[uu] * wy0;
-                        const float p01 = wx0[uu] * wy1, p11 = wx1[uu] * wy1;
+            for (int k = 0; k <= NU; ++k) {
+                ZRun<n> zcur;
+                lerp_col((a + 1) & 1, k, zcur);
+                if (k >= 1) {
+                    const int uu = k - 1;
+                    const float p00 = wx0[uu] * wy0, p10 = wx1[uu] * wy0;
+                    const float p01 = wx0[uu] * wy1, p11 = wx1[uu] * wy1;
+                    const f32x2 P00 = {p00, p00}, P10 = {p10, p10}, P01 = {p01, p01}, P11 = {p11, p11};
+                    const __amdgpu_buffer_rsrc_t rs = out_rsrc(obase, a, u0 + uu);
 #pragma unroll
-                        for (int v = 0; v < n; ++v) {
-                            float acc = p00 * zp[uu][v];
-                            acc = __builtin_fmaf(p10, zp[uu + 1][v], acc);
-                            acc = __builtin_fmaf(p01, zprev[v], acc);
-                            acc = __builtin_fmaf(p11, zcur[v], acc);
-                            const int soff = (int)(((u0 + uu) * chstep_u + v * chstep_v) * Nq * 4);
-                            if (active)
-                                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ax.dead ? 0.0f : acc), rs_out,
-                                                                      q4, soff, NT ? 2 : 0);
-                        }
-#pragma unroll
-                        for (int v = 0; v < n; ++v) zp[uu][v] = zprev[v];
+                    for (int i = 0; i < NP; ++i) {
+                        f32x2 acc = P00 * zp[uu].p[i];
+                        acc = __builtin_elementwise_fma(P10, zp[uu + 1].p[i], acc);
+                        acc = __builtin_elementwise_fma(P01, zprev.p[i], acc);
+                        acc = __builtin_elementwise_fma(P11, zcur.p[i], acc);
+                        store(rs, 2 * i, acc[0]);
+                        store(rs, 2 * i + 1, acc[1]);
                     }
-#pragma unroll
-                    for (int v = 0; v < n; ++v) zprev[v] = zcur[v];
-                    if (k == nu) {
-#pragma unroll
-                        for (int v = 0; v < n; ++v) zp[k][v] = zcur[v];
-                    }
+                    float acc = p00 * zp[uu].t;
+                    acc = __builtin_fmaf(p10, zp[uu + 1].t, acc);
+                    acc = __builtin_fmaf(p01, zprev.t, acc);
+                    acc = __builtin_fmaf(p11, zcur.t, acc);
+                    store(rs, n - 1, acc);
+                    zp[uu] = zprev;
                 }
+                zprev = zcur;
+                if (k == NU) zp[k] = zcur;
             }
-            if (more) write_plane(a & 1, st);            // slot of plane a, read in row a - 1
+            if (a + 2 < NW) write_plane(a & 1, st[a & 1]);   // plane a+2 into the slot of plane a (read in row a-1)
             __syncthreads();
         }
+    };
+
+    // odd tiles walk the levels coarse-to-fine, so the two tiles sharing a CU mix the
+    // gather-heavy fine levels with the store-heavy coarse ones
+    const bool rev = A.order && (blockIdx.x & 1);
+    for (int li = 0; li < A.nl; ++li) {
+        const int l = A.l0 + (rev ? A.nl - 1 - li : li);
+        if (A.generic[l] && !A.zero[l]) continue;   // legacy level with W != D: k_lookup_generic
+        if (NU_LAST == C::COLS || wave < C::NWAVES - 1) level(l, std::integral_constant<int, C::COLS>{});
+        else level(l, std::integral_constant<int, NU_LAST>{});
     }
 }
 
-#define DVC_TILE_INST(T, R)                                         \
-    template __global__ void k_lookup_tile<T, R, false>(LookupArgs); \
-    template __global__ void k_lookup_tile<T, R, true>(LookupArgs);
+#define DVC_TILE_INST(T, R)                                            \
+    template __global__ void k_lookup_tile<T, R, false, 0>(LookupArgs); \
+    template __global__ void k_lookup_tile<T, R, true, 0>(LookupArgs);
 DVC_TILE_INST(float, 1) DVC_TILE_INST(float, 2) DVC_TILE_INST(float, 3)
 DVC_TILE_INST(float, 4) DVC_TILE_INST(float, 5) DVC_TILE_INST(float, 6)
 DVC_TILE_INST(bf16_t, 1) DVC_TILE_INST(bf16_t, 2) DVC_TILE_INST(bf16_t, 3)
 DVC_TILE_INST(bf16_t, 4) DVC_TILE_INST(bf16_t, 5) DVC_TILE_INST(bf16_t, 6)
+template __global__ void k_lookup_tile<bf16_t, 4, true, 1>(LookupArgs);
+template __global__ void k_lookup_tile<bf16_t, 4, true, 2>(LookupArgs);
+template __global__ void k_lookup_tile<bf16_t, 4, true, 3>(LookupArgs);
 
 }  // namespace dvc

@@ -24,7 +24,7 @@ ap.add_argument("--radius", type=int, default=4)
 ap.add_argument("--precision", default="bf16")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--reps", type=int, default=12)
-ap.add_argument("--variants", default="0,1")
+ap.add_argument("--variants", default="0,2", help="comma list; a variant may carry knobs: 2:lookup_nt=1")
 ap.add_argument("--ablate", default="", help="comma list of lookup_ablate values to time (diagnostics)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
@@ -34,7 +34,17 @@ f1 = torch.randn(1, 128, S, S, S, generator=g).to(dev)
 f2 = torch.randn(1, 128, S, S, S, generator=g).to(dev)
 c = (dvccorr.coords_grid_3d(1, S, S, S, torch.device("cpu")) +
      (torch.rand(1, 3, S, S, S, generator=g) * 4 - 2)).to(dev)
-variants = [int(v) for v in a.variants.split(",")]
+variants = a.variants.split(",")
+
+
+def apply(v):
+    parts = v.split(":")
+    _lib.set_tuning("lookup_nt", 0)
+    _lib.set_tuning("lookup_variant", int(parts[0]))
+    for kv in parts[1:]:
+        k, val = kv.split("=")
+        _lib.set_tuning(k, int(val))
+
 res = {v: [] for v in variants}
 bres = []
 outs = {}
@@ -47,7 +57,7 @@ with torch.no_grad():
         torch.cuda.synchronize()
         bres.append(e0.elapsed_time(e1))
         for v in variants:
-            _lib.set_tuning("lookup_variant", v)
+            apply(v)
             out = blk(c)
             torch.cuda.synchronize()
             e0.record()
@@ -61,7 +71,7 @@ if a.ablate:
     abl = {}
     with torch.no_grad():
         for v in [int(x) for x in a.ablate.split(",")]:
-            _lib.set_tuning("lookup_variant", variants[0])
+            apply(variants[0])
             _lib.set_tuning("lookup_ablate", v)
             ts = []
             for _ in range(a.rounds):

@@ -18,8 +18,12 @@ ap.add_argument("--precision", default="bf16")
 ap.add_argument("--reps", type=int, default=4)
 ap.add_argument("--variant", type=int, default=0)
 ap.add_argument("--impl", default="materialised")
+ap.add_argument("--tune", default="", help="comma list key=value of dvc_set_tuning knobs")
 a = ap.parse_args()
 _lib.set_tuning("lookup_variant", a.variant)
+for kv in filter(None, a.tune.split(",")):
+    k, v = kv.split("=")
+    _lib.set_tuning(k, int(v))
 dev = torch.device("cuda:0")
 S = a.size
 g = torch.Generator(device="cpu").manual_seed(7)

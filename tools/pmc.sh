@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD
-OUT=$R/gpurun_out/${TAG:-r01}/pmc_v${VARIANT:-0}_${PREC:-bf16}_${SIZE:-32}
+OUT=$R/gpurun_out/${TAG:-r01}/pmc_v${VARIANT:-0}${TUNE:+_$TUNE}_${PREC:-bf16}_${SIZE:-32}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
@@ -12,7 +12,7 @@ i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" "TA_BUSY_avr TA_TA_BUSY_sum GRBM_GUI_ACTIVE GRBM_COUNT" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
   timeout -s KILL 90 rocprofv3 --pmc $grp --output-format csv -d "$OUT/p$i" -o run -- \
-      python "$R/tools/lookup_only.py" --variant ${VARIANT:-0} --precision ${PREC:-bf16} --size ${SIZE:-32} ${EXTRA:-} > "$OUT/p$i.log" 2>&1
+      python "$R/tools/lookup_only.py" --variant ${VARIANT:-0} --tune "${TUNE:-}" --precision ${PREC:-bf16} --size ${SIZE:-32} ${EXTRA:-} > "$OUT/p$i.log" 2>&1
   rc=$?; echo "pmc pass $i ($grp) rc=$rc"
   if [ $rc -ne 0 ]; then tail -3 "$OUT/p$i.log"; [ $rc -ge 124 ] && exit $rc; fi
 done
