@@ -201,7 +201,7 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3), 2) void k_lookup_tile(Looku
 
         __syncthreads();   // previous level's LDS reads are done; table free
         if (wave == 0) {
-            tab[0][lane] = active ? min(max(ih, -2 * NW), Hl) : -2 * NW;
+            tab[0][lane] = min(max(ih, -2 * NW), Hl);
             tab[1][lane] = cs;
             tab[2][lane] = za;
         }
@@ -209,10 +209,11 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3), 2) void k_lookup_tile(Looku
 
         // this thread's chunks of every plane: (query j, column c, z-chunk k).  voff =
         // byte offset of the chunk in window plane 0; window plane wp adds wp * plane_bytes.
-        // Planes outside the level read finite neighbouring data or 0 (negative offsets
-        // fail the range check): their weights are 0, so only finiteness matters.
+        // pk = LDS offset / 8 (low 16 bits; 0xffff: no chunk) | mask of the window planes
+        // inside the level (high 16 bits).  Planes outside it are not loaded: their LDS
+        // slots keep earlier, finite data, and their weights are 0.
         int voff[C::MAXCH];
-        unsigned lo8[C::MAXCH];   // LDS offset / 8 of the chunk (0xffff: no chunk)
+        unsigned pk[C::MAXCH];
 #pragma unroll
         for (int k = 0; k < C::MAXCH; ++k) {
             const int idx = tid + k * C::THREADS;
@@ -222,29 +223,36 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3), 2) void k_lookup_tile(Looku
             const int zc = rem - c * ZC;
             const bool ok = idx < nch;
             const int jj = ok ? j : 0;
-            lo8[k] = ok ? (unsigned)(jj * SQ + (c * ZW + zc * CE) * ES) >> 3 : 0xffffu;
-            voff[k] = ok ? (int)(((long long)jj * A.row_stride + A.off[l] + (long long)tab[0][jj] * Wl * Dpl +
-                                  (long long)(tab[1][jj] + c) * Dpl + tab[2][jj] + zc * CE) * ES)
-                         : 0x7ff00000;
+            const int ihj = tab[0][jj];
+            const int plo = min(max(-ihj, 0), NW), phi = min(max(Hl - ihj, 0), NW);
+            const unsigned mask = ok && jj < nvalid ? ((1u << phi) - 1u) & ~((1u << plo) - 1u) : 0u;
+            pk[k] = (ok ? (unsigned)(jj * SQ + (c * ZW + zc * CE) * ES) >> 3 : 0xffffu) | (mask << 16);
+            voff[k] = (int)(((long long)jj * A.row_stride + A.off[l] + (long long)ihj * Wl * Dpl +
+                             (long long)(tab[1][jj] + c) * Dpl + tab[2][jj] + zc * CE) * ES);
         }
         auto load_plane = [&](int wp, u32x4 (&st)[C::MAXCH]) {
 #pragma unroll
             for (int k = 0; k < C::MAXCH; ++k) {
                 if constexpr ((ABL & 2) != 0) st[k] = u32x4{(unsigned)k, 0, 0, 0};
-                else if (ldpol == 2) st[k] = __builtin_bit_cast(
-                    u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, voff[k] + wp * plane_bytes, 0, 2));
-                else st[k] = __builtin_bit_cast(
-                    u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, voff[k] + wp * plane_bytes, 0, 0));
+                else if (pk[k] & (1u << (16 + wp))) {
+                    if (ldpol == 2)
+                        st[k] = __builtin_bit_cast(
+                            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, voff[k] + wp * plane_bytes, 0, 2));
+                    else
+                        st[k] = __builtin_bit_cast(
+                            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, voff[k] + wp * plane_bytes, 0, 0));
+                }
             }
         };
-        auto write_plane = [&](int slot, const u32x4 (&st)[C::MAXCH]) {
+        auto write_plane = [&](int slot, int wp, const u32x4 (&st)[C::MAXCH]) {
             unsigned char *sb = smem + C::GUARD + slot * C::SLOT;
 #pragma unroll
             for (int k = 0; k < C::MAXCH; ++k) {
-                if (lo8[k] != 0xffffu) {
+                if (pk[k] & (1u << (16 + wp))) {
+                    const unsigned o = (pk[k] & 0xffffu) * 8;
                     u32x2 lo = {st[k][0], st[k][1]}, hi = {st[k][2], st[k][3]};
-                    *reinterpret_cast<u32x2 *>(sb + lo8[k] * 8) = lo;
-                    *reinterpret_cast<u32x2 *>(sb + lo8[k] * 8 + 8) = hi;
+                    *reinterpret_cast<u32x2 *>(sb + o) = lo;
+                    *reinterpret_cast<u32x2 *>(sb + o + 8) = hi;
                 }
             }
         };
@@ -263,12 +271,12 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3), 2) void k_lookup_tile(Looku
         ZRun<n> zp[NU + 1];       // z-lerped columns of the lower plane of the current row
         load_plane(0, st[0]);
         load_plane(1, st[1]);
-        write_plane(0, st[0]);
+        write_plane(0, 0, st[0]);
         load_plane(2, st[0]);
         __syncthreads();          // plane 0 in slot 0
 #pragma unroll
         for (int k = 0; k <= NU; ++k) lerp_col(0, k, zp[k]);
-        write_plane(1, st[1]);
+        write_plane(1, 1, st[1]);
         __syncthreads();          // plane 1 in slot 1
 #pragma unroll
         for (int a = 0; a < n; ++a) {
@@ -309,7 +317,7 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3), 2) void k_lookup_tile(Looku
                 zprev = zcur;
                 if (k == NU) zp[k] = zcur;
             }
-            if (a + 2 < NW) write_plane(a & 1, st[a & 1]);   // plane a+2 into the slot of plane a (read in row a-1)
+            if (a + 2 < NW) write_plane(a & 1, a + 2, st[a & 1]);   // plane a+2 into the slot of plane a (read in row a-1)
             __syncthreads();
         }
     };

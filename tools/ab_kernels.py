@@ -39,7 +39,8 @@ variants = a.variants.split(",")
 
 def apply(v):
     parts = v.split(":")
-    _lib.set_tuning("lookup_nt", 0)
+    for k, d in (("lookup_nt", 1), ("lookup_order", 1), ("lookup_ldpol", 0)):
+        _lib.set_tuning(k, d)
     _lib.set_tuning("lookup_variant", int(parts[0]))
     for kv in parts[1:]:
         k, val = kv.split("=")

@@ -23,6 +23,16 @@ if [ "${SKIP_BENCH:-0}" != "1" ]; then
   rc=$?; echo "bench rc=$rc"; cat "$OUT/bench.json"; tail -3 "$OUT/bench.err"
   if bad $rc; then echo "STOP after bench rc=$rc"; exit $rc; fi
 fi
+if [ "${SKIP_PMC:-0}" != "1" ]; then
+  cd /tmp
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/pmc_$c" -o run \
+        -- python "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --steps 2 --warmup 1 ${BENCH_ARGS:-} > "$GRAFT_REPO_ROOT/$OUT/pmc_$c.log" 2>&1
+    rc=$?; echo "pmc $c rc=$rc"
+    if [ $rc -ne 0 ]; then cd "$GRAFT_REPO_ROOT"; exit $rc; fi
+  done
+  cd "$GRAFT_REPO_ROOT"
+fi
 if [ "${SKIP_PROF:-0}" != "1" ]; then
   cd /tmp
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run \
