@@ -10,7 +10,14 @@ lookup.  One step = one RAFTDVC forward's worth of correlation work:
 value = 12 * (query voxels, all ranks) * steps / wall time (whole job).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...   (query voxels sharded by H slabs)
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Multi-GPU: the units are voxel-queries and they are independent.
+Default --scaling weak: every rank owns its own volume pair (global batch = N),
+so per-GPU work is fixed and there is no data-path collective (only the
+timing barrier / max-reduce).  --scaling strong shards ONE pair's query voxels
+by H slabs (ShardedCorrBlock: one RCCL all-gather of the fmap2 slabs per
+forward), the north star's layout for 256^3 inputs (--size 64).
 
 Prints one JSON line (rank 0) with roofline (dominant kernel, HIP-event timed
 on its stream) and cpu_baseline (oracle/torch_cpu.py on the host, rank 0, N=1).
@@ -46,7 +53,11 @@ def parse():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--impl", default="materialised", choices=["materialised", "fused"])
     ap.add_argument("--max-flow", type=float, default=2.0)
-    ap.add_argument("--gather-output", action="store_true", help="N>1: all-gather every lookup output")
+    ap.add_argument("--gather-output", action="store_true", help="strong scaling: all-gather every lookup output")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm); gloo only for rehearsals")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="N>1: weak = one volume pair per rank (global batch N); strong = one pair's query "
+                         "voxels sharded by H slabs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=4096, help="query rows of the bounded CPU sample")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
@@ -112,29 +123,36 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    if os.environ.get("DVCCORR_BENCH_ONE_DEVICE") == "1":   # rehearsal of N ranks on a 1-GPU box
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if dist:
         import torch.distributed as tdist
-        tdist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            tdist.init_process_group("nccl", device_id=dev)
+        else:
+            tdist.init_process_group(args.dist_backend)
     import dvccorr
     from dvccorr import ops
-    from dvccorr.sharded import ShardedCorrBlock, slab_bounds
+    from dvccorr.sharded import LOCAL, ShardedCorrBlock, slab_bounds
 
     S, C, L, R = args.size, args.channels, args.levels, args.radius
     B = 1
-    g = torch.Generator(device="cpu").manual_seed(1234)
+    strong = args.scaling == "strong" and dist
+    # weak scaling: each rank's own pair (seeded by rank); strong: every rank generates the same pair
+    g = torch.Generator(device="cpu").manual_seed(1234 + (0 if strong else rank))
     f1 = torch.randn(B, C, S, S, S, generator=g)
     f2 = torch.randn(B, C, S, S, S, generator=g)
     base = dvccorr.coords_grid_3d(B, S, S, S, torch.device("cpu"))
     coords_list = [base + (torch.rand(B, 3, S, S, S, generator=g) * 2 - 1) * args.max_flow
                    for _ in range(args.iters)]
-    h0, h1 = slab_bounds(S, world, rank)
+    h0, h1 = slab_bounds(S, world, rank) if strong else (0, S)
     f1_slab = f1[:, :, h0:h1].contiguous().to(dev)
     f2_slab = f2[:, :, h0:h1].contiguous().to(dev)
     coords_slab = [c[:, :, h0:h1].contiguous().to(dev) for c in coords_list]
     nq_local = (h1 - h0) * S * S
-    nq_total = S * S * S
+    nq_total = S * S * S * (1 if strong else world)   # query voxels of the whole job
     lay = dvccorr.layout(S, S, S, L, C)
     dims = lay.levels()
     store_bytes = 2 if args.precision == "bf16" else 4
@@ -145,7 +163,7 @@ def main():
 
     def step(timed: bool):
         blk = ShardedCorrBlock(f1_slab, f2_slab, S, L, R, precision=args.precision, impl=args.impl,
-                               group=group, gather_output=args.gather_output,
+                               group=group if strong else LOCAL, gather_output=args.gather_output,
                                build_events=ev["build"] if timed else None)
         for i in range(args.iters):
             if timed:
@@ -172,7 +190,7 @@ def main():
         barrier()
         elapsed = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([elapsed], device=dev)
+        t = torch.tensor([elapsed], device=dev if args.dist_backend == "nccl" else "cpu")
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -187,19 +205,20 @@ def main():
     lk_bytes = sum(lookup_algorithmic_bytes(c, dims, R, store_bytes if args.impl == "materialised" else 0)
                    for c in coords_slab) / len(coords_slab)
     unpadded = sum(h * w * d for (h, w, d) in dims)
-    bd_bytes = nq_local * unpadded * store_bytes + 2 * C * 4 * nq_total
-    bd_flops = 2.0 * nq_local * nq_total * C
+    n_targets = S * S * S
+    bd_bytes = nq_local * unpadded * store_bytes + 2 * C * 4 * n_targets
+    bd_flops = 2.0 * nq_local * n_targets * C
     traffic = None
     if os.path.exists(args.traffic_file):
         try:
             tf = json.load(open(args.traffic_file))
-            key = f"{args.impl}_{args.precision}_{S}_L{L}_r{R}_n{world}"
+            key = f"{args.impl}_{args.precision}_{S}_L{L}_r{R}_n{world if strong else 1}"
             traffic = tf.get(key, {}).get("lookup_hbm_bytes_per_launch")
         except Exception:
             traffic = None
     if args.iters * lk_avg >= bd_avg or args.impl == "fused":
         achieved = lk_bytes / (lk_avg * 1e-3) / 1e9
-        roof = {"kernel": "k_lookup_win (dvc_corr_lookup)" if args.impl == "materialised" else
+        roof = {"kernel": "k_lookup_tile (dvc_corr_lookup)" if args.impl == "materialised" else
                 "k_fused_dots + k_lookup_win (dvc_corr_lookup_fused)",
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -221,13 +240,16 @@ def main():
             "metric": "corr build+lookup voxel-queries/s (128^3 pair, 1/4 encoder)",
             "value": value, "unit": "voxel-queries/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None,
+            "scaling": "strong" if strong else "weak", "vs_baseline": None,
             "dtype": "bf16" if args.precision == "bf16" else "f32",
             "data": "synthetic: N(0,1) feature maps, coords = identity + U(-2,2), 12 coord fields per step",
-            "config": {"workload": f"corr build + {args.iters} lookups, {S}^3 x {C} fmaps (128^3 input, 1/4 "
+            "config": {"workload": f"corr build + {args.iters} lookups, {S}^3 x {C} fmaps ({4 * S}^3 input, 1/4 "
                                    f"encoder), L={L}, r={R}, {args.impl}, {args.precision} build / fp32 lookup",
-                       "global_batch": B, "query_voxels": nq_total, "levels": L, "radius": R,
-                       "parallelism": f"query-voxel H-slabs x{world}" + (", output all-gather" if
+                       "global_batch": B if strong else B * world, "query_voxels": nq_total, "levels": L,
+                       "radius": R,
+                       "parallelism": (f"query-voxel H-slabs x{world}" if strong else
+                                       f"one volume pair per rank x{world} (no data-path collective)") +
+                                      (", output all-gather" if
                                                                           args.gather_output else "")},
             "roofline": roof,
             "build": build_info,

@@ -36,11 +36,18 @@ def slab_bounds(H: int, world: int, rank: int):
     return h0, h0 + base + (1 if rank < rem else 0)
 
 
+LOCAL = "local"   # group sentinel: this rank alone (data-parallel replicas, no collective)
+
+
 def _world(group) -> int:
+    if group == LOCAL:
+        return 1
     return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
 
 
 def _rank(group) -> int:
+    if group == LOCAL:
+        return 0
     return dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
 
 

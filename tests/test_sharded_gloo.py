@@ -119,3 +119,48 @@ def test_slab_bounds_partition():
             assert b[0][0] == 0 and b[-1][1] == H
             assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
             assert max(h1 - h0 for h0, h1 in b) - min(h1 - h0 for h0, h1 in b) <= 1
+
+
+def _weak_worker(rank, world, port, shape, L, R, q):
+    """bench.py --scaling weak: every rank owns its own pair; group=LOCAL must not shard or communicate."""
+    import sys
+    for p in (REPO, PKG, os.path.join(REPO, "tests")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import prng
+        from dvccorr.sharded import LOCAL, ShardedCorrBlock
+        B, C, H, W, D = shape
+        f1 = torch.from_numpy(prng.normal(51 + 10 * rank, shape))
+        f2 = torch.from_numpy(prng.normal(52 + 10 * rank, shape))
+        coords = torch.from_numpy(prng.flow_coords(53 + 10 * rank, B, H, W, D, 2.0))
+        blk = ShardedCorrBlock(f1, f2, H, L, R, False, precision="fp32", backend=TorchCpuRows, group=LOCAL)
+        assert (blk.world, blk.rank, blk.h0, blk.h1) == (1, 0, 0, H)
+        q.put((rank, blk(coords).numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_weak_scaling_replicas_are_independent():
+    from oracle import torch_cpu
+    import prng
+    world, shape, L, R = 2, (1, 8, 8, 8, 8), 2, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_weak_worker, args=(r, world, port, shape, L, R, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    B, C, H, W, D = shape
+    for r in range(world):
+        f1 = torch.from_numpy(prng.normal(51 + 10 * r, shape))
+        f2 = torch.from_numpy(prng.normal(52 + 10 * r, shape))
+        coords = torch.from_numpy(prng.flow_coords(53 + 10 * r, B, H, W, D, 2.0))
+        ref = torch_cpu.corr_lookup(f1, f2, coords, L, R, False).numpy()
+        np.testing.assert_allclose(results[r], ref, rtol=0, atol=2e-6 * np.abs(ref).max())
