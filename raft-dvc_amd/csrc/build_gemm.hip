@@ -22,6 +22,9 @@
 
 namespace dvc {
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
 // ----------------------------------------------------------------------------- bf16
 // tile: 128 queries x 128 columns, 256 threads (4 waves as 2 (cols) x 2 (queries)),
 // each wave 64 x 64 = 2 x 2 accumulators of v_mfma_f32_32x32x16_bf16.
@@ -35,6 +38,10 @@ constexpr int kBQ = 128, kBP = 128;
 __device__ __forceinline__ void asm_load16(u32x4 &dst, const void *p) {
     asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(p) : "memory");
 }
+// Same, from a wave-uniform base (SGPR pair) plus a 32-bit per-lane byte offset.
+__device__ __forceinline__ void asm_load16_s(u32x4 &dst, const void *base, int off) {
+    asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(dst) : "v"(off), "s"(base) : "memory");
+}
 // After the counted wait: make every prefetch register opaque at this point so no
 // consumer is scheduled above the wait (guide 5.7, form (ii)).
 template <int PF> struct PfTouch {
@@ -46,7 +53,8 @@ template <int PF> struct PfTouch {
 
 __device__ __forceinline__ int swz_mask(int nch) { return (nch >= 16 ? 16 : nch) - 1; }
 
-template <int NCH, bool STORE_F32>
+// ABL (diagnostics only, never the product path): 1 = skip the global stores, 2 = skip the MFMAs.
+template <int NCH, bool STORE_F32, int ABL>
 __global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict__ Q, const bf16_t *__restrict__ T,
                                                        bf16_t *__restrict__ corr, long long Nq, int Cp,
                                                        long long t_batch_rows, long long row_stride,
@@ -157,7 +165,10 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict_
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], bq[j][ks], acc[i][j], 0, 0, 0);
+                    if constexpr ((ABL & 2) == 0)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], bq[j][ks], acc[i][j], 0, 0, 0);
+                    else
+                        acc[i][j][0] += __builtin_bit_cast(float, __builtin_bit_cast(u32x4, a[i])[0]);
         }
         __syncthreads();   // sT reads done: reuse as staging
 
@@ -193,7 +204,8 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict_
                 const int q = id >> 4, c = id & 15;
                 const u32x4 v = sT[q * 16 + (c ^ (q & 15))];
                 const int off = (p0 + 8 * c < col_end) ? (int)(q * row_stride * 2 + c * 16) : 0x7ffffff0;
-                __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
+                if constexpr ((ABL & 1) != 0) asm volatile("" ::"v"(v));
+                else __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
             }
         } else {
             // float32 store of a bf16-input build: two passes of 64 queries each,
@@ -236,6 +248,179 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict_
             }
         }
     }
+}
+
+// ------------------------------------------------------- bf16 build, bf16 store, 2 barriers
+// Same tile, orientation and XCD-aware grid as k_build_bf16, restructured so one
+// column tile costs two barriers instead of four: the LDS holds the target tile T
+// and a separate staging image S (the query tile's LDS is S's space: the query
+// MFMA operands live in registers after the first barrier).
+//   [barrier A]  T(t) visible, S free
+//   MFMA on T(t); epilogue writes S
+//   [barrier B]  S visible, T(t) reads done
+//   S -> global stores (t); prefetched registers -> T (tile t+1); issue loads (t+2)
+// The loads for tile t+2 are in flight for a whole tile; the stores of tile t
+// drain during tile t+1.
+template <int NCH>
+__global__ __launch_bounds__(256, 2) void k_build_bf16_2b(const bf16_t *__restrict__ Q, const bf16_t *__restrict__ T,
+                                                          bf16_t *__restrict__ corr, long long Nq, int Cp,
+                                                          long long t_batch_rows, long long row_stride,
+                                                          long long col_begin, long long col_end, int nchunk,
+                                                          float scale, int stpol) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int nch = NCH;
+    constexpr int msk = (NCH >= 16 ? 16 : NCH) - 1;
+    constexpr int PF = kBP * NCH / 256;
+    u32x4 *sS = reinterpret_cast<u32x4 *>(smem);          // query tile, then the staging image
+    u32x4 *sT = sS + kBQ * (nch > 16 ? nch : 16);
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int b = blockIdx.z;
+    const long long qtile = blockIdx.x / nchunk;
+    const int chunk = blockIdx.x % nchunk;
+    const long long q0 = qtile * kBQ;
+    const bf16_t *Qb = Q + (long long)b * Nq * Cp;
+    const bf16_t *Tb = T + (long long)b * t_batch_rows * Cp;
+    const long long ncol_tiles = (col_end - col_begin + kBP - 1) / kBP;
+    const int wp = w & 1, wq = w >> 1;
+    const int h = lane >> 5, r32 = lane & 31;
+
+    for (int id = t; id < kBQ * nch; id += 256) {
+        const int row = id / nch, c = id - row * nch;
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (q0 + row < Nq) v = *reinterpret_cast<const u32x4 *>(Qb + (q0 + row) * Cp + c * 8);
+        sS[row * nch + (c ^ (row & msk))] = v;
+    }
+    // two register sets of prefetched target tiles: tile k+1's loads are issued two
+    // tiles ahead, before tile k-1's stores, so waiting for them leaves the stores of
+    // the last two tiles in flight
+    u32x4 pfa[PF], pfb[PF];
+    int toff[PF];   // byte offset of this thread's chunk i inside a target tile
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+        const int id = i * 256 + t;
+        toff[i] = ((id / nch) * Cp + (id % nch) * 8) * 2;
+    }
+    auto issue = [&](u32x4 (&pf)[PF], long long ct) {   // clamped: past the end it re-reads the last tile
+        const long long cc = ct < ncol_tiles ? ct : ncol_tiles - 1;
+        const bf16_t *tile = Tb + (col_begin + cc * kBP) * Cp;   // wave-uniform base
+#pragma unroll
+        for (int i = 0; i < PF; ++i) asm_load16_s(pf[i], tile, toff[i]);
+    };
+    auto put = [&](u32x4 (&pf)[PF]) {
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+            const int id = i * 256 + t;
+            const int row = id / nch, c = id % nch;
+            sT[row * nch + (c ^ (row & msk))] = pf[i];
+        }
+    };
+    if (chunk >= ncol_tiles) return;
+    issue(pfa, chunk);
+    issue(pfb, chunk + nchunk);
+    __syncthreads();   // query tile in LDS
+    bf16x8 bq[2][NCH / 2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < NCH / 2; ++ks) {
+            const int row = 64 * wq + 32 * j + r32;
+            const int c = 2 * ks + h;
+            bq[j][ks] = __builtin_bit_cast(bf16x8, sS[row * nch + (c ^ (row & msk))]);
+        }
+    constexpr int NSTORE = kBQ * 16 / 256;   // global stores per thread per tile
+    asm volatile("s_waitcnt vmcnt(%c0)" ::"i"(PF) : "memory");   // tile 0 landed (tile 1 may fly)
+    __builtin_amdgcn_sched_barrier(0);
+    PfTouch<PF>::touch(pfa);
+    put(pfa);
+    issue(pfa, chunk + 2 * nchunk);
+    const long long nrow = Nq - q0 < kBQ ? Nq - q0 : kBQ;
+    u32x2 *st = reinterpret_cast<u32x2 *>(sS);
+    const f32x2 sc2 = {scale, scale};
+    int soff[NSTORE];   // byte offset of this thread's store it inside the tile's rows
+#pragma unroll
+    for (int it = 0; it < NSTORE; ++it) {
+        const int id = it * 256 + t;
+        soff[it] = (int)((id >> 4) * row_stride * 2 + (id & 15) * 16);
+    }
+    // one column tile; `nxt` holds tile ct + nchunk (loaded two tiles ago), `fut`
+    // receives tile ct + 3 * nchunk after `nxt` is written to LDS
+    auto tile_step = [&](long long ct, u32x4 (&nxt)[PF], bool first) {
+        const long long p0 = col_begin + ct * kBP;
+        __syncthreads();   // A: T(ct) visible; the staging image's previous reads are done
+        f32x16 acc[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int k = 0; k < 16; ++k) acc[i][j][k] = 0.0f;
+#pragma unroll
+        for (int ks = 0; ks < NCH / 2; ++ks) {
+            const int c = 2 * ks + h;
+            bf16x8 a[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int row = 64 * wp + 32 * i + r32;
+                a[i] = __builtin_bit_cast(bf16x8, sT[row * nch + (c ^ (row & msk))]);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], bq[j][ks], acc[i][j], 0, 0, 0);
+        }
+        // staging [128 q][16 chunks of 8 cols] bf16, chunk' = chunk ^ (q & 15)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int q = 64 * wq + 32 * j + r32;
+                    const int pch = 8 * wp + 4 * i + g;
+                    // scale and round two columns at a time (v_pk_mul_f32 + v_cvt_pk_bf16_f32)
+                    const f32x2 lo = f32x2{acc[i][j][4 * g + 0], acc[i][j][4 * g + 1]} * sc2;
+                    const f32x2 hi = f32x2{acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]} * sc2;
+                    u32x2 v;
+                    v[0] = __builtin_bit_cast(unsigned, __builtin_convertvector(lo, bf16x2));
+                    v[1] = __builtin_bit_cast(unsigned, __builtin_convertvector(hi, bf16x2));
+                    st[(q * 16 + (pch ^ (q & 15))) * 2 + h] = v;
+                }
+        __syncthreads();   // B: staging visible; every wave is done reading T(ct)
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            corr + ((long long)b * Nq + q0) * row_stride + p0, (short)0,
+            (int)(nrow * row_stride * (long long)sizeof(bf16_t)), 0x00020000);
+#pragma unroll
+        for (int it = 0; it < NSTORE; ++it) {
+            const int id = it * 256 + t;
+            const int q = id >> 4, c = id & 15;
+            const u32x4 v = sS[q * 16 + (c ^ (q & 15))];
+            const int off = (p0 + 8 * c < col_end) ? soff[it] : 0x7ffffff0;
+            if (stpol) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 2);
+            else __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
+        }
+        // wait for `nxt` only: younger are the previous tile's stores (absent on the
+        // first tile), the other set's loads and this tile's stores
+        if (first) asm volatile("s_waitcnt vmcnt(%c0)" ::"i"(PF + NSTORE) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%c0)" ::"i"(PF + 2 * NSTORE) : "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        PfTouch<PF>::touch(nxt);
+        put(nxt);
+        issue(nxt, ct + 3 * nchunk);
+    };
+    // pfb holds tile chunk + nchunk, pfa tile chunk + 2 nchunk
+    long long ct = chunk;
+    bool first = true;
+    while (true) {
+        tile_step(ct, pfb, first);
+        first = false;
+        ct += nchunk;
+        if (ct >= ncol_tiles) break;
+        tile_step(ct, pfa, false);
+        ct += nchunk;
+        if (ct >= ncol_tiles) break;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no load left in flight at exit
 }
 
 // ----------------------------------------------------------------------------- f32
@@ -334,21 +519,34 @@ __global__ __launch_bounds__(256, 1) void k_build_f32(const float *__restrict__ 
     }
 }
 
-template __global__ void k_build_bf16<4, false>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+template __global__ void k_build_bf16<4, false, 0>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
                                                  long long, long long, long long, int, float);
-template __global__ void k_build_bf16<4, true>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+template __global__ void k_build_bf16<4, true, 0>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
                                                 long long, long long, long long, int, float);
-template __global__ void k_build_bf16<8, false>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+template __global__ void k_build_bf16<8, false, 0>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
                                                  long long, long long, long long, int, float);
-template __global__ void k_build_bf16<8, true>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+template __global__ void k_build_bf16<8, true, 0>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
                                                 long long, long long, long long, int, float);
-template __global__ void k_build_bf16<16, false>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+template __global__ void k_build_bf16<16, false, 0>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
                                                  long long, long long, long long, int, float);
-template __global__ void k_build_bf16<16, true>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+template __global__ void k_build_bf16<16, true, 0>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
                                                 long long, long long, long long, int, float);
-template __global__ void k_build_bf16<32, false>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+template __global__ void k_build_bf16<32, false, 0>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
                                                  long long, long long, long long, int, float);
-template __global__ void k_build_bf16<32, true>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+template __global__ void k_build_bf16<32, true, 0>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
                                                 long long, long long, long long, int, float);
+
+template __global__ void k_build_bf16_2b<4>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+                                            long long, long long, long long, int, float, int);
+template __global__ void k_build_bf16_2b<8>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+                                            long long, long long, long long, int, float, int);
+template __global__ void k_build_bf16_2b<16>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+                                             long long, long long, long long, int, float, int);
+template __global__ void k_build_bf16_2b<32>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+                                             long long, long long, long long, int, float, int);
+template __global__ void k_build_bf16<16, false, 1>(const bf16_t *, const bf16_t *, bf16_t *, long long, int,
+                                                    long long, long long, long long, long long, int, float);
+template __global__ void k_build_bf16<16, false, 2>(const bf16_t *, const bf16_t *, bf16_t *, long long, int,
+                                                    long long, long long, long long, long long, int, float);
 
 }  // namespace dvc

@@ -18,9 +18,12 @@ namespace dvc {
 __global__ void k_pool_fmap(const float *, float *, long long, int, int, int, int, int, int);
 template <typename T>
 __global__ void k_pack_rows(const float *, T *, int, int, long long, long long, int, int, long long, long long);
-template <int NCH, bool STORE_F32>
+template <int NCH, bool STORE_F32, int ABL>
 __global__ void k_build_bf16(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long, long long, long long,
                              long long, int, float);
+template <int NCH>
+__global__ void k_build_bf16_2b(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long, long long,
+                                long long, long long, int, float, int);
 __global__ void k_build_f32(const float *, const float *, float *, long long, int, long long, long long, long long,
                             long long, int, float);
 template <typename T>
@@ -43,6 +46,9 @@ static int g_lookup_ablate = 0;
 static int g_lookup_nt = 1;          // nontemporal output stores in the tile kernel
 static int g_lookup_order = 1;       // tile kernel level order (LookupArgs::order)
 static int g_lookup_ldpol = 0;       // tile kernel load cache policy (LookupArgs::ldpol)
+static int g_build_ablate = 0;       // diagnostics only: k_build_bf16 ablation instance
+static int g_build_stpol = 0;        // cache-policy bits of the build's output stores
+static int g_build_variant = 1;      // 1 = two-barrier bf16-store kernel (k_build_bf16_2b), 0 = k_build_bf16
 
 static int fail(int code, const char *fmt, ...) {
     va_list ap;
@@ -170,6 +176,19 @@ int dvc_set_tuning(const char *key, int value) {
     if (!strcmp(key, "lookup_ldpol")) {
         if (value < 0 || value > 3) return fail(DVC_ERR_INVALID, "set_tuning: lookup_ldpol %d", value);
         g_lookup_ldpol = value;
+        return DVC_OK;
+    }
+    if (!strcmp(key, "build_stpol")) {
+        g_build_stpol = value != 0;
+        return DVC_OK;
+    }
+    if (!strcmp(key, "build_variant")) {
+        if (value < 0 || value > 1) return fail(DVC_ERR_INVALID, "set_tuning: build_variant %d", value);
+        g_build_variant = value;
+        return DVC_OK;
+    }
+    if (!strcmp(key, "build_ablate")) {   // diagnostics only (outputs become invalid)
+        g_build_ablate = value;
         return DVC_OK;
     }
     if (!strcmp(key, "lookup_ablate")) {   // diagnostics only (outputs become invalid)
@@ -304,11 +323,33 @@ int dvc_corr_build(const void *packed_q, const void *packed_t, void *corr, int B
                                         lay.row_stride, lay.row_stride, col_begin, col_end, nchunk, scale);
         };
         const bool f32s = store_dtype == DVC_F32;
+        if (!f32s && g_build_variant == 1 && !g_build_ablate) {
+            const size_t lds2 = (size_t)128 * std::max(Cp, 128) * 2 + (size_t)128 * Cp * 2;
+            auto launch2 = [&](auto kern) {
+                (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                kern<<<grid, 256, lds2, s>>>((const bf16_t *)packed_q, (const bf16_t *)packed_t, (bf16_t *)corr, Nq,
+                                             Cp, lay.row_stride, lay.row_stride, col_begin, col_end, nchunk, scale,
+                                             g_build_stpol);
+            };
+            switch (Cp / 8) {
+            case 4: launch2(k_build_bf16_2b<4>); break;
+            case 8: launch2(k_build_bf16_2b<8>); break;
+            case 16: launch2(k_build_bf16_2b<16>); break;
+            case 32: launch2(k_build_bf16_2b<32>); break;
+            default: return fail(DVC_ERR_UNSUPPORTED, "build: C=%d not supported on the bf16 path", C);
+            }
+            return check_launch("corr_build");
+        }
+        if (g_build_ablate && Cp == 128 && !f32s) {   // diagnostics only
+            if (g_build_ablate == 1) launch(k_build_bf16<16, false, 1>);
+            else launch(k_build_bf16<16, false, 2>);
+            return check_launch("corr_build");
+        }
         switch (Cp / 8) {
-        case 4: f32s ? launch(k_build_bf16<4, true>) : launch(k_build_bf16<4, false>); break;
-        case 8: f32s ? launch(k_build_bf16<8, true>) : launch(k_build_bf16<8, false>); break;
-        case 16: f32s ? launch(k_build_bf16<16, true>) : launch(k_build_bf16<16, false>); break;
-        case 32: f32s ? launch(k_build_bf16<32, true>) : launch(k_build_bf16<32, false>); break;
+        case 4: f32s ? launch(k_build_bf16<4, true, 0>) : launch(k_build_bf16<4, false, 0>); break;
+        case 8: f32s ? launch(k_build_bf16<8, true, 0>) : launch(k_build_bf16<8, false, 0>); break;
+        case 16: f32s ? launch(k_build_bf16<16, true, 0>) : launch(k_build_bf16<16, false, 0>); break;
+        case 32: f32s ? launch(k_build_bf16<32, true, 0>) : launch(k_build_bf16<32, false, 0>); break;
         default: return fail(DVC_ERR_UNSUPPORTED, "build: C=%d not supported on the bf16 path", C);
         }
     } else if (in_dtype == DVC_F32) {
