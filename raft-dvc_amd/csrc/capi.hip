@@ -33,8 +33,8 @@ template <typename T> __global__ void k_lookup_generic(LookupArgs);
 template <typename T, int R, bool NT, int ABL> __global__ void k_lookup_tile(LookupArgs);
 __global__ void k_sample3d(const float *, const float *, float *, int, int, int, int, int, long long, int);
 int fused_lookup(const void *packed_q, const void *packed_t, const float *coords, float *out, void *workspace, int B,
-                 long long Nq, int C, const dvc_layout &lay, int radius, int convention, int dtype, hipStream_t s,
-                 char *err, size_t errlen);
+                 long long Nq, int C, const dvc_layout &lay, int radius, int convention, int dtype, int variant,
+                 hipStream_t s, char *err, size_t errlen);
 size_t fused_workspace_bytes(int B, long long Nq, int L, int radius);
 }  // namespace dvc
 
@@ -49,6 +49,7 @@ static int g_lookup_ldpol = 0;       // tile kernel load cache policy (LookupArg
 static int g_build_ablate = 0;       // diagnostics only: k_build_bf16 ablation instance
 static int g_build_stpol = 0;        // cache-policy bits of the build's output stores
 static int g_build_variant = 1;      // 1 = two-barrier bf16-store kernel (k_build_bf16_2b), 0 = k_build_bf16
+static int g_fused_variant = 1;      // 1 = MFMA tile kernel (k_fused_tile) where it applies, 0 = two-stage VALU
 
 static int fail(int code, const char *fmt, ...) {
     va_list ap;
@@ -185,6 +186,11 @@ int dvc_set_tuning(const char *key, int value) {
     if (!strcmp(key, "build_variant")) {
         if (value < 0 || value > 1) return fail(DVC_ERR_INVALID, "set_tuning: build_variant %d", value);
         g_build_variant = value;
+        return DVC_OK;
+    }
+    if (!strcmp(key, "fused_variant")) {
+        if (value < 0 || value > 1) return fail(DVC_ERR_INVALID, "set_tuning: fused_variant %d", value);
+        g_fused_variant = value;
         return DVC_OK;
     }
     if (!strcmp(key, "build_ablate")) {   // diagnostics only (outputs become invalid)
@@ -448,7 +454,7 @@ int dvc_corr_lookup_fused(const void *packed_q, const void *packed_t, const floa
         return fail(DVC_ERR_INVALID, "lookup_fused: bad convention %d", convention);
     if (dtype != DVC_BF16 && dtype != DVC_F32) return fail(DVC_ERR_INVALID, "lookup_fused: bad dtype %d", dtype);
     return fused_lookup(packed_q, packed_t, coords, out, workspace, B, Nq, C, lay, radius, convention, dtype,
-                        (hipStream_t)stream, g_err, sizeof(g_err));
+                        g_fused_variant, (hipStream_t)stream, g_err, sizeof(g_err));
 }
 
 int dvc_sample3d(const float *vol, const float *pts, float *out, int B, int C, int Hv, int Wv, int Dv, int64_t Nq,

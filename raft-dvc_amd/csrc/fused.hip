@@ -185,9 +185,34 @@ static void fused_level(int R, const T *Q, const T *Tt, LookupArgs &A, float *ws
     }
 }
 
+template <int R, int NCH>
+__global__ void k_fused_tile(const bf16_t *, const bf16_t *, LookupArgs, int, long long, int, int, int, float);
+
+// The MFMA tile kernel (fused_tile.hip) covers bf16, r <= 4, C <= 256, whole (y, x)
+// planes of queries (Nq a multiple of W*D: the full grid or an H-slab of it) and
+// packed targets addressable with 32-bit byte offsets.
+static bool fused_tile_ok(long long Nq, int W, int D, int Cp, long long t_rows, int radius, int dtype) {
+    return dtype == DVC_BF16 && radius >= 1 && radius <= 4 && (Cp == 32 || Cp == 64 || Cp == 128 || Cp == 256) &&
+           Nq % ((long long)W * D) == 0 &&
+           t_rows * Cp * 2 < (1LL << 31) - 65536;
+}
+
+template <int R>
+static void launch_fused_tile(const bf16_t *Q, const bf16_t *Tt, const LookupArgs &A, int Cp, long long t_rows,
+                              int Hq, int Wq, int Dq, float scale, hipStream_t s) {
+    const long long tiles = (long long)A.B * ((Hq + 1) / 2) * ((Wq + 1) / 2) * ((Dq + 15) / 16);
+    const unsigned grid = (unsigned)tiles;
+    switch (Cp / 8) {
+    case 4: k_fused_tile<R, 4><<<grid, 256, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;
+    case 8: k_fused_tile<R, 8><<<grid, 256, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;
+    case 16: k_fused_tile<R, 16><<<grid, 256, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;
+    default: k_fused_tile<R, 32><<<grid, 256, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;
+    }
+}
+
 int fused_lookup(const void *packed_q, const void *packed_t, const float *coords, float *out, void *workspace, int B,
-                 long long Nq, int C, const dvc_layout &lay, int radius, int convention, int dtype, hipStream_t s,
-                 char *err, size_t errlen) {
+                 long long Nq, int C, const dvc_layout &lay, int radius, int convention, int dtype, int variant,
+                 hipStream_t s, char *err, size_t errlen) {
     const int Cp = lay.c_pad;
     if ((dtype == DVC_BF16 && Cp > 512) || (dtype == DVC_F32 && Cp > 256)) {
         snprintf(err, errlen, "lookup_fused: C=%d too large", C);
@@ -198,7 +223,8 @@ int fused_lookup(const void *packed_q, const void *packed_t, const float *coords
         snprintf(err, errlen, "lookup_fused: Nq=%lld too large for 32-bit output offsets", Nq);
         return DVC_ERR_UNSUPPORTED;
     }
-    if (win_ok && !workspace) {
+    const bool tile = variant == 1 && fused_tile_ok(Nq, lay.W[0], lay.D[0], Cp, lay.row_stride, radius, dtype);
+    if (win_ok && !tile && !workspace) {
         snprintf(err, errlen, "lookup_fused: workspace required (%zu bytes)", fused_workspace_bytes(B, Nq, 0, radius));
         return DVC_ERR_INVALID;
     }
@@ -215,6 +241,31 @@ int fused_lookup(const void *packed_q, const void *packed_t, const float *coords
         A.zero[l] = lay.zero_level[l]; A.off[l] = lay.offset[l];
         A.generic[l] = 0;   // the fused path routes these levels to k_fused_generic itself
     }
+    if (tile) {
+        // one launch for every level; legacy levels with W != D go to k_fused_generic below
+        LookupArgs T = A;
+        T.q0 = 0; T.nq = Nq; T.nqb = (Nq + 63) / 64; T.l0 = 0; T.nl = lay.num_levels;
+        bool any_generic = false;
+        for (int l = 0; l < lay.num_levels; ++l) {
+            T.generic[l] = T.legacy && lay.W[l] != lay.D[l];
+            any_generic |= T.generic[l] && !T.zero[l];
+        }
+        const int Wq = lay.W[0], Dq = lay.D[0];
+        const int Hq = (int)(Nq / ((long long)Wq * Dq));
+        const bf16_t *Q = (const bf16_t *)packed_q, *Tt = (const bf16_t *)packed_t;
+        switch (radius) {
+        case 1: launch_fused_tile<1>(Q, Tt, T, Cp, lay.row_stride, Hq, Wq, Dq, scale, s); break;
+        case 2: launch_fused_tile<2>(Q, Tt, T, Cp, lay.row_stride, Hq, Wq, Dq, scale, s); break;
+        case 3: launch_fused_tile<3>(Q, Tt, T, Cp, lay.row_stride, Hq, Wq, Dq, scale, s); break;
+        default: launch_fused_tile<4>(Q, Tt, T, Cp, lay.row_stride, Hq, Wq, Dq, scale, s); break;
+        }
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) {
+            snprintf(err, errlen, "lookup_fused(tile): %s", hipGetErrorString(e));
+            return DVC_ERR_LAUNCH;
+        }
+        if (!any_generic) return DVC_OK;
+    }
     for (long long q0 = 0; q0 < Nq; q0 += kFusedChunk) {
         A.q0 = q0;
         A.nq = std::min(kFusedChunk, Nq - q0);
@@ -222,6 +273,7 @@ int fused_lookup(const void *packed_q, const void *packed_t, const float *coords
         for (int l = 0; l < lay.num_levels; ++l) {
             A.l0 = l;
             const bool generic = !win_ok || (A.legacy && lay.W[l] != lay.D[l]);
+            if (tile && !generic) continue;   // done by k_fused_tile
             if (generic) {
                 const long long total = (long long)B * A.nq * n3;
                 if (dtype == DVC_BF16)

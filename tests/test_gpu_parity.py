@@ -291,3 +291,70 @@ def test_tile_kernel_matches_walk(shape, L, r):
                                                         float((outs[0] - outs[1]).abs().max()))
     finally:
         _lib.set_tuning("lookup_variant", 2)
+
+
+@pytest.mark.parametrize("shape,C,L,r", [((9, 7, 5), 32, 2, 1), ((12, 10, 16), 64, 3, 2), ((16, 16, 16), 32, 4, 3),
+                                         ((20, 13, 24), 128, 3, 4), ((32, 32, 32), 128, 4, 4),
+                                         ((18, 34, 40), 64, 2, 4), ((8, 8, 8), 256, 2, 3)])
+def test_fused_tile_matches_materialised(shape, C, L, r):
+    """k_fused_tile (MFMA window dots of the union window, no volume) reproduces the bf16 materialised
+    pyramid + lookup bit for bit: the same v_mfma_f32_32x32x16_bf16 dot order, the same scale-then-round to
+    bf16, the same interpolation arithmetic.  Ragged query boxes, non-cubic sizes, flows wide enough to
+    push the union window past 32 z-rows, NaN / huge coordinates, both conventions.  Legacy levels with
+    W != D go to the per-output kernel (fp32 dots of the same operands) and are held to BF16_TOL."""
+    import dvccorr
+    from dvccorr import _lib
+    H, W, D = shape
+    g = torch.Generator(device="cpu").manual_seed(H * 1000 + W * 10 + D + r + C)
+    f1 = torch.randn(1, C, H, W, D, generator=g).to(DEV)
+    f2 = torch.randn(1, C, H, W, D, generator=g).to(DEV)
+    base = dvccorr.coords_grid_3d(1, H, W, D, torch.device("cpu"))
+    c = base + (torch.rand(1, 3, H, W, D, generator=g) * 2 - 1) * (r + 6)
+    c.view(3, -1)[:, 5] = float("nan")
+    c.view(3, -1)[1, 17] = 1e30
+    c.view(3, -1)[2, 23] = -float("inf")
+    c = c.to(DEV)
+    lay = dvccorr.layout(H, W, D, L, C)
+    n3 = (2 * r + 1) ** 3
+    for legacy in (False, True):
+        ref = dvccorr.CorrBlock(f1, f2, L, r, legacy_wd_swap=legacy, precision="bf16")(c)
+        fz = dvccorr.CorrBlockFused(f1, f2, L, r, legacy_wd_swap=legacy, precision="bf16")
+        _lib.set_tuning("fused_variant", 1)
+        out = fz(c)
+        _lib.set_tuning("fused_variant", 0)
+        try:
+            two_stage = fz(c)
+        finally:
+            _lib.set_tuning("fused_variant", 1)
+        torch.cuda.synchronize()
+        assert torch.isfinite(out).all()
+        for l, (h, w, d) in enumerate(lay.levels()):
+            sl = slice(l * n3, (l + 1) * n3)
+            if legacy and w != d and min(h, w, d) > 1:
+                e = orc.rel_err(out[:, sl].cpu().numpy(), ref[:, sl].cpu().numpy())
+                assert e <= BF16_TOL, (shape, l, legacy, e)
+            else:
+                assert torch.equal(out[:, sl], ref[:, sl]), (shape, C, L, r, l, legacy,
+                                                             float((out[:, sl] - ref[:, sl]).abs().max()))
+        assert orc.rel_err(out.cpu().numpy(), two_stage.cpu().numpy()) <= BF16_TOL
+
+
+def test_fused_tile_slab():
+    """The tile kernel on one rank's H-slab of queries (Nq = slab planes x W x D) equals the slab of the
+    whole-grid result (the sharded layout of SURVEY 8(e))."""
+    import dvccorr
+    from dvccorr import ops
+    H, W, D, C, L, r = 24, 20, 18, 64, 3, 4
+    g = torch.Generator(device="cpu").manual_seed(5)
+    f1 = torch.randn(1, C, H, W, D, generator=g).to(DEV)
+    f2 = torch.randn(1, C, H, W, D, generator=g).to(DEV)
+    c = (dvccorr.coords_grid_3d(1, H, W, D, torch.device("cpu")) +
+         (torch.rand(1, 3, H, W, D, generator=g) * 2 - 1) * 3).to(DEV)
+    dt = ops.dtype_code("bf16")
+    t = ops.pack_targets(f2, L, dt)
+    full = ops.lookup_fused(ops.pack_queries(f1.reshape(1, C, -1), dt), t, c.reshape(1, 3, -1), C, H, W, D, L, r,
+                            False, dt)
+    h0, h1 = 7, 15
+    q = ops.pack_queries(f1[:, :, h0:h1].reshape(1, C, -1), dt)
+    part = ops.lookup_fused(q, t, c[:, :, h0:h1].reshape(1, 3, -1), C, H, W, D, L, r, False, dt)
+    assert torch.equal(part, full.view(1, -1, H, W, D)[:, :, h0:h1].reshape(1, -1, (h1 - h0) * W * D))
