@@ -96,7 +96,8 @@ def cpu_baseline(args, f1, f2, coords_list):
     f1c, f2c = f1.float().cpu(), f2.float().cpu()
     cc = [c.cpu() for c in coords_list]
     N = f1c[0, 0].numel()
-    rows = min(args.cpu_rows, N)
+    # the restatement materialises rows x N fp32 per level: cap it near 512 MB (128^3 fmaps: 64 rows)
+    rows = min(args.cpu_rows, N, max(16, (1 << 27) // N))
     q0, q1 = 0, rows
     pyr = torch_cpu.build_rows(f1c, f2c, args.levels, q0, q1)           # warmup (allocations)
     torch_cpu.lookup_rows(pyr, cc[0], args.radius, False, q0, q1)

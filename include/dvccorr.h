@@ -19,6 +19,9 @@
  *   dvc_corr_lookup        -- CorrBlock.__call__                              src/core/corr.py:169-208
  *   dvc_corr_lookup_fused  -- CorrBlockOnTheFly.__call__ (any convention)     src/core/corr_otf.py:96-138,
  *                             / the CUDA OTF forward_one_level* launchers     src/core/cuda/corr_otf_cuda.cu:448-488
+ *   dvc_corr_backward      -- autograd backward of CorrBlock (matmul,        src/core/corr.py:141-208;
+ *                             avg_pool3d, grid_sample) / the CUDA OTF         src/core/cuda/corr_otf_cuda.cu:247-441,
+ *                             backward launcher                               :491-530
  *   dvc_sample3d           -- bilinear_sampler_3d                             src/core/corr.py:17-68
  *
  * Layouts (row-major, element counts):
@@ -121,6 +124,20 @@ size_t dvc_lookup_fused_workspace_bytes(int B, int64_t Nq, int num_levels, int r
 int dvc_corr_lookup_fused(const void *packed_q, const void *packed_t, const float *coords, float *out,
                           void *workspace, int B, int64_t Nq, int C, int H, int W, int D, int num_levels,
                           int radius, int convention, int dtype, void *stream);
+
+/* Backward of dvc_corr_lookup / dvc_corr_lookup_fused w.r.t. both feature maps
+ * (autograd through corr.py:141-208; coords get no gradient, raft_dvc.py:441):
+ *   grad_out   (B, L*(2r+1)^3, Nq) float32   gradient of the lookup output
+ *   grad_fmap1 (B, C, Nq) float32            overwritten
+ *   grad_fmap2 (B, C, H, W, D) float32       overwritten (these Nq queries' contribution)
+ * packed_q / packed_t are the forward's packed operands (dtype).  No atomics: every
+ * sum runs in a fixed order, so results are bitwise reproducible.  Supported:
+ * radius 1..6, c_pad <= 128, Nq a multiple of W*D, and for the legacy convention
+ * W == D at every non-zero level (DVC_ERR_UNSUPPORTED otherwise). */
+size_t dvc_corr_backward_workspace_bytes(int B, int64_t Nq, int C, int H, int W, int D, int num_levels, int radius);
+int dvc_corr_backward(const void *packed_q, const void *packed_t, const float *coords, const float *grad_out,
+                      float *grad_fmap1, float *grad_fmap2, void *workspace, int B, int64_t Nq, int C, int H, int W,
+                      int D, int num_levels, int radius, int convention, int dtype, void *stream);
 
 /* bilinear_sampler_3d: vol (B, C, Hv, Wv, Dv), pts (B, Nq, 3) in (h, w, d) -> out (B, C, Nq). */
 int dvc_sample3d(const float *vol, const float *pts, float *out, int B, int C, int Hv, int Wv, int Dv, int64_t Nq,

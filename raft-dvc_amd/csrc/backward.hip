@@ -1,0 +1,610 @@
+// backward.hip -- gradient of the correlation lookup w.r.t. both feature maps.
+//
+// Reference semantics: autograd through src/core/corr.py:141-208 (matmul / sqrt(C),
+// the avg_pool3d pyramid, the grid_sample lookup); coordinates get no gradient
+// (raft_dvc.py:441 detaches them).  The reference's CUDA design
+// (src/core/cuda/corr_otf_cuda.cu:247-441) scatters every sample into grad_fmap2 with
+// per-channel atomics; here nothing is atomic and no dense d(corr) is formed --
+// memory is O(C * voxels + Nq * (2r+2)^3):
+//
+//   k_win_grad    dwin[b][l][q][i][j][k]: the transpose of the lookup's separable
+//                 interpolation, i.e. each query's gradient on the (2r+2)^3 integer
+//                 window of every level (lane = query);
+//   k_grad_q      dQ[q] = s * sum_l sum_{p in win_l(q)} dwin[q][p - o_q] * T_l[p]:
+//                 one workgroup per 4x4x4 query box, lane = channel pair, the four
+//                 waves splitting the rows of the union of the box's windows;
+//   k_bw_keys + rocprim radix sort + k_cell_starts: the queries of one (b, l) in
+//                 window-origin order (key = origin cell << 32 | q is unique, so the
+//                 order is deterministic);
+//   k_grad_t      dT_l[p] = s * sum_{q : p in win_l(q)} dwin[q][p - o_q] * Q[q]:
+//                 one workgroup per 4x4x4 target brick, streaming the queries whose
+//                 window origins can reach it (contiguous key ranges, query order);
+//   k_unpack_sum  dfmap1 (B, C, Nq) <- dQ, and dfmap2 (B, C, H, W, D) <- sum_l 8^-l dT_l
+//                 (the adjoint of the floor-mode 2x2x2 avg_pool3d pyramid).
+// Every sum runs in a fixed order, so the result is bitwise reproducible.
+#include <stdio.h>
+
+#include <algorithm>
+
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include "common.h"
+#include "lookup_common.h"
+
+namespace dvc {
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+struct BwdArgs {
+    const float *coords;   // (B, 3, Nq)
+    const float *gout;     // (B, L*n^3, Nq)
+    float *gwin;           // [B][L][Nq][NW^3]
+    long long Nq, row_stride;
+    int B, L, legacy, Hq, Wq, Dq, Cp;
+    int H[DVC_MAX_LEVELS], W[DVC_MAX_LEVELS], D[DVC_MAX_LEVELS], Dp[DVC_MAX_LEVELS], zero[DVC_MAX_LEVELS];
+    long long off[DVC_MAX_LEVELS];
+    float scale;
+};
+
+__device__ __forceinline__ int bw_wave_min(int v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = min(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ int bw_wave_max(int v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return v;
+}
+
+// the forward's window geometry of coords / 2^l (corr.py:197)
+__device__ __forceinline__ void bw_axes(const BwdArgs &A, int l, float cy, float cx, float cz, WinAxes &ax) {
+    const float sc = (float)(1 << l);
+    window_axes(cy / sc, cx / sc, cz / sc, A.H[l], A.W[l], A.D[l], A.legacy, ax);
+}
+
+template <typename TT> __device__ __forceinline__ f32x2 load2(const TT *p);
+template <> __device__ __forceinline__ f32x2 load2<float>(const float *p) { return *reinterpret_cast<const f32x2 *>(p); }
+template <> __device__ __forceinline__ f32x2 load2<bf16_t>(const bf16_t *p) {
+    const unsigned u = *reinterpret_cast<const unsigned *>(p);
+    return f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+}
+
+// ---------------------------------------------------------------------------------
+// 1. window gradients.  Forward (lookup_tile.hip / lookup.hip): output (a, u, v) of a
+// level = sum over corners of wy[a] * wx[u] * wz[v] * win[a+dy][u+dx][v+dz] with the
+// per-axis weights of axis_weights() zeroed outside the level.  Its transpose, per
+// window plane i and column j, combines output rows a in {i, i-1} and columns
+// u in {j, j-1}, then spreads each v over window z in {v, v+1}.
+// ---------------------------------------------------------------------------------
+template <int R>
+__global__ __launch_bounds__(256) void k_win_grad(BwdArgs A) {
+    constexpr int n = 2 * R + 1, NW = 2 * R + 2, NW3 = NW * NW * NW;
+    const int lane = threadIdx.x & 63;
+    const long long nqb = (A.Nq + 63) / 64;
+    const long long item = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (item >= (long long)A.B * A.L * nqb) return;
+    const int bl = (int)(item / nqb);
+    const int l = bl % A.L, b = bl / A.L;
+    const long long q = (item - (long long)bl * nqb) * 64 + lane;
+    if (q >= A.Nq) return;
+    float *gw = A.gwin + ((long long)bl * A.Nq + q) * NW3;
+    if (A.zero[l]) {   // a size-1 level samples zeros (corr.py:41-44): no gradient reaches it
+        for (int i = 0; i < NW3; i += 2) *reinterpret_cast<f32x2 *>(gw + i) = f32x2{0.0f, 0.0f};
+        return;
+    }
+    const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l];
+    float cy, cx, cz;
+    load_coords(A.coords, b, A.Nq, q, cy, cx, cz);
+    WinAxes ax;
+    bw_axes(A, l, cy, cx, cz, ax);
+    const int ih = (int)ax.kh - R, iu = (int)ax.ku - R, iv = (int)ax.kv - R;
+    float wx0[n], wx1[n], wz0[n], wz1[n];
+#pragma unroll
+    for (int t = 0; t < n; ++t) {
+        axis_weights(ax.pu, ax.ku, t - R, ax.un, ax.uu, wx0[t], wx1[t]);
+        wx0[t] = (unsigned)(iu + t) < (unsigned)Wl ? wx0[t] : 0.0f;
+        wx1[t] = (unsigned)(iu + t + 1) < (unsigned)Wl ? wx1[t] : 0.0f;
+        axis_weights(ax.pv, ax.kv, t - R, ax.vn, ax.vu, wz0[t], wz1[t]);
+        wz0[t] = (unsigned)(iv + t) < (unsigned)Dl ? wz0[t] : 0.0f;
+        wz1[t] = (unsigned)(iv + t + 1) < (unsigned)Dl ? wz1[t] : 0.0f;
+    }
+    const long long chu = A.legacy ? 1 : n, chv = A.legacy ? n : 1;
+    const float *g = A.gout + (long long)bl * n * n * n * A.Nq + q;
+    for (int i = 0; i < NW; ++i) {
+        // window plane i collects output row a = i (corner 0) and a = i - 1 (corner 1)
+        float wa0 = 0.0f, wa1 = 0.0f, t0, t1;
+        if (i < n) {
+            axis_weights(ax.ph, ax.kh, i - R, ax.hs, ax.hs, t0, t1);
+            wa0 = (unsigned)(ih + i) < (unsigned)Hl ? t0 : 0.0f;
+        }
+        if (i >= 1) {
+            axis_weights(ax.ph, ax.kh, i - 1 - R, ax.hs, ax.hs, t0, t1);
+            wa1 = (unsigned)(ih + i) < (unsigned)Hl ? t1 : 0.0f;
+        }
+        const float *g0 = g + (long long)i * n * n * A.Nq;         // output row a = i
+        const float *g1 = g + (long long)(i - 1) * n * n * A.Nq;   // output row a = i - 1
+        float Pp[n];
+#pragma unroll
+        for (int v = 0; v < n; ++v) Pp[v] = 0.0f;
+#pragma unroll
+        for (int j = 0; j < NW; ++j) {
+            float Pc[n];
+#pragma unroll
+            for (int v = 0; v < n; ++v) Pc[v] = 0.0f;
+            if (j < n) {
+                if (i < n) {
+#pragma unroll
+                    for (int v = 0; v < n; ++v) Pc[v] = wa0 * g0[(j * chu + v * chv) * A.Nq];
+                }
+                if (i >= 1) {
+#pragma unroll
+                    for (int v = 0; v < n; ++v) Pc[v] = __builtin_fmaf(wa1, g1[(j * chu + v * chv) * A.Nq], Pc[v]);
+                }
+            }
+            const float wj0 = j < n ? wx0[j < n ? j : 0] : 0.0f;
+            const float wj1 = j >= 1 ? wx1[j >= 1 ? j - 1 : 0] : 0.0f;
+            float o[NW];
+#pragma unroll
+            for (int k = 0; k < NW; ++k) o[k] = 0.0f;
+#pragma unroll
+            for (int v = 0; v < n; ++v) {
+                const float gz = __builtin_fmaf(wj0, Pc[v], wj1 * Pp[v]);
+                o[v] = __builtin_fmaf(wz0[v], gz, o[v]);
+                o[v + 1] = __builtin_fmaf(wz1[v], gz, o[v + 1]);
+            }
+            f32x2 *dst = reinterpret_cast<f32x2 *>(gw + (i * NW + j) * NW);
+#pragma unroll
+            for (int k = 0; k < NW / 2; ++k) dst[k] = f32x2{o[2 * k], o[2 * k + 1]};
+#pragma unroll
+            for (int v = 0; v < n; ++v) Pp[v] = Pc[v];
+        }
+    }
+}
+
+// Cross-wave sum of the four waves' 64 x (2 channels) partials: waves 2, 3 -> LDS ->
+// waves 0, 1; wave 1 -> LDS -> wave 0.  Fixed order (deterministic).  Every wave of the
+// block must call it.
+__device__ __forceinline__ void reduce4(f32x2 (&acc)[64], f32x2 (*red)[64][64], int w, int lane) {
+    __syncthreads();
+    if (w >= 2) {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) red[w - 2][i][lane] = acc[i];
+    }
+    __syncthreads();
+    if (w < 2) {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) acc[i] += red[w][i][lane];
+    }
+    __syncthreads();
+    if (w == 1) {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) red[0][i][lane] = acc[i];
+    }
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) acc[i] += red[0][i][lane];
+    }
+}
+
+// acc[i] += g[k][i] * v[k] for the KB partners staged in gs (broadcast LDS reads)
+template <int KB>
+__device__ __forceinline__ void fma_partners(f32x2 (&acc)[64], float (*gs)[64], const f32x2 (&v)[KB]) {
+#pragma unroll
+    for (int k = 0; k < KB; ++k)
+#pragma unroll
+        for (int i = 0; i < 64; i += 4) {
+            const float4 g4 = *reinterpret_cast<const float4 *>(&gs[k][i]);
+            acc[i + 0] = __builtin_elementwise_fma(f32x2{g4.x, g4.x}, v[k], acc[i + 0]);
+            acc[i + 1] = __builtin_elementwise_fma(f32x2{g4.y, g4.y}, v[k], acc[i + 1]);
+            acc[i + 2] = __builtin_elementwise_fma(f32x2{g4.z, g4.z}, v[k], acc[i + 2]);
+            acc[i + 3] = __builtin_elementwise_fma(f32x2{g4.w, g4.w}, v[k], acc[i + 3]);
+        }
+}
+
+constexpr int kBatch = 4;   // partners staged per LDS round
+
+// ---------------------------------------------------------------------------------
+// 2. dQ for one 4x4x4 box of queries (owner lane i = query i), summed over levels.
+// ---------------------------------------------------------------------------------
+template <typename TT, int R>
+__global__ __launch_bounds__(256) void k_grad_q(const TT *__restrict__ Tt, float *__restrict__ dQ, BwdArgs A) {
+    constexpr int NW = 2 * R + 2, NW3 = NW * NW * NW;
+    __shared__ __attribute__((aligned(16))) float gs_all[4][kBatch][64];
+    __shared__ __attribute__((aligned(16))) f32x2 red[2][64][64];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float (*gs)[64] = gs_all[w];
+    const int nbz = (A.Dq + 3) >> 2, nbx = (A.Wq + 3) >> 2, nby = (A.Hq + 3) >> 2;
+    int t = blockIdx.x;
+    const int bz = t % nbz; t /= nbz;
+    const int bx = t % nbx; t /= nbx;
+    const int by = t % nby;
+    const int b = t / nby;
+    const int qy = by * 4 + (lane >> 4), qx = bx * 4 + ((lane >> 2) & 3), qz = bz * 4 + (lane & 3);
+    const bool active = qy < A.Hq && qx < A.Wq && qz < A.Dq;
+    const long long q = active ? ((long long)qy * A.Wq + qx) * A.Dq + qz : 0;
+    float cy = 0.0f, cx = 0.0f, cz = 0.0f;
+    if (active) load_coords(A.coords, b, A.Nq, q, cy, cx, cz);
+    const int c0 = 2 * lane;
+    const bool cok = c0 < A.Cp;
+    f32x2 acc[64];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) acc[i] = f32x2{0.0f, 0.0f};
+    const int BIG = 1 << 29;
+    for (int l = 0; l < A.L; ++l) {
+        if (A.zero[l]) continue;
+        const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
+        WinAxes ax;
+        bw_axes(A, l, cy, cx, cz, ax);
+        const int ih = (int)ax.kh - R, iu = (int)ax.ku - R, iv = (int)ax.kv - R;
+        const bool live = active && !ax.dead;
+        const int ys = max(bw_wave_min(live ? ih : BIG), 0), ye = min(bw_wave_max(live ? ih : -BIG) + NW - 1, Hl - 1);
+        const int xs = max(bw_wave_min(live ? iu : BIG), 0), xe = min(bw_wave_max(live ? iu : -BIG) + NW - 1, Wl - 1);
+        const int nx = xe - xs + 1;
+        const int nrows = (ye >= ys && nx > 0) ? (ye - ys + 1) * nx : 0;
+        const float *gq = A.gwin + (((long long)b * A.L + l) * A.Nq + q) * NW3;
+        for (int row = w; row < nrows; row += 4) {
+            const int y = ys + row / nx, x = xs + row % nx;
+            const int wy = y - ih, wx = x - iu;
+            const bool rok = live && (unsigned)wy < (unsigned)NW && (unsigned)wx < (unsigned)NW;
+            if (__ballot(rok) == 0) continue;
+            const int zlo = max(bw_wave_min(rok ? iv : BIG), 0);
+            const int zhi = min(bw_wave_max(rok ? iv : -BIG) + NW - 1, Dl - 1);
+            const float *grow = gq + (wy * NW + wx) * NW;
+            const TT *trow = Tt + ((long long)b * A.row_stride + A.off[l] + ((long long)y * Wl + x) * Dpl) * A.Cp + c0;
+            for (int z = zlo; z <= zhi; z += kBatch) {
+                float g[kBatch];
+                f32x2 tv[kBatch];
+#pragma unroll
+                for (int k = 0; k < kBatch; ++k) {
+                    const int zz = z + k;
+                    const int wz = zz - iv;
+                    g[k] = (rok && zz <= zhi && (unsigned)wz < (unsigned)NW) ? grow[wz] : 0.0f;
+                    tv[k] = (cok && zz <= zhi) ? load2<TT>(trow + (long long)zz * A.Cp) : f32x2{0.0f, 0.0f};
+                }
+#pragma unroll
+                for (int k = 0; k < kBatch; ++k) gs[k][lane] = g[k];
+                __builtin_amdgcn_wave_barrier();
+                fma_partners<kBatch>(acc, gs, tv);
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+    }
+    reduce4(acc, red, w, lane);
+    if (w == 0 && cok) {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+            const int y = by * 4 + (i >> 4), x = bx * 4 + ((i >> 2) & 3), z = bz * 4 + (i & 3);
+            if (y < A.Hq && x < A.Wq && z < A.Dq) {
+                const long long qi = ((long long)y * A.Wq + x) * A.Dq + z;
+                *reinterpret_cast<f32x2 *>(dQ + ((long long)b * A.Nq + qi) * A.Cp + c0) =
+                    acc[i] * f32x2{A.scale, A.scale};
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// 3. queries of (b, l) keyed by window-origin cell: o' = origin + NW - 1 per axis, in
+// [0, S_l + NW - 2] exactly when the window meets the level; others sort last.
+// ---------------------------------------------------------------------------------
+template <int R>
+__global__ __launch_bounds__(256) void k_bw_keys(BwdArgs A, int b, int l, unsigned long long *__restrict__ keys) {
+    constexpr int NW = 2 * R + 2;
+    const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (q >= A.Nq) return;
+    float cy, cx, cz;
+    load_coords(A.coords, b, A.Nq, q, cy, cx, cz);
+    WinAxes ax;
+    bw_axes(A, l, cy, cx, cz, ax);
+    const int oy = (int)ax.kh - R + NW - 1, ox = (int)ax.ku - R + NW - 1, oz = (int)ax.kv - R + NW - 1;
+    const int CY = A.H[l] + NW - 1, CX = A.W[l] + NW - 1, CZ = A.D[l] + NW - 1;
+    const long long ncell = (long long)CY * CX * CZ;
+    const bool in = !ax.dead && (unsigned)oy < (unsigned)CY && (unsigned)ox < (unsigned)CX && (unsigned)oz < (unsigned)CZ;
+    const long long cell = in ? ((long long)oy * CX + ox) * CZ + oz : ncell;
+    keys[q] = ((unsigned long long)cell << 32) | (unsigned long long)(unsigned)q;
+}
+
+// starts[c] = first sorted index whose cell >= c, for c in [0, ncell]
+__global__ __launch_bounds__(256) void k_cell_starts(const unsigned long long *__restrict__ keys, long long Nq,
+                                                     long long ncell, int *__restrict__ starts) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i > Nq) return;
+    const long long prev = i > 0 ? (long long)(keys[i - 1] >> 32) : -1;
+    const long long cur = i < Nq ? min((long long)(keys[i] >> 32), ncell) : ncell;
+    for (long long c = prev + 1; c <= cur; ++c) starts[c] = (int)i;
+}
+
+// ---------------------------------------------------------------------------------
+// 4. dT_l for one 4x4x4 brick of level-l targets of batch element b (owner lane i =
+// target i), streaming the queries whose window origin cell lies in
+// [brick, brick + NW - 1] (per axis, in o' coordinates).
+// ---------------------------------------------------------------------------------
+template <typename TT, int R>
+__global__ __launch_bounds__(256) void k_grad_t(const TT *__restrict__ Qp, const unsigned long long *__restrict__ keys,
+                                                const int *__restrict__ starts, float *__restrict__ dT, BwdArgs A,
+                                                int b, int l) {
+    constexpr int NW = 2 * R + 2, NW3 = NW * NW * NW;
+    __shared__ __attribute__((aligned(16))) float gs_all[4][kBatch][64];
+    __shared__ __attribute__((aligned(16))) f32x2 red[2][64][64];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float (*gs)[64] = gs_all[w];
+    const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
+    const int nbz = (Dl + 3) >> 2, nbx = (Wl + 3) >> 2;
+    int t = blockIdx.x;
+    const int bz = t % nbz; t /= nbz;
+    const int bx = t % nbx;
+    const int by = t / nbx;
+    const int ty = by * 4 + (lane >> 4), tx = bx * 4 + ((lane >> 2) & 3), tz = bz * 4 + (lane & 3);
+    const bool tval = ty < Hl && tx < Wl && tz < Dl;
+    const int CX = Wl + NW - 1, CZ = Dl + NW - 1;
+    const int oy0 = by * 4, oy1 = min(by * 4 + 3, Hl - 1) + NW - 1;
+    const int ox0 = bx * 4, ox1 = min(bx * 4 + 3, Wl - 1) + NW - 1;
+    const int oz0 = bz * 4, oz1 = min(bz * 4 + 3, Dl - 1) + NW - 1;
+    const int nox = ox1 - ox0 + 1, nrows = (oy1 - oy0 + 1) * nox;
+    const int c0 = 2 * lane;
+    const bool cok = c0 < A.Cp;
+    const float *gl = A.gwin + ((long long)b * A.L + l) * A.Nq * NW3;
+    const TT *qb = Qp + (long long)b * A.Nq * A.Cp + c0;
+    f32x2 acc[64];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) acc[i] = f32x2{0.0f, 0.0f};
+    for (int row = w; row < nrows; row += 4) {
+        const int oy = oy0 + row / nox, ox = ox0 + row % nox;
+        const long long cbase = ((long long)oy * CX + ox) * CZ;
+        const int s = starts[cbase + oz0], e = starts[cbase + oz1 + 1];
+        // window position of this lane's target for a query of origin o' = (oy, ox, ozq)
+        const int py = ty - oy + NW - 1, px = tx - ox + NW - 1;
+        const bool yxok = tval && (unsigned)py < (unsigned)NW && (unsigned)px < (unsigned)NW;
+        for (int idx = s; idx < e; idx += kBatch) {
+            float g[kBatch];
+            f32x2 qv[kBatch];
+#pragma unroll
+            for (int k = 0; k < kBatch; ++k) {
+                const bool in = idx + k < e;
+                const unsigned long long key = keys[in ? idx + k : s];
+                const long long qq = (long long)(unsigned)(key & 0xffffffffu);
+                const int ozq = (int)((long long)(key >> 32) - cbase);
+                const int pz = tz - ozq + NW - 1;
+                const bool ok = in && yxok && (unsigned)pz < (unsigned)NW;
+                g[k] = ok ? gl[qq * NW3 + (py * NW + px) * NW + pz] : 0.0f;
+                qv[k] = (in && cok) ? load2<TT>(qb + qq * A.Cp) : f32x2{0.0f, 0.0f};
+            }
+#pragma unroll
+            for (int k = 0; k < kBatch; ++k) gs[k][lane] = g[k];
+            __builtin_amdgcn_wave_barrier();
+            fma_partners<kBatch>(acc, gs, qv);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    reduce4(acc, red, w, lane);
+    if (w == 0 && cok) {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+            const int y = by * 4 + (i >> 4), x = bx * 4 + ((i >> 2) & 3), z = bz * 4 + (i & 3);
+            if (y < Hl && x < Wl && z < Dl) {
+                const long long row = (long long)b * A.row_stride + A.off[l] + ((long long)y * Wl + x) * Dpl + z;
+                *reinterpret_cast<f32x2 *>(dT + row * A.Cp + c0) = acc[i] * f32x2{A.scale, A.scale};
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// 5. dst[b][c][v] = sum_s wts[s] * src[b][offs[s] + ((y>>s) * Ws + (x>>s)) * Dps + (z>>s)][c]
+// for v = (y*W + x)*D + z (parents outside a level contribute nothing): 64 voxels x 64
+// channels per block through an LDS transpose (coalesced reads along c, writes along v).
+// ---------------------------------------------------------------------------------
+struct UnpackArgs {
+    const float *src;
+    float *dst;
+    long long src_bstride, N;
+    int C, Cp, W, D, ns;
+    int Hs[DVC_MAX_LEVELS], Ws[DVC_MAX_LEVELS], Ds[DVC_MAX_LEVELS], Dps[DVC_MAX_LEVELS];
+    long long offs[DVC_MAX_LEVELS];
+    float wts[DVC_MAX_LEVELS];
+};
+
+__global__ __launch_bounds__(256) void k_unpack_sum(UnpackArgs U) {
+    __shared__ float tile[64][65];
+    const int b = blockIdx.z, c0 = blockIdx.y * 64;
+    const long long v0 = (long long)blockIdx.x * 64;
+    const float *src = U.src + (long long)b * U.src_bstride * U.Cp;
+#pragma unroll 4
+    for (int k = 0; k < 16; ++k) {
+        const int idx = k * 256 + (int)threadIdx.x;
+        const int vl = idx >> 6, c = idx & 63;
+        const long long v = v0 + vl;
+        float s = 0.0f;
+        if (v < U.N && c0 + c < U.C) {
+            const int z = (int)(v % U.D);
+            const long long yx = v / U.D;
+            const int x = (int)(yx % U.W), y = (int)(yx / U.W);
+            for (int l = 0; l < U.ns; ++l) {
+                const int py = y >> l, px = x >> l, pz = z >> l;
+                if (py < U.Hs[l] && px < U.Ws[l] && pz < U.Ds[l])
+                    s += U.wts[l] * src[(U.offs[l] + ((long long)py * U.Ws[l] + px) * U.Dps[l] + pz) * U.Cp + c0 + c];
+            }
+        }
+        tile[vl][c] = s;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int k = 0; k < 16; ++k) {
+        const int idx = k * 256 + (int)threadIdx.x;
+        const int c = idx >> 6, vl = idx & 63;
+        const long long v = v0 + vl;
+        if (v < U.N && c0 + c < U.C) U.dst[((long long)b * U.C + c0 + c) * U.N + v] = tile[vl][c];
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------
+static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct BwdPlan {
+    size_t gwin, dq, dt, keys, starts, temp, total;
+};
+
+static long long max_cells(const dvc_layout &lay, int NW) {
+    long long m = 0;
+    for (int l = 0; l < lay.num_levels; ++l)
+        m = std::max(m, (long long)(lay.H[l] + NW - 1) * (lay.W[l] + NW - 1) * (lay.D[l] + NW - 1));
+    return m;
+}
+
+static void bwd_plan(int B, long long Nq, const dvc_layout &lay, int radius, BwdPlan &P) {
+    const int NW = 2 * radius + 2;
+    const long long NW3 = (long long)NW * NW * NW;
+    P.gwin = al256((size_t)B * lay.num_levels * Nq * NW3 * sizeof(float));
+    P.dq = al256((size_t)B * Nq * lay.c_pad * sizeof(float));
+    P.dt = al256((size_t)B * lay.row_stride * lay.c_pad * sizeof(float));
+    P.keys = al256((size_t)Nq * sizeof(unsigned long long));
+    P.starts = al256((size_t)(max_cells(lay, NW) + 1) * sizeof(int));
+    size_t tb = 0;
+    (void)rocprim::radix_sort_keys(nullptr, tb, (unsigned long long *)nullptr, (unsigned long long *)nullptr,
+                                   (size_t)Nq, 0u, 64u, (hipStream_t)0);
+    P.temp = al256(tb);
+    P.total = P.gwin + P.dq + P.dt + 2 * P.keys + P.starts + P.temp;
+}
+
+size_t backward_workspace_bytes(int B, long long Nq, const dvc_layout &lay, int radius) {
+    BwdPlan P;
+    bwd_plan(B, Nq, lay, radius, P);
+    return P.total;
+}
+
+template <typename TT, int R>
+static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &lay, const BwdPlan &P,
+                      unsigned char *ws, float *g1, float *g2, int C, hipStream_t s, char *err, size_t errlen) {
+    constexpr int NW = 2 * R + 2;
+    float *dq = (float *)(ws + P.gwin);
+    float *dt = (float *)(ws + P.gwin + P.dq);
+    unsigned long long *kin = (unsigned long long *)(ws + P.gwin + P.dq + P.dt);
+    unsigned long long *kout = (unsigned long long *)(ws + P.gwin + P.dq + P.dt + P.keys);
+    int *starts = (int *)(ws + P.gwin + P.dq + P.dt + 2 * P.keys);
+    void *temp = ws + P.gwin + P.dq + P.dt + 2 * P.keys + P.starts;
+    A.gwin = (float *)ws;
+    auto launched = [&](const char *what) {
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) {
+            snprintf(err, errlen, "corr_backward(%s): %s", what, hipGetErrorString(e));
+            return false;
+        }
+        return true;
+    };
+    const long long nqb = (A.Nq + 63) / 64;
+    k_win_grad<R><<<(unsigned)((A.B * A.L * nqb + 3) / 4), 256, 0, s>>>(A);
+    if (!launched("win_grad")) return DVC_ERR_LAUNCH;
+    const long long boxes = (long long)A.B * ((A.Hq + 3) / 4) * ((A.Wq + 3) / 4) * ((A.Dq + 3) / 4);
+    k_grad_q<TT, R><<<(unsigned)boxes, 256, 0, s>>>(Tt, dq, A);
+    if (!launched("grad_q")) return DVC_ERR_LAUNCH;
+    for (int b = 0; b < A.B; ++b)
+        for (int l = 0; l < A.L; ++l) {
+            if (A.zero[l]) continue;
+            const long long ncell = (long long)(A.H[l] + NW - 1) * (A.W[l] + NW - 1) * (A.D[l] + NW - 1);
+            unsigned bits = 1;
+            while ((1LL << bits) <= ncell) ++bits;
+            k_bw_keys<R><<<(unsigned)((A.Nq + 255) / 256), 256, 0, s>>>(A, b, l, kin);
+            if (!launched("keys")) return DVC_ERR_LAUNCH;
+            size_t tb = P.temp;
+            if (rocprim::radix_sort_keys(temp, tb, kin, kout, (size_t)A.Nq, 0u, 32u + bits, s) != hipSuccess) {
+                snprintf(err, errlen, "corr_backward: radix sort failed");
+                return DVC_ERR_RUNTIME;
+            }
+            k_cell_starts<<<(unsigned)((A.Nq + 1 + 255) / 256), 256, 0, s>>>(kout, A.Nq, ncell, starts);
+            if (!launched("cell_starts")) return DVC_ERR_LAUNCH;
+            const long long bricks = (long long)((A.H[l] + 3) / 4) * ((A.W[l] + 3) / 4) * ((A.D[l] + 3) / 4);
+            k_grad_t<TT, R><<<(unsigned)bricks, 256, 0, s>>>(Q, kout, starts, dt, A, b, l);
+            if (!launched("grad_t")) return DVC_ERR_LAUNCH;
+        }
+    // dfmap1 (B, C, Nq) <- dQ
+    UnpackArgs U{};
+    U.src = dq; U.dst = g1; U.src_bstride = A.Nq; U.N = A.Nq; U.C = C; U.Cp = A.Cp; U.W = A.Wq; U.D = A.Dq;
+    U.ns = 1; U.Hs[0] = A.Hq; U.Ws[0] = A.Wq; U.Ds[0] = A.Dq; U.Dps[0] = A.Dq; U.offs[0] = 0; U.wts[0] = 1.0f;
+    dim3 g1grid((unsigned)((A.Nq + 63) / 64), (unsigned)((C + 63) / 64), (unsigned)A.B);
+    k_unpack_sum<<<g1grid, 256, 0, s>>>(U);
+    if (!launched("unpack_q")) return DVC_ERR_LAUNCH;
+    // dfmap2 (B, C, H, W, D) <- sum_l 8^-l dT_l (floor-mode avg_pool3d adjoint)
+    UnpackArgs V{};
+    V.src = dt; V.dst = g2; V.src_bstride = lay.row_stride; V.C = C; V.Cp = A.Cp; V.W = lay.W[0]; V.D = lay.D[0];
+    V.N = (long long)lay.H[0] * lay.W[0] * lay.D[0];
+    // slot l = level l (the unpack shifts coordinates by the slot index); a zero level's
+    // dT rows are never written, so its slot gets an empty extent
+    V.ns = lay.num_levels;
+    float wl = 1.0f;
+    for (int l = 0; l < lay.num_levels; ++l, wl *= 0.125f) {
+        V.Hs[l] = lay.zero_level[l] ? 0 : lay.H[l];
+        V.Ws[l] = lay.W[l]; V.Ds[l] = lay.D[l]; V.Dps[l] = lay.Dp[l];
+        V.offs[l] = lay.offset[l]; V.wts[l] = wl;
+    }
+    dim3 g2grid((unsigned)((V.N + 63) / 64), (unsigned)((C + 63) / 64), (unsigned)A.B);
+    k_unpack_sum<<<g2grid, 256, 0, s>>>(V);
+    if (!launched("unpack_t")) return DVC_ERR_LAUNCH;
+    return DVC_OK;
+}
+
+int corr_backward(const void *packed_q, const void *packed_t, const float *coords, const float *grad_out,
+                  float *grad_fmap1, float *grad_fmap2, void *workspace, int B, long long Nq, int C,
+                  const dvc_layout &lay, int radius, int convention, int dtype, hipStream_t s, char *err,
+                  size_t errlen) {
+    if (radius < 1 || radius > 6) {
+        snprintf(err, errlen, "corr_backward: radius %d outside [1, 6]", radius);
+        return DVC_ERR_UNSUPPORTED;
+    }
+    if (lay.c_pad > 128) {
+        snprintf(err, errlen, "corr_backward: C=%d > 128 not supported", C);
+        return DVC_ERR_UNSUPPORTED;
+    }
+    const long long plane = (long long)lay.W[0] * lay.D[0];
+    if (Nq % plane) {
+        snprintf(err, errlen, "corr_backward: Nq=%lld is not a whole number of (W, D) planes", Nq);
+        return DVC_ERR_UNSUPPORTED;
+    }
+    const bool legacy = convention == DVC_LEGACY;
+    for (int l = 0; l < lay.num_levels; ++l)
+        if (legacy && !lay.zero_level[l] && lay.W[l] != lay.D[l]) {
+            snprintf(err, errlen, "corr_backward: legacy convention with W != D at level %d is not supported", l);
+            return DVC_ERR_UNSUPPORTED;
+        }
+    const int NW = 2 * radius + 2;
+    if (max_cells(lay, NW) >= (1LL << 31) - 1 || Nq >= (1LL << 31) - 1) {
+        snprintf(err, errlen, "corr_backward: volume too large for 32-bit keys");
+        return DVC_ERR_UNSUPPORTED;
+    }
+    BwdArgs A{};
+    A.coords = coords; A.gout = grad_out; A.Nq = Nq; A.row_stride = lay.row_stride;
+    A.B = B; A.L = lay.num_levels; A.legacy = legacy; A.Wq = lay.W[0]; A.Dq = lay.D[0];
+    A.Hq = (int)(Nq / plane); A.Cp = lay.c_pad; A.scale = 1.0f / sqrtf((float)C);
+    for (int l = 0; l < DVC_MAX_LEVELS; ++l) {
+        A.H[l] = lay.H[l]; A.W[l] = lay.W[l]; A.D[l] = lay.D[l]; A.Dp[l] = lay.Dp[l];
+        A.zero[l] = lay.zero_level[l]; A.off[l] = lay.offset[l];
+    }
+    BwdPlan P;
+    bwd_plan(B, Nq, lay, radius, P);
+    unsigned char *ws = (unsigned char *)workspace;
+#define DVC_BWD_CASE(RR)                                                                                           \
+    case RR:                                                                                                       \
+        return dtype == DVC_BF16                                                                                   \
+                   ? backward_r<bf16_t, RR>((const bf16_t *)packed_q, (const bf16_t *)packed_t, A, lay, P, ws,     \
+                                            grad_fmap1, grad_fmap2, C, s, err, errlen)                             \
+                   : backward_r<float, RR>((const float *)packed_q, (const float *)packed_t, A, lay, P, ws,        \
+                                           grad_fmap1, grad_fmap2, C, s, err, errlen);
+    switch (radius) {
+        DVC_BWD_CASE(1)
+        DVC_BWD_CASE(2)
+        DVC_BWD_CASE(3)
+        DVC_BWD_CASE(4)
+        DVC_BWD_CASE(5)
+        DVC_BWD_CASE(6)
+    default: break;
+    }
+#undef DVC_BWD_CASE
+    return DVC_ERR_UNSUPPORTED;
+}
+
+}  // namespace dvc

@@ -36,6 +36,11 @@ int fused_lookup(const void *packed_q, const void *packed_t, const float *coords
                  long long Nq, int C, const dvc_layout &lay, int radius, int convention, int dtype, int variant,
                  hipStream_t s, char *err, size_t errlen);
 size_t fused_workspace_bytes(int B, long long Nq, int L, int radius);
+int corr_backward(const void *packed_q, const void *packed_t, const float *coords, const float *grad_out,
+                  float *grad_fmap1, float *grad_fmap2, void *workspace, int B, long long Nq, int C,
+                  const dvc_layout &lay, int radius, int convention, int dtype, hipStream_t s, char *err,
+                  size_t errlen);
+size_t backward_workspace_bytes(int B, long long Nq, const dvc_layout &lay, int radius);
 }  // namespace dvc
 
 using namespace dvc;
@@ -455,6 +460,29 @@ int dvc_corr_lookup_fused(const void *packed_q, const void *packed_t, const floa
     if (dtype != DVC_BF16 && dtype != DVC_F32) return fail(DVC_ERR_INVALID, "lookup_fused: bad dtype %d", dtype);
     return fused_lookup(packed_q, packed_t, coords, out, workspace, B, Nq, C, lay, radius, convention, dtype,
                         g_fused_variant, (hipStream_t)stream, g_err, sizeof(g_err));
+}
+
+size_t dvc_corr_backward_workspace_bytes(int B, int64_t Nq, int C, int H, int W, int D, int num_levels, int radius) {
+    dvc_layout lay;
+    if (dvc_layout_init(H, W, D, num_levels, C, &lay)) return 0;
+    if (B < 1 || Nq < 1 || radius < 1 || radius > 6) return 0;
+    return backward_workspace_bytes(B, Nq, lay, radius);
+}
+
+int dvc_corr_backward(const void *packed_q, const void *packed_t, const float *coords, const float *grad_out,
+                      float *grad_fmap1, float *grad_fmap2, void *workspace, int B, int64_t Nq, int C, int H, int W,
+                      int D, int num_levels, int radius, int convention, int dtype, void *stream) {
+    dvc_layout lay;
+    int rc = dvc_layout_init(H, W, D, num_levels, C, &lay);
+    if (rc) return rc;
+    if (!packed_q || !packed_t || !coords || !grad_out || !grad_fmap1 || !grad_fmap2 || !workspace)
+        return fail(DVC_ERR_INVALID, "corr_backward: null pointer");
+    if (B < 1 || Nq < 1) return fail(DVC_ERR_INVALID, "corr_backward: B=%d Nq=%lld", B, (long long)Nq);
+    if (convention != DVC_FIXED && convention != DVC_LEGACY)
+        return fail(DVC_ERR_INVALID, "corr_backward: bad convention %d", convention);
+    if (dtype != DVC_BF16 && dtype != DVC_F32) return fail(DVC_ERR_INVALID, "corr_backward: bad dtype %d", dtype);
+    return corr_backward(packed_q, packed_t, coords, grad_out, grad_fmap1, grad_fmap2, workspace, B, Nq, C, lay, radius,
+                         convention, dtype, (hipStream_t)stream, g_err, sizeof(g_err));
 }
 
 int dvc_sample3d(const float *vol, const float *pts, float *out, int B, int C, int Hv, int Wv, int Dv, int64_t Nq,

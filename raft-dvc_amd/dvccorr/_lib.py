@@ -23,6 +23,7 @@ EXPORTED = (
     "dvc_layout_init", "dvc_pack_workspace_bytes", "dvc_pack_queries", "dvc_pack_targets", "dvc_corr_build",
     "dvc_corr_pool", "dvc_corr_lookup", "dvc_lookup_fused_workspace_bytes", "dvc_corr_lookup_fused",
     "dvc_sample3d", "dvc_set_tuning", "dvc_last_error", "dvc_version", "dvc_abi_version",
+    "dvc_corr_backward_workspace_bytes", "dvc_corr_backward",
 )
 
 
@@ -74,6 +75,9 @@ def lib() -> ctypes.CDLL:
         "dvc_lookup_fused_workspace_bytes": (sz, [i32, i64, i32, i32]),
         "dvc_corr_lookup_fused": (i32, [vp, vp, vp, vp, vp, i32, i64, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
         "dvc_sample3d": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i64, i32, vp]),
+        "dvc_corr_backward_workspace_bytes": (sz, [i32, i64, i32, i32, i32, i32, i32, i32]),
+        "dvc_corr_backward": (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i64, i32, i32, i32, i32, i32, i32, i32, i32,
+                                    vp]),
         "dvc_set_tuning": (i32, [ctypes.c_char_p, i32]),
         "dvc_last_error": (ctypes.c_char_p, []),
         "dvc_version": (ctypes.c_char_p, []),

@@ -20,7 +20,13 @@ Precision: fp32 feature maps build in exact f32 MFMA and store fp32
 (tolerance 1e-5 relative to the reference); `precision="bf16"` builds on
 bf16 MFMA and stores bf16 (tolerance 1e-2), halving the HBM traffic; the
 default follows the input dtype (fp16/bf16 inputs -> bf16), overridable with
-the DVCCORR_PRECISION environment variable.  Backward is not implemented yet.
+the DVCCORR_PRECISION environment variable.
+
+Backward: when a feature map requires grad, every call is an autograd node whose
+backward runs dvc_corr_backward (sparse per-query window gradients, no dense
+d(corr), no atomics) and returns d fmap1 / d fmap2; coordinates get no gradient,
+as RAFTDVC.forward detaches them (raft_dvc.py:441).  Twelve calls on one block
+accumulate in autograd like the reference's twelve grid_sample calls.
 """
 from __future__ import annotations
 
@@ -45,10 +51,48 @@ def resolve_precision(fmap: torch.Tensor, precision: Optional[str]) -> str:
     return "bf16" if precision in ("bf16", "bfloat16") else "fp32"
 
 
-def _no_grad_guard(*ts: torch.Tensor) -> None:
-    if torch.is_grad_enabled() and any(t.requires_grad for t in ts):
-        raise NotImplementedError("dvccorr: backward through the correlation block is not implemented yet; "
-                                  "run under torch.no_grad() or detach the feature maps")
+def _wants_grad(*ts: torch.Tensor) -> bool:
+    return torch.is_grad_enabled() and any(t.requires_grad for t in ts)
+
+
+class _LookupFn(torch.autograd.Function):
+    """One lookup call as an autograd node (reference: autograd through corr.py:141-208).
+
+    forward: the block's lookup kernels; backward: dvc_corr_backward -> (d fmap1, d fmap2).
+    Coordinates get no gradient (RAFTDVC.forward detaches them, raft_dvc.py:441)."""
+
+    @staticmethod
+    def forward(ctx, coords, fmap1, fmap2, blk):
+        ctx.blk = blk
+        ctx.legacy = blk.legacy_wd_swap
+        ctx.dtypes = (fmap1.dtype, fmap2.dtype)
+        ctx.save_for_backward(coords)
+        return blk._lookup(coords)
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        (coords,) = ctx.saved_tensors
+        blk = ctx.blk
+        B, C, H, W, D = blk.shape
+        N = H * W * D
+        d1, d2 = ops.corr_backward(blk._q, blk._t, coords.reshape(B, 3, N), grad_out.reshape(B, -1, N), C, H, W, D,
+                                   blk.num_levels, blk.radius, ctx.legacy, blk._dt)
+        return None, d1.view(B, C, H, W, D).to(ctx.dtypes[0]), d2.to(ctx.dtypes[1]), None
+
+
+class _Block:
+    """Shared __call__: coords check, then the kernels (wrapped in _LookupFn when grad is needed)."""
+
+    def _check_coords(self, coords: torch.Tensor) -> None:
+        B, _, H, W, D = self.shape
+        if coords.ndim != 5 or tuple(coords.shape) != (B, 3, H, W, D):
+            raise ValueError(f"coords must be (B, 3, H, W, D) = {(B, 3, H, W, D)}; got {tuple(coords.shape)}")
+
+    def __call__(self, coords: torch.Tensor) -> torch.Tensor:
+        self._check_coords(coords)
+        if self._grad_fmaps is not None and torch.is_grad_enabled():
+            return _LookupFn.apply(coords, *self._grad_fmaps, self)
+        return self._lookup(coords)
 
 
 def _check_fmaps(fmap1: torch.Tensor, fmap2: torch.Tensor) -> None:
@@ -59,13 +103,12 @@ def _check_fmaps(fmap1: torch.Tensor, fmap2: torch.Tensor) -> None:
                          f"{tuple(fmap2.shape)}")
 
 
-class CorrBlock:
+class CorrBlock(_Block):
     """All-pairs 3-D correlation pyramid + radius-r trilinear lookup (materialised)."""
 
     def __init__(self, fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int = 4, radius: int = 4,
                  legacy_wd_swap: bool = False, *, precision: Optional[str] = None, build: str = "gemm"):
         _check_fmaps(fmap1, fmap2)
-        _no_grad_guard(fmap1, fmap2)
         self.num_levels = num_levels
         self.radius = radius
         self.legacy_wd_swap = legacy_wd_swap
@@ -74,8 +117,11 @@ class CorrBlock:
         self._lay = layout(H, W, D, num_levels, C)      # RuntimeError where avg_pool3d would raise
         self.precision = resolve_precision(fmap1, precision)
         self._dt = ops.dtype_code(self.precision)
-        q = ops.pack_queries(fmap1.reshape(B, C, H * W * D), self._dt)
-        t = ops.pack_targets(fmap2, num_levels, self._dt)
+        self._grad_fmaps = (fmap1, fmap2) if _wants_grad(fmap1, fmap2) else None
+        q = ops.pack_queries(fmap1.detach().reshape(B, C, H * W * D), self._dt)
+        t = ops.pack_targets(fmap2.detach(), num_levels, self._dt)
+        # the backward needs the packed operands (O(C * voxels)): keep them only then
+        self._q, self._t = (q, t) if self._grad_fmaps is not None else (None, None)
         if build == "gemm":       # every level from the pooled targets, one launch
             self._corr = ops.build(q, t, C, H, W, D, num_levels, self._dt, self._dt)
         elif build == "pool":     # the reference's op order: level 0 GEMM, then avg-pool the volume
@@ -100,16 +146,14 @@ class CorrBlock:
             views.append(v)
         return views
 
-    def __call__(self, coords: torch.Tensor) -> torch.Tensor:
+    def _lookup(self, coords: torch.Tensor) -> torch.Tensor:
         B, _, H, W, D = self.shape
-        if coords.ndim != 5 or tuple(coords.shape) != (B, 3, H, W, D):
-            raise ValueError(f"coords must be (B, 3, H, W, D) = {(B, 3, H, W, D)}; got {tuple(coords.shape)}")
         out = ops.lookup(self._corr, coords.reshape(B, 3, H * W * D), H, W, D, self.num_levels, self.radius,
                          self.legacy_wd_swap, self._dt)
         return out.view(B, -1, H, W, D)
 
 
-class CorrBlockFused:
+class CorrBlockFused(_Block):
     """On-the-fly lookup (no correlation volume), any sampler convention.
 
     Keeps the packed fmap1 rows and the packed fmap2 pyramid (O(C * voxels));
@@ -119,7 +163,6 @@ class CorrBlockFused:
     def __init__(self, fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int = 4, radius: int = 4,
                  legacy_wd_swap: bool = False, *, precision: Optional[str] = None):
         _check_fmaps(fmap1, fmap2)
-        _no_grad_guard(fmap1, fmap2)
         self.num_levels = num_levels
         self.radius = radius
         self.legacy_wd_swap = legacy_wd_swap
@@ -128,14 +171,13 @@ class CorrBlockFused:
         self._lay = layout(H, W, D, num_levels, C)
         self.precision = resolve_precision(fmap1, precision)
         self._dt = ops.dtype_code(self.precision)
-        self._q = ops.pack_queries(fmap1.reshape(B, C, H * W * D), self._dt)
-        self._t = ops.pack_targets(fmap2, num_levels, self._dt)
+        self._grad_fmaps = (fmap1, fmap2) if _wants_grad(fmap1, fmap2) else None
+        self._q = ops.pack_queries(fmap1.detach().reshape(B, C, H * W * D), self._dt)
+        self._t = ops.pack_targets(fmap2.detach(), num_levels, self._dt)
         self._ws = ops.fused_workspace(B, H * W * D, num_levels, radius, fmap1.device)
 
-    def __call__(self, coords: torch.Tensor) -> torch.Tensor:
+    def _lookup(self, coords: torch.Tensor) -> torch.Tensor:
         B, C, H, W, D = self.shape
-        if coords.ndim != 5 or tuple(coords.shape) != (B, 3, H, W, D):
-            raise ValueError(f"coords must be (B, 3, H, W, D) = {(B, 3, H, W, D)}; got {tuple(coords.shape)}")
         out = ops.lookup_fused(self._q, self._t, coords.reshape(B, 3, H * W * D), C, H, W, D, self.num_levels,
                                self.radius, self.legacy_wd_swap, self._dt, workspace=self._ws)
         return out.view(B, -1, H, W, D)

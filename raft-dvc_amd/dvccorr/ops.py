@@ -143,6 +143,25 @@ def fused_workspace(B: int, Nq: int, num_levels: int, radius: int, device) -> to
     return torch.empty((max(nws, 4) // 4,), dtype=torch.float32, device=device)
 
 
+def corr_backward(packed_q: torch.Tensor, packed_t: torch.Tensor, coords: torch.Tensor, grad_out: torch.Tensor,
+                  C: int, H: int, W: int, D: int, num_levels: int, radius: int, legacy: bool, dtype: int):
+    """d loss / d fmap1 (B, C, Nq) and d loss / d fmap2 (B, C, H, W, D), both float32, from the gradient of
+    a lookup output (B, L*(2r+1)^3, Nq) (dvc_corr_backward)."""
+    _need_cuda(packed_q, packed_t, coords, grad_out)
+    B, Nq, _ = packed_q.shape
+    c = _f32c(coords)
+    g = _f32c(grad_out)
+    dev = packed_q.device
+    d1 = torch.empty((B, C, Nq), dtype=torch.float32, device=dev)
+    d2 = torch.empty((B, C, H, W, D), dtype=torch.float32, device=dev)
+    nws = lib().dvc_corr_backward_workspace_bytes(B, Nq, C, H, W, D, num_levels, radius)
+    ws = torch.empty((max(nws, 256),), dtype=torch.uint8, device=dev)
+    check(lib().dvc_corr_backward(_ptr(packed_q), _ptr(packed_t), _ptr(c), _ptr(g), _ptr(d1), _ptr(d2), _ptr(ws), B,
+                                  Nq, C, H, W, D, num_levels, radius, DVC_LEGACY if legacy else DVC_FIXED, dtype,
+                                  _stream(packed_q)), "corr_backward")
+    return d1, d2
+
+
 def sample3d(vol: torch.Tensor, pts: torch.Tensor, legacy: bool) -> torch.Tensor:
     _need_cuda(vol, pts)
     v = _f32c(vol)
@@ -155,5 +174,5 @@ def sample3d(vol: torch.Tensor, pts: torch.Tensor, legacy: bool) -> torch.Tensor
     return out
 
 
-__all__ = ["pack_queries", "pack_targets", "build", "pool", "lookup", "lookup_fused", "sample3d", "fused_workspace",
-           "dtype_code", "layout", "_lib"]
+__all__ = ["pack_queries", "pack_targets", "build", "pool", "lookup", "lookup_fused", "corr_backward", "sample3d",
+           "fused_workspace", "dtype_code", "layout", "_lib"]

@@ -46,3 +46,29 @@ def corr_inputs(g):
     f2 = prng.normal(s[1], (B, C, H, W, D))
     coords = prng.flow_coords(s[2], B, H, W, D, float(g["max_flow"][0]))
     return f1, f2, coords, L, r
+
+
+def grad_inputs(g):
+    """Regenerate a grad_* fixture's inputs (tests/golden/gen_grad_golden.py): fmaps, coords, the output
+    gradient G (all ones or N(0,1)), L, r, legacy."""
+    import prng
+    B, C, H, W, D, L, r = (int(v) for v in g["shape"])
+    s = [int(v) for v in g["seeds"]]
+    f1 = prng.normal(s[0], (B, C, H, W, D))
+    f2 = prng.normal(s[1], (B, C, H, W, D))
+    coords = prng.flow_coords(s[2], B, H, W, D, float(g["max_flow"][0]))
+    gshape = (B, L * (2 * r + 1) ** 3, H, W, D)
+    G = np.ones(gshape, np.float32) if int(g["gkind"][0]) == 0 else prng.normal(s[3], gshape)
+    return f1, f2, coords, G, L, r, bool(int(g["legacy"][0]))
+
+
+def oracle_grads(f1, f2, coords, G, L, r, legacy):
+    """The backward oracle: autograd through oracle/torch_cpu.py (bit-identical to the reference's autograd on
+    every grad_* fixture, tests/golden/grad_meta.json)."""
+    import torch
+    from oracle import torch_cpu
+    t1 = torch.from_numpy(np.ascontiguousarray(f1)).requires_grad_(True)
+    t2 = torch.from_numpy(np.ascontiguousarray(f2)).requires_grad_(True)
+    out = torch_cpu.corr_lookup(t1, t2, torch.from_numpy(np.ascontiguousarray(coords)), L, r, legacy)
+    (out * torch.from_numpy(np.ascontiguousarray(G))).sum().backward()
+    return t1.grad.numpy(), t2.grad.numpy()

@@ -113,8 +113,26 @@ def test_reference_style_argument_errors():
         dvccorr.CorrBlockOnTheFly(f, f, chunk_size=0)
     with pytest.raises(ValueError):
         dvccorr.make_corr_block("mi355x", f, f, sampler_version=3)
-    with pytest.raises(NotImplementedError):
-        dvccorr.CorrBlock(f.requires_grad_(True), f)
+    with pytest.raises(RuntimeError, match="MI355X"):   # grad-tracking maps: same refusal of CPU tensors
+        dvccorr.CorrBlock(f.clone().requires_grad_(True), f)
+
+
+def test_backward_validation_without_gpu():
+    """dvc_corr_backward's host checks: null pointers -> ValueError; unsupported radius -> NotImplementedError."""
+    from dvccorr import _lib
+    L = _lib.lib()
+    p = ctypes.c_void_p(16)
+    rc = L.dvc_corr_backward(None, p, p, p, p, p, p, 1, 512, 16, 8, 8, 8, 2, 4, 0, 0, None)
+    assert rc == _lib.DVC_ERR_INVALID
+    rc = L.dvc_corr_backward(p, p, p, p, p, p, p, 1, 512, 16, 8, 8, 8, 2, 9, 0, 0, None)
+    assert rc == _lib.DVC_ERR_UNSUPPORTED
+    with pytest.raises(NotImplementedError, match="radius"):
+        _lib.check(rc)
+    rc = L.dvc_corr_backward(p, p, p, p, p, p, p, 1, 512, 16, 8, 8, 4, 2, 4, 1, 0, None)
+    assert rc == _lib.DVC_ERR_UNSUPPORTED     # legacy convention with W != D
+    # workspace: window gradients (B*L*Nq*(2r+2)^3 f32) + dQ + dT + keys + cell starts + sort scratch
+    nws = L.dvc_corr_backward_workspace_bytes(1, 32768, 128, 32, 32, 32, 4, 4)
+    assert nws >= 4 * 32768 * 1000 * 4 and nws < 4 * 32768 * 1000 * 4 + 64 * 2 ** 20
 
 
 def test_coords_grid_matches_reference_fixture():

@@ -99,6 +99,28 @@ def test_torch_cpu_restatement_matches_golden():
         np.testing.assert_array_equal(got, g[f"out_rows_{tag}"])
 
 
+GRAD_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "grad_*.npz")))
+
+
+@pytest.mark.parametrize("case", GRAD_CASES)
+def test_backward_oracle_matches_reference_gradients(case):
+    """The backward oracle (autograd through oracle/torch_cpu.py) reproduces the gradients the reference's own
+    autograd produced (tests/golden/gen_grad_golden.py; bitwise there, 1e-6 here to allow another BLAS)."""
+    from conftest import grad_inputs, oracle_grads
+    g = load_golden(case + ".npz")
+    f1, f2, coords, G, L, r, legacy = grad_inputs(g)
+    d1, d2 = oracle_grads(f1, f2, coords, G, L, r, legacy)
+    if "grad_f1" in g:
+        assert orc.rel_err(d1, g["grad_f1"]) < 1e-6 and orc.rel_err(d2, g["grad_f2"]) < 1e-6
+    else:
+        idx = g["idx"]
+        assert orc.rel_err(d1.reshape(-1)[idx], g["grad_f1_s"]) < 1e-6
+        assert orc.rel_err(d2.reshape(-1)[idx], g["grad_f2_s"]) < 1e-6
+    for d, cs in ((d1, g["checksum_f1"]), (d2, g["checksum_f2"])):
+        dd = d.astype(np.float64)
+        assert abs((dd * dd).sum() - cs[2]) / cs[2] < 1e-6
+
+
 def test_size1_level_raises_where_reference_raises():
     with pytest.raises(RuntimeError):
         orc.level_dims(8, 8, 2, 3)
