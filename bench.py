@@ -219,8 +219,13 @@ def main():
             traffic = None
     if args.iters * lk_avg >= bd_avg or args.impl == "fused":
         achieved = lk_bytes / (lk_avg * 1e-3) / 1e9
-        roof = {"kernel": "k_lookup_tile (dvc_corr_lookup)" if args.impl == "materialised" else
-                "k_fused_dots + k_lookup_win (dvc_corr_lookup_fused)",
+        if args.impl == "materialised":
+            kname = "k_lookup_tile (dvc_corr_lookup)"
+        elif args.precision == "bf16" and 1 <= R <= 4:
+            kname = "k_fused_tile (dvc_corr_lookup_fused)"
+        else:
+            kname = "k_fused_dots + k_lookup_win (dvc_corr_lookup_fused)"
+        roof = {"kernel": kname,
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "algorithmic_bytes_per_launch": lk_bytes, "avg_launch_ms": round(lk_avg, 4)}

@@ -319,7 +319,9 @@ int dvc_corr_build(const void *packed_q, const void *packed_t, void *corr, int B
         return fail(DVC_ERR_INVALID, "build: bad column range [%lld, %lld) for row_stride %lld", (long long)col_begin,
                     (long long)col_end, lay.row_stride);
     const int Cp = lay.c_pad;
-    if (Cp > 256) return fail(DVC_ERR_UNSUPPORTED, "build: C=%d > 256 not supported", C);
+    // C_pad 256 faulted once on the GPU (bf16 build or fused tile, tests/test_gpu_parity.py, round 1): refused
+    // until it is isolated; every configuration of the reference uses C = 128
+    if (Cp > 128) return fail(DVC_ERR_UNSUPPORTED, "build: C=%d > 128 not supported", C);
     const float scale = 1.0f / sqrtf((float)C);   // corr / sqrt(C) (corr.py:165)
     hipStream_t s = (hipStream_t)stream;
     const long long ncol_tiles = ceil_div(col_end - col_begin, 128);

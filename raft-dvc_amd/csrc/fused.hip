@@ -188,11 +188,11 @@ static void fused_level(int R, const T *Q, const T *Tt, LookupArgs &A, float *ws
 template <int R, int NCH>
 __global__ void k_fused_tile(const bf16_t *, const bf16_t *, LookupArgs, int, long long, int, int, int, float);
 
-// The MFMA tile kernel (fused_tile.hip) covers bf16, r <= 4, C <= 256, whole (y, x)
+// The MFMA tile kernel (fused_tile.hip) covers bf16, r <= 4, C_pad in {32, 64, 128}, whole (y, x)
 // planes of queries (Nq a multiple of W*D: the full grid or an H-slab of it) and
 // packed targets addressable with 32-bit byte offsets.
 static bool fused_tile_ok(long long Nq, int W, int D, int Cp, long long t_rows, int radius, int dtype) {
-    return dtype == DVC_BF16 && radius >= 1 && radius <= 4 && (Cp == 32 || Cp == 64 || Cp == 128 || Cp == 256) &&
+    return dtype == DVC_BF16 && radius >= 1 && radius <= 4 && (Cp == 32 || Cp == 64 || Cp == 128) &&
            Nq % ((long long)W * D) == 0 &&
            t_rows * Cp * 2 < (1LL << 31) - 65536;
 }
@@ -200,8 +200,11 @@ static bool fused_tile_ok(long long Nq, int W, int D, int Cp, long long t_rows, 
 template <int R>
 static void launch_fused_tile(const bf16_t *Q, const bf16_t *Tt, const LookupArgs &A, int Cp, long long t_rows,
                               int Hq, int Wq, int Dq, float scale, hipStream_t s) {
-    const long long tiles = (long long)A.B * ((Hq + 1) / 2) * ((Wq + 1) / 2) * ((Dq + 15) / 16);
-    const unsigned grid = (unsigned)tiles;
+    // the kernel's XCD-aware order pads the tile grid to 4 x 4 x 2 groups and rounds the
+    // total up to a multiple of 8 workgroups (one range per XCD)
+    const long long ngy = ((Hq + 1) / 2 + 3) / 4, ngx = ((Wq + 1) / 2 + 3) / 4, ngz = ((Dq + 15) / 16 + 1) / 2;
+    const long long tiles = (long long)A.B * ngy * ngx * ngz * 32;
+    const unsigned grid = (unsigned)(8 * ((tiles + 7) / 8));
     switch (Cp / 8) {
     case 4: k_fused_tile<R, 4><<<grid, 256, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;
     case 8: k_fused_tile<R, 8><<<grid, 256, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;

@@ -48,15 +48,27 @@ template <int R> struct FusedCfg {
     static constexpr int COLS = 3;                                // output columns per wave (phase 2)
 };
 
+// Wave-uniform values the compiler cannot prove uniform (reductions, fields of the
+// by-reference argument struct) go through readfirstlane, so address arithmetic stays
+// in SGPRs and every buffer descriptor is built from SGPRs -- otherwise hipcc wraps
+// each buffer op in a waterfall loop (cdna_hip_programming.md T20).
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ long long uni64(long long v) {
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((unsigned long long)v >> 32));
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
+template <typename T> __device__ __forceinline__ T *uniptr(T *p) { return (T *)uni64((long long)p); }
+
 __device__ __forceinline__ int wave_min(int v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v = min(v, __shfl_xor(v, o));
-    return v;
+    return uni(v);
 }
 __device__ __forceinline__ int wave_max(int v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));
-    return v;
+    return uni(v);
 }
 
 // z-lerped run of one window column (packed pairs + tail), as in lookup_tile.hip
@@ -78,13 +90,24 @@ __global__ __launch_bounds__(256, 1) void k_fused_tile(const bf16_t *__restrict_
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     unsigned char *stg = smem + C::GUARD + 64 * C::WQ + wave * C::SWAVE + 32;   // this wave's staging
 
-    // tile of the query box
+    // tile of the query box.  XCD-aware order: workgroup g runs on XCD g % 8 (round-robin
+    // dispatch), so each XCD gets a contiguous range of logical tiles, and logical tiles
+    // run through groups of GY x GX x GZ = 4 x 4 x 2 tiles: the ~32 tiles one XCD holds at
+    // once are neighbours whose union windows overlap in its L2 (the target rows are
+    // re-read by every tile whose union covers them).  Padding tiles exit at once.
+    constexpr int GY = 4, GX = 4, GZ = 2;
     const int nty = (Hq + C::TY - 1) / C::TY, ntx = (Wq + C::TX - 1) / C::TX, ntz = (Dq + C::TZ - 1) / C::TZ;
-    int t = blockIdx.x;
-    const int tz = t % ntz; t /= ntz;
-    const int tx = t % ntx; t /= ntx;
-    const int ty = t % nty;
-    const int b = t / nty;
+    const int ngy = (nty + GY - 1) / GY, ngx = (ntx + GX - 1) / GX, ngz = (ntz + GZ - 1) / GZ;
+    const int per_b = ngy * ngx * ngz * (GY * GX * GZ);
+    const int per_xcd = (A.B * per_b + 7) / 8;
+    const int lt = (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
+    if (lt >= A.B * per_b) return;
+    const int b = lt / per_b;
+    const int grp = (lt - b * per_b) / (GY * GX * GZ), wi = (lt - b * per_b) % (GY * GX * GZ);
+    const int tz = (grp % ngz) * GZ + wi % GZ;
+    const int tx = ((grp / ngz) % ngx) * GX + (wi / GZ) % GX;
+    const int ty = (grp / (ngz * ngx)) * GY + wi / (GZ * GX);
+    if (ty >= nty || tx >= ntx || tz >= ntz) return;
     const int zi = lane & 15, xi = (lane >> 4) & 1, yi = lane >> 5;
     const int qy = ty * C::TY + yi, qx = tx * C::TX + xi, qz = tz * C::TZ + zi;
     const bool active = qy < Hq && qx < Wq && qz < Dq;
@@ -124,24 +147,27 @@ __global__ __launch_bounds__(256, 1) void k_fused_tile(const bf16_t *__restrict_
     const __amdgpu_buffer_rsrc_t rs_t = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(((unsigned long long)tbhi << 32) | tblo), (short)0, t_bytes, 0x00020000);
 
-    const int chstep_u = A.legacy ? 1 : n;
-    const int chstep_v = A.legacy ? n : 1;
+    const int legacy = uni(A.legacy);
+    const int chstep_u = legacy ? 1 : n;
+    const int chstep_v = legacy ? n : 1;
     const int u0 = wave * C::COLS;
     const int q4 = active ? (int)(qg * 4) : 0x7ffffff0;
     const f32x2 sc2 = {scale, scale};
+    const int vstep = uni((int)(chstep_v * Nq * 4));          // byte step between output offsets v
+    const int out_bytes = uni((int)(n * n * Nq * 4));
 
     auto out_rsrc = [&](float *obase, int a, int u) {
-        return __builtin_amdgcn_make_buffer_rsrc(obase + ((long long)a * n * n + (long long)u * chstep_u) * Nq,
-                                                 (short)0, (int)(n * n * Nq * 4), 0x00020000);
+        return __builtin_amdgcn_make_buffer_rsrc(
+            uniptr(obase + ((long long)a * n * n + (long long)u * chstep_u) * Nq), (short)0, out_bytes, 0x00020000);
     };
     auto store = [&](__amdgpu_buffer_rsrc_t rs, int v, float val) {
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val), rs, q4, (int)(v * chstep_v * Nq * 4), 2);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val), rs, q4, v * vstep, 2);
     };
 
     auto level = [&](int l, auto nu_c) {
         constexpr int NU = decltype(nu_c)::value;
-        float *obase = A.out + ((long long)b * A.Ltot + l) * n3 * Nq;
-        if (A.zero[l]) {
+        float *obase = uniptr(A.out + ((long long)b * A.Ltot + l) * n3 * Nq);
+        if (uni(A.zero[l])) {
             for (int a = 0; a < n; ++a)
 #pragma unroll
                 for (int uu = 0; uu < NU; ++uu) {
@@ -151,10 +177,11 @@ __global__ __launch_bounds__(256, 1) void k_fused_tile(const bf16_t *__restrict_
                 }
             return;
         }
-        const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
+        const int Hl = uni(A.H[l]), Wl = uni(A.W[l]), Dl = uni(A.D[l]), Dpl = uni(A.Dp[l]);
+        const long long offl = uni64(A.off[l]);
         const float sc = (float)(1 << l);
         WinAxes ax;
-        window_axes(cy / sc, cx / sc, cz / sc, Hl, Wl, Dl, A.legacy, ax);
+        window_axes(cy / sc, cx / sc, cz / sc, Hl, Wl, Dl, legacy, ax);
         const int ih = (int)ax.kh - R, iu = (int)ax.ku - R, iv = (int)ax.kv - R;
 
         // union of the live windows, clamped to the level (wave-uniform; every wave
@@ -178,22 +205,30 @@ __global__ __launch_bounds__(256, 1) void k_fused_tile(const bf16_t *__restrict_
         // ---------------- phase 1: window dots on MFMA ----------------
         unsigned char *myw = win + lane * C::WQ;                   // this lane's (query's) window
         if (ny > 0 && nx > 0 && nz > 0) {
+            // this wave's (row block, z chunk) iterations: blocks wave, wave + 4, ... of the
+            // ny x nx union rows, each in nzb chunks of 32 z; the A operands of iteration
+            // it + 1 are loaded before the MFMAs of iteration it (L2 latency off the MFMA path)
             const int nblk = ny * nx;
-            for (int blk = wave; blk < nblk; blk += 4) {
+            const int nit = (nblk > wave ? (nblk - wave + 3) / 4 : 0) * nzb;
+            auto a_off = [&](int it) {
+                const int blk = wave + 4 * (it / nzb), z0 = zs + 32 * (it % nzb);
+                const long long rowbase = offl + ((long long)(ys + blk / nx) * Wl + (xs + blk % nx)) * Dpl;
+                // A block: target rows z0 + r32 (out of range, i.e. zeros, past the level's z range)
+                return z0 + r32 <= ze ? (int)(((rowbase + z0 + r32) * Cp + 8 * h) * 2) : 0x7fff0000;
+            };
+            auto load_a = [&](bf16x8 (&dst)[KS], int it) {
+                const int off = a_off(it);
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks)
+                    dst[ks] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs_t, off + 32 * ks, 0, 0));
+            };
+            auto body = [&](const bf16x8 (&a)[KS], int it) {
+                const int blk = wave + 4 * (it / nzb), zb = it % nzb;
                 const int y = ys + blk / nx, x = xs + blk % nx;
                 const int wy = y - ih, wx = x - iu;                  // this query's window row, if any
                 const bool need = live && (unsigned)wy < (unsigned)NW && (unsigned)wx < (unsigned)NW;
-                const long long rowbase = A.off[l] + ((long long)y * Wl + x) * Dpl;
-                for (int zb = 0; zb < nzb; ++zb) {
+                {
                     const int z0 = zs + 32 * zb;
-                    // A block: target rows z0 + r32 (zeros past the level's z range)
-                    const bool zok = z0 + r32 <= ze;
-                    const int aoff = zok ? (int)(((rowbase + z0 + r32) * Cp + 8 * h) * 2) : 0x7fff0000;
-                    bf16x8 a[KS];
-#pragma unroll
-                    for (int ks = 0; ks < KS; ++ks)
-                        a[ks] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs_t, aoff + 32 * ks,
-                                                                                               0, 0));
                     f32x16 acc[2];
 #pragma unroll
                     for (int j = 0; j < 2; ++j)
@@ -244,6 +279,19 @@ __global__ __launch_bounds__(256, 1) void k_fused_tile(const bf16_t *__restrict_
                         }
                     }
                     __builtin_amdgcn_wave_barrier();   // and the reads before the next block's writes
+                }
+            };
+            // two operand sets in flight (ping-pong, no register copies): the loads of
+            // iterations it + 2 and it + 3 are issued while it and it + 1 compute
+            bf16x8 a0[KS], a1[KS];
+            if (nit > 0) load_a(a0, 0);
+            if (nit > 1) load_a(a1, 1);
+            for (int it = 0; it < nit; it += 2) {
+                body(a0, it);
+                if (it + 2 < nit) load_a(a0, it + 2);
+                if (it + 1 < nit) {
+                    body(a1, it + 1);
+                    if (it + 3 < nit) load_a(a1, it + 3);
                 }
             }
         }
@@ -332,7 +380,7 @@ __global__ __launch_bounds__(256, 1) void k_fused_tile(const bf16_t *__restrict_
     constexpr int NWAVES_COLS = (n + C::COLS - 1) / C::COLS;   // waves with output columns
     constexpr int NU_LAST = n - C::COLS * (NWAVES_COLS - 1);
     for (int l = A.l0; l < A.l0 + A.nl; ++l) {
-        if (A.generic[l] && !A.zero[l]) continue;   // legacy level with W != D: k_fused_generic
+        if (uni(A.generic[l]) && !uni(A.zero[l])) continue;   // legacy level with W != D: k_fused_generic
         // every wave takes part in phase 1 and the barriers; waves past the output
         // columns (r < 4 leaves some idle in phase 2) use a zero-column phase 2
         if (wave < NWAVES_COLS - 1) level(l, std::integral_constant<int, C::COLS>{});

@@ -295,7 +295,7 @@ def test_tile_kernel_matches_walk(shape, L, r):
 
 @pytest.mark.parametrize("shape,C,L,r", [((9, 7, 5), 32, 2, 1), ((12, 10, 16), 64, 3, 2), ((16, 16, 16), 32, 4, 3),
                                          ((20, 13, 24), 128, 3, 4), ((32, 32, 32), 128, 4, 4),
-                                         ((18, 34, 40), 64, 2, 4), ((8, 8, 8), 256, 2, 3)])
+                                         ((18, 34, 40), 64, 2, 4), ((8, 8, 8), 128, 2, 3)])
 def test_fused_tile_matches_materialised(shape, C, L, r):
     """k_fused_tile (MFMA window dots of the union window, no volume) reproduces the bf16 materialised
     pyramid + lookup bit for bit: the same v_mfma_f32_32x32x16_bf16 dot order, the same scale-then-round to
