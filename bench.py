@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--size", type=int, default=32, help="feature-map edge (32 = 128^3 input, 1/4 encoder)")
+    ap.add_argument("--encoder", type=int, default=4, help="encoder downsampling (input edge = size x encoder)")
     ap.add_argument("--channels", type=int, default=128)
     ap.add_argument("--levels", type=int, default=4)
     ap.add_argument("--radius", type=int, default=4)
@@ -207,8 +208,12 @@ def main():
                    for c in coords_slab) / len(coords_slab)
     unpadded = sum(h * w * d for (h, w, d) in dims)
     n_targets = S * S * S
-    bd_bytes = nq_local * unpadded * store_bytes + 2 * C * 4 * n_targets
-    bd_flops = 2.0 * nq_local * n_targets * C
+    if args.impl == "materialised":
+        bd_bytes = nq_local * unpadded * store_bytes + 2 * C * 4 * n_targets
+        bd_flops = 2.0 * nq_local * n_targets * C
+    else:   # fused: the "build" only packs fmap1 rows and the pooled fmap2 pyramid (read f32, write bf16/f32)
+        bd_bytes = (nq_local + n_targets) * C * 4 + (nq_local + unpadded) * C * store_bytes
+        bd_flops = 0.0
     traffic = None
     if os.path.exists(args.traffic_file):
         try:
@@ -229,13 +234,19 @@ def main():
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "algorithmic_bytes_per_launch": lk_bytes, "avg_launch_ms": round(lk_avg, 4)}
+        if args.impl == "fused":
+            # the reference OTF dot count 2 C (2r+1)^3 L per voxel-query, against the dtype's MFMA peak
+            fl = 2.0 * C * (2 * R + 1) ** 3 * L * nq_local
+            peak = BF16_PEAK_TFS if args.precision == "bf16" else F32_PEAK_TFS
+            roof["mfma"] = {"achieved": round(fl / (lk_avg * 1e-3) / 1e12, 1), "peak": peak, "unit": "TFLOP/s",
+                            "frac": round(fl / (lk_avg * 1e-3) / 1e12 / peak, 4), "flops_per_launch": fl}
     else:
         achieved = bd_bytes / (bd_avg * 1e-3) / 1e9
         roof = {"kernel": "build (pack + k_build_bf16/f32)", "bound": "hbm", "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                 "algorithmic_bytes_per_launch": bd_bytes, "avg_launch_ms": round(bd_avg, 4)}
     build_info = {"avg_ms": round(bd_avg, 4), "GB/s": round(bd_bytes / (bd_avg * 1e-3) / 1e9, 1) if bd_avg else None,
-                  "TFLOP/s": round(bd_flops / (bd_avg * 1e-3) / 1e12, 1) if bd_avg else None}
+                  "TFLOP/s": round(bd_flops / (bd_avg * 1e-3) / 1e12, 1) if bd_avg and bd_flops else None}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -243,14 +254,14 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "corr build+lookup voxel-queries/s (128^3 pair, 1/4 encoder)",
+            "metric": f"corr build+lookup voxel-queries/s ({args.encoder * S}^3 pair, 1/{args.encoder} encoder)",
             "value": value, "unit": "voxel-queries/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
             "scaling": "strong" if strong else "weak", "vs_baseline": None,
             "dtype": "bf16" if args.precision == "bf16" else "f32",
             "data": "synthetic: N(0,1) feature maps, coords = identity + U(-2,2), 12 coord fields per step",
-            "config": {"workload": f"corr build + {args.iters} lookups, {S}^3 x {C} fmaps ({4 * S}^3 input, 1/4 "
-                                   f"encoder), L={L}, r={R}, {args.impl}, {args.precision} build / fp32 lookup",
+            "config": {"workload": f"corr build + {args.iters} lookups, {S}^3 x {C} fmaps ({args.encoder * S}^3 "
+                                   f"input, 1/{args.encoder} encoder), L={L}, r={R}, {args.impl}, {args.precision} build / fp32 lookup",
                        "global_batch": B if strong else B * world, "query_voxels": nq_total, "levels": L,
                        "radius": R,
                        "parallelism": (f"query-voxel H-slabs x{world}" if strong else

@@ -32,12 +32,12 @@ run_bench() {
 if [ "${SKIP_BENCH:-0}" != "1" ]; then
   run_bench mat32 ${BENCH_ARGS:-}
   run_bench fused32 --impl fused --no-cpu-baseline
-  run_bench fused128 --impl fused --size 128 --levels 2 --steps 3 --warmup 1
+  run_bench fused128 --impl fused --size 128 --encoder 2 --levels 2 --steps 3 --warmup 1
 fi
 
 if [ "${SKIP_PROF:-0}" != "1" ]; then
   cd /tmp
-  for cfg in "mat32|" "fused32|--impl fused" "fused128|--impl fused --size 128 --levels 2 --steps 2 --warmup 1"; do
+  for cfg in "mat32|" "fused32|--impl fused" "fused128|--impl fused --size 128 --encoder 2 --levels 2 --steps 2 --warmup 1"; do
     name=${cfg%%|*}; args=${cfg#*|}
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$name" -o run \
         -- python "$R/bench.py" --no-cpu-baseline $args > "$OUT/prof_$name.log" 2>&1
