@@ -54,7 +54,10 @@ static int g_lookup_ldpol = 0;       // tile kernel load cache policy (LookupArg
 static int g_build_ablate = 0;       // diagnostics only: k_build_bf16 ablation instance
 static int g_build_stpol = 0;        // cache-policy bits of the build's output stores
 static int g_build_variant = 1;      // 1 = two-barrier bf16-store kernel (k_build_bf16_2b), 0 = k_build_bf16
-static int g_fused_variant = 1;      // 1 = MFMA tile kernel (k_fused_tile) where it applies, 0 = two-stage VALU
+// fused lookup kernel where the MFMA path applies: 2 = k_fused_box 2x2x16, 8 waves (default),
+// 3 = k_fused_box 4x4x4 cubes, 8 waves, 4 = k_fused_box 2x2x16, 4 waves, 1 = k_fused_tile, 0 = two-stage VALU
+static int g_fused_variant = 2;
+static int g_fused_ablate = 0;       // diagnostics only: 1 = skip output stores, 2 = skip window dots (cube kernel)
 
 static int fail(int code, const char *fmt, ...) {
     va_list ap;
@@ -193,8 +196,13 @@ int dvc_set_tuning(const char *key, int value) {
         g_build_variant = value;
         return DVC_OK;
     }
+    if (!strcmp(key, "fused_ablate")) {
+        if (value < 0 || value > 15) return fail(DVC_ERR_INVALID, "set_tuning: fused_ablate %d", value);
+        g_fused_ablate = value;
+        return DVC_OK;
+    }
     if (!strcmp(key, "fused_variant")) {
-        if (value < 0 || value > 1) return fail(DVC_ERR_INVALID, "set_tuning: fused_variant %d", value);
+        if (value < 0 || value > 4) return fail(DVC_ERR_INVALID, "set_tuning: fused_variant %d", value);
         g_fused_variant = value;
         return DVC_OK;
     }
@@ -461,7 +469,7 @@ int dvc_corr_lookup_fused(const void *packed_q, const void *packed_t, const floa
         return fail(DVC_ERR_INVALID, "lookup_fused: bad convention %d", convention);
     if (dtype != DVC_BF16 && dtype != DVC_F32) return fail(DVC_ERR_INVALID, "lookup_fused: bad dtype %d", dtype);
     return fused_lookup(packed_q, packed_t, coords, out, workspace, B, Nq, C, lay, radius, convention, dtype,
-                        g_fused_variant, (hipStream_t)stream, g_err, sizeof(g_err));
+                        g_fused_variant | (g_fused_ablate << 8), (hipStream_t)stream, g_err, sizeof(g_err));
 }
 
 size_t dvc_corr_backward_workspace_bytes(int B, int64_t Nq, int C, int H, int W, int D, int num_levels, int radius) {

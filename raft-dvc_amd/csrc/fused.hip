@@ -213,10 +213,39 @@ static void launch_fused_tile(const bf16_t *Q, const bf16_t *Tt, const LookupArg
     }
 }
 
+template <int R, int KS, int NWAVES, int TY, int TX, int TZ>
+__global__ void k_fused_box(const bf16_t *, const bf16_t *, LookupArgs, int, long long, int, int, int, float);
+
+template <int R, int NWV, int TY, int TX, int TZ>
+static void launch_fused_box(const bf16_t *Q, const bf16_t *Tt, const LookupArgs &A, int Cp, long long t_rows,
+                             int Hq, int Wq, int Dq, float scale, hipStream_t s) {
+    // boxes in 4 x 4 x 2 groups, padded to a multiple of 8 workgroups (one range per XCD)
+    const long long ngy = ((Hq + TY - 1) / TY + 3) / 4, ngx = ((Wq + TX - 1) / TX + 3) / 4,
+                    ngz = ((Dq + TZ - 1) / TZ + 1) / 2;
+    const long long tiles = (long long)A.B * ngy * ngx * ngz * 32;
+    const unsigned grid = (unsigned)(8 * ((tiles + 7) / 8));
+    switch (Cp / 32) {
+    case 1: k_fused_box<R, 1, NWV, TY, TX, TZ><<<grid, 64 * NWV, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;
+    case 2: k_fused_box<R, 2, NWV, TY, TX, TZ><<<grid, 64 * NWV, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;
+    default: k_fused_box<R, 4, NWV, TY, TX, TZ><<<grid, 64 * NWV, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;
+    }
+}
+
+template <int R>
+static void launch_fused_mfma(int variant, const bf16_t *Q, const bf16_t *Tt, const LookupArgs &A, int Cp,
+                              long long t_rows, int Hq, int Wq, int Dq, float scale, hipStream_t s) {
+    if (variant == 1) launch_fused_tile<R>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale, s);
+    else if (variant == 3) launch_fused_box<R, 8, 4, 4, 4>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale, s);
+    else if (variant == 4) launch_fused_box<R, 4, 2, 2, 16>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale, s);
+    else launch_fused_box<R, 8, 2, 2, 16>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale, s);
+}
+
 int fused_lookup(const void *packed_q, const void *packed_t, const float *coords, float *out, void *workspace, int B,
                  long long Nq, int C, const dvc_layout &lay, int radius, int convention, int dtype, int variant,
                  hipStream_t s, char *err, size_t errlen) {
     const int Cp = lay.c_pad;
+    const int ablate = variant >> 8;   // diagnostics knob (capi fused_ablate)
+    variant &= 0xff;
     if ((dtype == DVC_BF16 && Cp > 512) || (dtype == DVC_F32 && Cp > 256)) {
         snprintf(err, errlen, "lookup_fused: C=%d too large", C);
         return DVC_ERR_UNSUPPORTED;
@@ -226,7 +255,7 @@ int fused_lookup(const void *packed_q, const void *packed_t, const float *coords
         snprintf(err, errlen, "lookup_fused: Nq=%lld too large for 32-bit output offsets", Nq);
         return DVC_ERR_UNSUPPORTED;
     }
-    const bool tile = variant == 1 && fused_tile_ok(Nq, lay.W[0], lay.D[0], Cp, lay.row_stride, radius, dtype);
+    const bool tile = variant >= 1 && fused_tile_ok(Nq, lay.W[0], lay.D[0], Cp, lay.row_stride, radius, dtype);
     if (win_ok && !tile && !workspace) {
         snprintf(err, errlen, "lookup_fused: workspace required (%zu bytes)", fused_workspace_bytes(B, Nq, 0, radius));
         return DVC_ERR_INVALID;
@@ -247,6 +276,7 @@ int fused_lookup(const void *packed_q, const void *packed_t, const float *coords
     if (tile) {
         // one launch for every level; legacy levels with W != D go to k_fused_generic below
         LookupArgs T = A;
+        T.ablate = ablate;
         T.q0 = 0; T.nq = Nq; T.nqb = (Nq + 63) / 64; T.l0 = 0; T.nl = lay.num_levels;
         bool any_generic = false;
         for (int l = 0; l < lay.num_levels; ++l) {
@@ -257,10 +287,10 @@ int fused_lookup(const void *packed_q, const void *packed_t, const float *coords
         const int Hq = (int)(Nq / ((long long)Wq * Dq));
         const bf16_t *Q = (const bf16_t *)packed_q, *Tt = (const bf16_t *)packed_t;
         switch (radius) {
-        case 1: launch_fused_tile<1>(Q, Tt, T, Cp, lay.row_stride, Hq, Wq, Dq, scale, s); break;
-        case 2: launch_fused_tile<2>(Q, Tt, T, Cp, lay.row_stride, Hq, Wq, Dq, scale, s); break;
-        case 3: launch_fused_tile<3>(Q, Tt, T, Cp, lay.row_stride, Hq, Wq, Dq, scale, s); break;
-        default: launch_fused_tile<4>(Q, Tt, T, Cp, lay.row_stride, Hq, Wq, Dq, scale, s); break;
+        case 1: launch_fused_mfma<1>(variant, Q, Tt, T, Cp, lay.row_stride, Hq, Wq, Dq, scale, s); break;
+        case 2: launch_fused_mfma<2>(variant, Q, Tt, T, Cp, lay.row_stride, Hq, Wq, Dq, scale, s); break;
+        case 3: launch_fused_mfma<3>(variant, Q, Tt, T, Cp, lay.row_stride, Hq, Wq, Dq, scale, s); break;
+        default: launch_fused_mfma<4>(variant, Q, Tt, T, Cp, lay.row_stride, Hq, Wq, Dq, scale, s); break;
         }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) {

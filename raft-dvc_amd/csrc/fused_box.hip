@@ -1,0 +1,428 @@
+// fused_box.hip -- on-the-fly lookup on MFMA over query boxes, two waves per SIMD
+// (reference semantics: src/core/corr_otf.py:96-237, CorrBlockOnTheFly; the dots are
+// taken at the integer window positions and interpolated, equal by linearity).
+//
+// One workgroup = one TY x TX x TZ box of 64 query voxels (phase 2: lane = query,
+// z fastest), NWAVES waves:
+//
+//   phase 1  the union of the 64 queries' integer windows (2r+2)^3 is a box; its rows
+//            (y, x) x 16-target z blocks are dealt round-robin to the waves.  Per block:
+//            v_mfma_f32_16x16x32_bf16 with the 16 target rows as A (streamed from L2 two
+//            blocks ahead) and the 64 query feature rows as four 16-query B blocks held
+//            in registers for the whole box; a lane ends with 4 consecutive z values of
+//            4 queries, scales and rounds them to bf16 exactly as the materialised build
+//            rounds the corr volume, and writes each value that falls in its query's
+//            integer window straight into that query's dense (2r+2)^3 window in LDS
+//            (the others go to a per-lane scratch slot: no branches, no staging).
+//   phase 2  the window walk of lookup_tile.hip (z-lerp per column run, then the four
+//            (y, x) bilinear terms, packed f32), each wave a few output columns.
+//
+// Box shape.  Output stores are one dword per lane into the channel-major output, so a
+// wave store writes TX*TY segments of 4*TZ bytes: the MI355X write path sustains
+// 5.8 TB/s for 64-byte segments and 0.55 TB/s for 16-byte ones (tools/probe, round 1),
+// so the default box is 2 x 2 x 16 (union 15 x 15 x 29 at +-2 voxel flows, two z
+// blocks per row).  The 4 x 4 x 4 cube has the smallest union (16^3, one z block) but
+// 16-byte segments; it is kept as a tuning variant.
+//
+// Two waves per SIMD (NWAVES = 8, <= 256 VGPRs): one wave's epilogue (VALU + LDS)
+// issues while the other's MFMAs run; with one wave per SIMD every MFMA -> epilogue
+// dependency and LDS round trip is exposed.
+//
+// Nothing is zeroed per level: window slots outside the level are never written and
+// keep earlier finite values (the LDS is cleared once at kernel start); their weights
+// are 0, as in the materialised lookup.  Dots are bit-identical to the bf16 pyramid's
+// (tests/test_gpu_parity.py::test_fused_tile_matches_materialised).
+#include "common.h"
+#include "lookup_common.h"
+
+#include <type_traits>
+
+namespace dvc {
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+template <int R, int NWAVES> struct BoxCfg {
+    static constexpr int n = 2 * R + 1;
+    static constexpr int NW = 2 * R + 2;
+    static constexpr int WROW = NW * 2;                           // bytes of one window z-row (bf16)
+    static constexpr int WQ = NW * NW * WROW + 8;                 // bytes per query window (+8: banks)
+    static constexpr int GUARD = 64;
+    static constexpr int TRASH = GUARD + 64 * WQ;                 // per-lane scratch slots
+    static constexpr int LDS = (TRASH + 64 * 4 + GUARD + 15) & ~15;
+    static constexpr int COLS = NWAVES >= 8 ? 2 : 3;              // output columns per wave (phase 2)
+};
+
+__device__ __forceinline__ int buni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ long long buni64(long long v) {
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((unsigned long long)v >> 32));
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
+template <typename T> __device__ __forceinline__ T *buniptr(T *p) { return (T *)buni64((long long)p); }
+__device__ __forceinline__ int bwave_min(int v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = min(v, __shfl_xor(v, o));
+    return buni(v);
+}
+__device__ __forceinline__ int bwave_max(int v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return buni(v);
+}
+
+template <int n> struct BRun {
+    f32x2 p[n / 2];
+    float t;
+};
+
+template <int R, int KS, int NWAVES, int TY, int TX, int TZ>
+__global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__restrict__ Q,
+                                                              const bf16_t *__restrict__ Tt, LookupArgs A,
+                                                              int Cp, long long t_rows, int Hq, int Wq, int Dq,
+                                                              float scale) {
+    static_assert(TY * TX * TZ == 64, "a box is 64 queries");
+    using C = BoxCfg<R, NWAVES>;
+    constexpr int n = C::n, NW = C::NW, NP = n / 2;
+    constexpr long long n3 = (long long)n * n * n;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[C::LDS];
+    unsigned char *win = smem + C::GUARD;                          // [64 q][NW wy][NW wx][NW z] bf16
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    // XCD-aware box order: workgroup g runs on XCD g % 8 (round-robin dispatch), so each
+    // XCD gets a contiguous range of logical boxes, walked in groups of GY x GX x GZ
+    // neighbouring boxes whose unions overlap in that XCD's L2.
+    constexpr int GY = 4, GX = 4, GZ = 2;
+    const int nty = (Hq + TY - 1) / TY, ntx = (Wq + TX - 1) / TX, ntz = (Dq + TZ - 1) / TZ;
+    const int ngy = (nty + GY - 1) / GY, ngx = (ntx + GX - 1) / GX, ngz = (ntz + GZ - 1) / GZ;
+    const int per_b = ngy * ngx * ngz * (GY * GX * GZ);
+    const int per_xcd = (A.B * per_b + 7) / 8;
+    const int lt = (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
+    if (lt >= A.B * per_b) return;
+    const int b = lt / per_b;
+    const int grp = (lt - b * per_b) / (GY * GX * GZ), wi = (lt - b * per_b) % (GY * GX * GZ);
+    const int tz = (grp % ngz) * GZ + wi % GZ;
+    const int tx = ((grp / ngz) % ngx) * GX + (wi / GZ) % GX;
+    const int ty = (grp / (ngz * ngx)) * GY + wi / (GZ * GX);
+    if (ty >= nty || tx >= ntx || tz >= ntz) return;
+
+    // clear the LDS once: window slots that are never written must hold finite values
+    for (int i = tid * 16; i < C::LDS; i += 64 * NWAVES * 16)
+        *reinterpret_cast<u32x4 *>(smem + i) = u32x4{0, 0, 0, 0};
+
+    // phase-2 lane = query (yi, xi, zi), z fastest
+    const int zi = lane % TZ, xi = (lane / TZ) % TX, yi = lane / (TZ * TX);
+    const int qy = ty * TY + yi, qx = tx * TX + xi, qz = tz * TZ + zi;
+    const bool active = qy < Hq && qx < Wq && qz < Dq;
+    const long long Nq = A.Nq;
+    const long long q = active ? ((long long)qy * Wq + qx) * Dq + qz : 0;
+    const long long qg = A.q0 + q;
+    float cy = 0.f, cx = 0.f, cz = 0.f;
+    if (active) load_coords(A.coords, b, Nq, qg, cy, cx, cz);
+
+    // MFMA B operands, resident for the whole box: block j = box queries 16 j .. 16 j + 15
+    // (lane order), lane i holds query 16 j + (i & 15), channels 32 ks + 8 (i >> 4) .. + 7
+    // (v_mfma_f32_16x16x32_bf16 B layout)
+    const int m16 = lane & 15, h4 = lane >> 4;
+    bf16x8 bq[4][KS];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int s = 16 * j + m16;
+        const int jy = ty * TY + s / (TZ * TX), jx = tx * TX + (s / TZ) % TX, jz = tz * TZ + s % TZ;
+        const bool ok = jy < Hq && jx < Wq && jz < Dq;
+        const long long jq = ok ? ((long long)jy * Wq + jx) * Dq + jz : 0;
+        const bf16_t *row = Q + ((long long)b * Nq + A.q0 + jq) * Cp;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+            bq[j][ks] = *reinterpret_cast<const bf16x8 *>(row + 32 * ks + 8 * h4);
+    }
+    // packed targets of this batch element as a buffer: rows past the union's z range are
+    // addressed out of range and read as zeros.  num_records is the exact byte size
+    // (< 2^31 - 64 KB, checked on the host; the hardware range-checks every dword).
+    const bf16_t *tb = Tt + (long long)b * t_rows * Cp;
+    const unsigned long long tbp = (unsigned long long)tb;
+    const unsigned tblo = __builtin_amdgcn_readfirstlane((unsigned)tbp);
+    const unsigned tbhi = __builtin_amdgcn_readfirstlane((unsigned)(tbp >> 32));
+    const int t_bytes = (int)(t_rows * Cp * 2);
+    const __amdgpu_buffer_rsrc_t rs_t = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(((unsigned long long)tbhi << 32) | tblo), (short)0, t_bytes, 0x00020000);
+
+    const int legacy = buni(A.legacy);
+    const int chstep_u = legacy ? 1 : n;
+    const int chstep_v = legacy ? n : 1;
+    const int q4 = active ? (int)(qg * 4) : 0x7ffffff0;
+    const int vstep = buni((int)(chstep_v * Nq * 4));
+    const int out_bytes = buni((int)(n * n * Nq * 4));
+    const f32x2 sc2 = {scale, scale};
+    const int trash = C::TRASH + lane * 4;
+    const int ablate = buni(A.ablate);
+    unsigned sink = 0;
+    const int u0 = wave * C::COLS;
+    __syncthreads();   // LDS cleared
+
+    auto out_rsrc = [&](float *obase, int a, int u) {
+        return __builtin_amdgcn_make_buffer_rsrc(
+            buniptr(obase + ((long long)a * n * n + (long long)u * chstep_u) * Nq), (short)0, out_bytes, 0x00020000);
+    };
+    auto store = [&](__amdgpu_buffer_rsrc_t rs, int v, float val) {
+        if (!(ablate & 1)) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val), rs, q4, v * vstep, 2);
+    };
+
+    auto level = [&](int l, auto nu_c) {
+        constexpr int NU = decltype(nu_c)::value;
+        float *obase = buniptr(A.out + ((long long)b * A.Ltot + l) * n3 * Nq);
+        if (buni(A.zero[l])) {
+            if constexpr (NU > 0) {
+                for (int a = 0; a < n; ++a)
+#pragma unroll
+                    for (int uu = 0; uu < NU; ++uu) {
+                        const __amdgpu_buffer_rsrc_t rs = out_rsrc(obase, a, u0 + uu);
+#pragma unroll
+                        for (int v = 0; v < n; ++v) store(rs, v, 0.0f);
+                    }
+            }
+            return;
+        }
+        const int Hl = buni(A.H[l]), Wl = buni(A.W[l]), Dl = buni(A.D[l]), Dpl = buni(A.Dp[l]);
+        const long long offl = buni64(A.off[l]);
+        const float sc = (float)(1 << l);
+        WinAxes ax;
+        window_axes(cy / sc, cx / sc, cz / sc, Hl, Wl, Dl, legacy, ax);
+        const int ih = (int)ax.kh - R, iu = (int)ax.ku - R, iv = (int)ax.kv - R;
+        const bool live = active && !ax.dead;
+
+        const int BIG = 1 << 29;
+        const int ys = max(bwave_min(live ? ih : BIG), 0), ye = min(bwave_max(live ? ih : -BIG) + NW - 1, Hl - 1);
+        const int xs = max(bwave_min(live ? iu : BIG), 0), xe = min(bwave_max(live ? iu : -BIG) + NW - 1, Wl - 1);
+        const int zs = max(bwave_min(live ? iv : BIG), 0), ze = min(bwave_max(live ? iv : -BIG) + NW - 1, Dl - 1);
+        const int ny = ye - ys + 1, nx = xe - xs + 1, nz = ze - zs + 1;
+        const int nzb = (nz + 15) / 16;
+
+        // per B block j: this lane's query is 16 j + m16; its window origin and LDS base.
+        // A value of target (y, x, z) lands at
+        //   win + q * WQ + ((y - ih) * NW + (x - iu)) * WROW + (z - iv) * 2
+        // = wb[j] + (y * NW + x) * WROW + z * 2            (wb[j] folds the query's part)
+        int oh[4], ou[4], ov[4], wb[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int src = 16 * j + m16;
+            const int sh = __shfl(ih, src);                 // |ih| < 2^20: finite or "dead" origins
+            oh[j] = __shfl((int)live, src) ? sh : -BIG;     // dead / inactive queries take no values
+            ou[j] = __shfl(iu, src);
+            ov[j] = __shfl(iv, src) - 4 * h4;               // lane holds z = z0 + 4 h4 + k
+            wb[j] = C::GUARD + src * C::WQ - (sh * NW + ou[j]) * C::WROW - ov[j] * 2;
+        }
+
+        __syncthreads();   // previous level's phase-2 reads are done
+
+        // ---------------- phase 1: window dots on MFMA ----------------
+        if (ny > 0 && nx > 0 && nz > 0 && !(ablate & 2)) {
+            // this wave's iterations it = wave + NWAVES k over (row, z block), row-major,
+            // z block fastest; (by, bx, zb) advance without divisions
+            const int total = ny * nx * nzb;
+            const int nit = total > wave ? (total - wave + NWAVES - 1) / NWAVES : 0;
+            const int dzb = NWAVES % nzb, dblk = NWAVES / nzb;
+            struct Pos { int by, bx, zb; };
+            auto advance = [&](Pos &p) {
+                p.zb += dzb;
+                p.bx += dblk;
+                if (p.zb >= nzb) { p.zb -= nzb; p.bx += 1; }
+                while (p.bx >= nx) { p.bx -= nx; p.by += 1; }
+            };
+            Pos pl;   // position of the next load
+            {
+                const int blk = wave / nzb;
+                pl.zb = wave - blk * nzb;
+                pl.by = blk / nx;
+                pl.bx = blk - pl.by * nx;
+            }
+            Pos pe = pl;   // position of the next epilogue
+            auto load_a = [&](bf16x8 (&dst)[KS]) {
+                const int z0 = zs + 16 * pl.zb;
+                const long long rowbase = offl + ((long long)(ys + pl.by) * Wl + (xs + pl.bx)) * Dpl;
+                const int off = z0 + m16 <= ze ? (int)(((rowbase + z0 + m16) * Cp + 8 * h4) * 2) : 0x7fff0000;
+                advance(pl);
+                if (ablate & 4) {   // diagnostics: no target loads
+#pragma unroll
+                    for (int ks = 0; ks < KS; ++ks) dst[ks] = bq[0][ks];
+                    return;
+                }
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks)
+                    dst[ks] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs_t, off + 64 * ks, 0, 0));
+            };
+            auto mfma = [&](const bf16x8 (&a)[KS], f32x4 (&acc)[4]) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], bq[j][ks], acc[j], 0, 0, 0);
+            };
+            auto epilogue = [&](const f32x4 (&acc)[4]) {
+                const int z0 = zs + 16 * pe.zb;
+                const int y = ys + pe.by, x = xs + pe.bx;
+                advance(pe);
+                const int rowu = (y * NW + x) * C::WROW + z0 * 2;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const f32x2 lo = f32x2{acc[j][0], acc[j][1]} * sc2;
+                    const f32x2 hi = f32x2{acc[j][2], acc[j][3]} * sc2;
+                    const unsigned p01 = __builtin_bit_cast(unsigned, __builtin_convertvector(lo, bf16x2));
+                    const unsigned p23 = __builtin_bit_cast(unsigned, __builtin_convertvector(hi, bf16x2));
+                    if (ablate & 8) {   // diagnostics: no window writes (keep the values live)
+                        sink ^= p01 ^ p23;
+                        continue;
+                    }
+                    const bool rok = (unsigned)(y - oh[j]) < (unsigned)NW && (unsigned)(x - ou[j]) < (unsigned)NW;
+                    const int t0 = z0 - ov[j];                   // window z of this lane's k = 0 value
+                    const int base = wb[j] + rowu;
+                    const int a0 = rok && (unsigned)(t0 + 0) < (unsigned)NW ? base + 0 : trash;
+                    const int a1 = rok && (unsigned)(t0 + 1) < (unsigned)NW ? base + 2 : trash;
+                    const int a2 = rok && (unsigned)(t0 + 2) < (unsigned)NW ? base + 4 : trash;
+                    const int a3 = rok && (unsigned)(t0 + 3) < (unsigned)NW ? base + 6 : trash;
+                    *reinterpret_cast<unsigned short *>(smem + a0) = (unsigned short)p01;
+                    *reinterpret_cast<unsigned short *>(smem + a1) = (unsigned short)(p01 >> 16);
+                    *reinterpret_cast<unsigned short *>(smem + a2) = (unsigned short)p23;
+                    *reinterpret_cast<unsigned short *>(smem + a3) = (unsigned short)(p23 >> 16);
+                }
+            };
+            // two operand sets in flight; the MFMAs of iteration k + 1 are issued before the
+            // epilogue of iteration k
+            bf16x8 a0[KS], a1[KS];
+            f32x4 c0[4], c1[4];
+            if (nit > 0) load_a(a0);
+            if (nit > 1) load_a(a1);
+            if (nit > 0) {
+                mfma(a0, c0);
+                if (nit > 2) load_a(a0);
+            }
+            for (int k = 0; k < nit; k += 2) {
+                if (k + 1 < nit) {
+                    mfma(a1, c1);
+                    if (k + 3 < nit) load_a(a1);
+                }
+                epilogue(c0);
+                if (k + 1 < nit) {
+                    if (k + 2 < nit) {
+                        mfma(a0, c0);
+                        if (k + 4 < nit) load_a(a0);
+                    }
+                    epilogue(c1);
+                }
+            }
+        }
+        __syncthreads();   // every window complete
+        if constexpr (NU == 0) return;
+
+        // ---------------- phase 2: interpolation from the windows ----------------
+        const unsigned char *myw = win + lane * C::WQ;
+        float wv0[n], wv1[n];
+#pragma unroll
+        for (int tt = 0; tt < n; ++tt) {
+            axis_weights(ax.pv, ax.kv, tt - R, ax.vn, ax.vu, wv0[tt], wv1[tt]);
+            wv0[tt] = (unsigned)(iv + tt) < (unsigned)Dl ? wv0[tt] : 0.0f;
+            wv1[tt] = (unsigned)(iv + tt + 1) < (unsigned)Dl ? wv1[tt] : 0.0f;
+        }
+        f32x2 w0p[NP], w1p[NP];
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+            w0p[i] = f32x2{wv0[2 * i], wv0[2 * i + 1]};
+            w1p[i] = f32x2{wv1[2 * i], wv1[2 * i + 1]};
+        }
+        float wx0[NU > 0 ? NU : 1], wx1[NU > 0 ? NU : 1];
+#pragma unroll
+        for (int uu = 0; uu < NU; ++uu) {
+            const int u = u0 + uu;
+            axis_weights(ax.pu, ax.ku, u - R, ax.un, ax.uu, wx0[uu], wx1[uu]);
+            wx0[uu] = (unsigned)(iu + u) < (unsigned)Wl ? wx0[uu] : 0.0f;
+            wx1[uu] = (unsigned)(iu + u + 1) < (unsigned)Wl ? wx1[uu] : 0.0f;
+        }
+        auto lerp_col = [&](int wp, int k, BRun<n> &z) {
+            const unsigned *p = reinterpret_cast<const unsigned *>(myw + (wp * NW + u0 + k) * C::WROW);
+            float r[NW];
+#pragma unroll
+            for (int i = 0; i < NW / 2; ++i) {
+                const unsigned w = p[i];
+                r[2 * i] = __uint_as_float(w << 16);
+                r[2 * i + 1] = __uint_as_float(w & 0xffff0000u);
+            }
+#pragma unroll
+            for (int i = 0; i < NP; ++i)
+                z.p[i] = __builtin_elementwise_fma(f32x2{r[2 * i + 1], r[2 * i + 2]}, w1p[i],
+                                                   f32x2{r[2 * i], r[2 * i + 1]} * w0p[i]);
+            z.t = __builtin_fmaf(r[n], wv1[n - 1], r[n - 1] * wv0[n - 1]);
+        };
+        BRun<n> zp[NU + 1];
+#pragma unroll
+        for (int k = 0; k <= NU; ++k) lerp_col(0, k, zp[k]);
+#pragma unroll
+        for (int a = 0; a < n; ++a) {
+            float wy0, wy1;
+            axis_weights(ax.ph, ax.kh, a - R, ax.hs, ax.hs, wy0, wy1);
+            wy0 = (unsigned)(ih + a) < (unsigned)Hl ? wy0 : 0.0f;
+            wy1 = (unsigned)(ih + a + 1) < (unsigned)Hl ? wy1 : 0.0f;
+            BRun<n> zprev;
+#pragma unroll
+            for (int k = 0; k <= NU; ++k) {
+                BRun<n> zcur;
+                lerp_col(a + 1, k, zcur);
+                if (k >= 1) {
+                    const int uu = k - 1;
+                    const float p00 = wx0[uu] * wy0, p10 = wx1[uu] * wy0;
+                    const float p01 = wx0[uu] * wy1, p11 = wx1[uu] * wy1;
+                    const f32x2 P00 = {p00, p00}, P10 = {p10, p10}, P01 = {p01, p01}, P11 = {p11, p11};
+                    const __amdgpu_buffer_rsrc_t rs = out_rsrc(obase, a, u0 + uu);
+#pragma unroll
+                    for (int i = 0; i < NP; ++i) {
+                        f32x2 acc = P00 * zp[uu].p[i];
+                        acc = __builtin_elementwise_fma(P10, zp[uu + 1].p[i], acc);
+                        acc = __builtin_elementwise_fma(P01, zprev.p[i], acc);
+                        acc = __builtin_elementwise_fma(P11, zcur.p[i], acc);
+                        store(rs, 2 * i, acc[0]);
+                        store(rs, 2 * i + 1, acc[1]);
+                    }
+                    float acc = p00 * zp[uu].t;
+                    acc = __builtin_fmaf(p10, zp[uu + 1].t, acc);
+                    acc = __builtin_fmaf(p01, zprev.t, acc);
+                    acc = __builtin_fmaf(p11, zcur.t, acc);
+                    store(rs, n - 1, acc);
+                    zp[uu] = zprev;
+                }
+                zprev = zcur;
+                if (k == NU) zp[k] = zcur;
+            }
+        }
+    };
+
+    // phase-2 roles: wave w owns output columns [w COLS, w COLS + NU); waves past the
+    // columns take part in phase 1 and the barriers only
+    constexpr int COLS = C::COLS;
+    constexpr int NWC = (n + COLS - 1) / COLS;   // waves with output columns (<= NWAVES)
+    static_assert(NWC <= NWAVES, "not enough waves for the output columns");
+    constexpr int NU_LAST = n - COLS * (NWC - 1);
+    for (int l = A.l0; l < A.l0 + A.nl; ++l) {
+        if (buni(A.generic[l]) && !buni(A.zero[l])) continue;   // legacy level with W != D: k_fused_generic
+        if (wave < NWC - 1) level(l, std::integral_constant<int, COLS>{});
+        else if (wave == NWC - 1) level(l, std::integral_constant<int, NU_LAST>{});
+        else level(l, std::integral_constant<int, 0>{});
+    }
+    if ((ablate & 8) && sink == 0x9e3779b9u) A.out[0] = (float)sink;   // keeps the diagnostics' dots live
+}
+
+#define DVC_FBOX_INST1(R, KS, NWV, TY, TX, TZ)                                                                 \
+    template __global__ void k_fused_box<R, KS, NWV, TY, TX, TZ>(const bf16_t *, const bf16_t *, LookupArgs, int, \
+                                                                 long long, int, int, int, float);
+#define DVC_FBOX_INST(R, NWV, TY, TX, TZ)                                                                      \
+    DVC_FBOX_INST1(R, 1, NWV, TY, TX, TZ) DVC_FBOX_INST1(R, 2, NWV, TY, TX, TZ) DVC_FBOX_INST1(R, 4, NWV, TY, TX, TZ)
+#define DVC_FBOX_ALLR(NWV, TY, TX, TZ)                                                                         \
+    DVC_FBOX_INST(1, NWV, TY, TX, TZ) DVC_FBOX_INST(2, NWV, TY, TX, TZ) DVC_FBOX_INST(3, NWV, TY, TX, TZ)       \
+    DVC_FBOX_INST(4, NWV, TY, TX, TZ)
+DVC_FBOX_ALLR(8, 2, 2, 16)
+DVC_FBOX_ALLR(4, 2, 2, 16)
+DVC_FBOX_ALLR(8, 4, 4, 4)
+
+}  // namespace dvc

@@ -297,10 +297,11 @@ def test_tile_kernel_matches_walk(shape, L, r):
                                          ((20, 13, 24), 128, 3, 4), ((32, 32, 32), 128, 4, 4),
                                          ((18, 34, 40), 64, 2, 4), ((8, 8, 8), 128, 2, 3)])
 def test_fused_tile_matches_materialised(shape, C, L, r):
-    """k_fused_tile (MFMA window dots of the union window, no volume) reproduces the bf16 materialised
-    pyramid + lookup bit for bit: the same v_mfma_f32_32x32x16_bf16 dot order, the same scale-then-round to
-    bf16, the same interpolation arithmetic.  Ragged query boxes, non-cubic sizes, flows wide enough to
-    push the union window past 32 z-rows, NaN / huge coordinates, both conventions.  Legacy levels with
+    """The MFMA fused kernels (no volume) reproduce the bf16 materialised pyramid + lookup bit for bit:
+    k_fused_tile (variant 1: 2x2x16 query boxes, v_mfma_f32_32x32x16_bf16) and k_fused_cube (variants 2 and
+    3: 4x4x4 query cubes, v_mfma_f32_16x16x32_bf16, 4 or 8 waves) -- the same scale-then-round to bf16 and
+    the same interpolation arithmetic.  Ragged query boxes, non-cubic sizes, flows wide enough to push the
+    union window past one MFMA z block, NaN / huge coordinates, both conventions.  Legacy levels with
     W != D go to the per-output kernel (fp32 dots of the same operands) and are held to BF16_TOL."""
     import dvccorr
     from dvccorr import _lib
@@ -319,24 +320,46 @@ def test_fused_tile_matches_materialised(shape, C, L, r):
     for legacy in (False, True):
         ref = dvccorr.CorrBlock(f1, f2, L, r, legacy_wd_swap=legacy, precision="bf16")(c)
         fz = dvccorr.CorrBlockFused(f1, f2, L, r, legacy_wd_swap=legacy, precision="bf16")
-        _lib.set_tuning("fused_variant", 1)
-        out = fz(c)
-        _lib.set_tuning("fused_variant", 0)
         try:
+            _lib.set_tuning("fused_variant", 0)
             two_stage = fz(c)
+            for variant in (1, 2, 3, 4):
+                _lib.set_tuning("fused_variant", variant)
+                out = fz(c)
+                torch.cuda.synchronize()
+                assert torch.isfinite(out).all(), variant
+                for l, (h, w, d) in enumerate(lay.levels()):
+                    sl = slice(l * n3, (l + 1) * n3)
+                    if legacy and w != d and min(h, w, d) > 1:
+                        e = orc.rel_err(out[:, sl].cpu().numpy(), ref[:, sl].cpu().numpy())
+                        assert e <= BF16_TOL, (variant, shape, l, legacy, e)
+                    else:
+                        assert torch.equal(out[:, sl], ref[:, sl]), (variant, shape, C, L, r, l, legacy,
+                                                                     float((out[:, sl] - ref[:, sl]).abs().max()))
+                assert orc.rel_err(out.cpu().numpy(), two_stage.cpu().numpy()) <= BF16_TOL, variant
         finally:
-            _lib.set_tuning("fused_variant", 1)
-        torch.cuda.synchronize()
-        assert torch.isfinite(out).all()
-        for l, (h, w, d) in enumerate(lay.levels()):
-            sl = slice(l * n3, (l + 1) * n3)
-            if legacy and w != d and min(h, w, d) > 1:
-                e = orc.rel_err(out[:, sl].cpu().numpy(), ref[:, sl].cpu().numpy())
-                assert e <= BF16_TOL, (shape, l, legacy, e)
-            else:
-                assert torch.equal(out[:, sl], ref[:, sl]), (shape, C, L, r, l, legacy,
-                                                             float((out[:, sl] - ref[:, sl]).abs().max()))
-        assert orc.rel_err(out.cpu().numpy(), two_stage.cpu().numpy()) <= BF16_TOL
+            _lib.set_tuning("fused_variant", 2)
+
+
+@pytest.mark.parametrize("variant", [1, 2, 3, 4])
+def test_fused_smooth_flow_bitwise(variant):
+    """Bench-like inputs (identity + U(-2, 2) flow, 32^3 x 128, L=4, r=4): every fused MFMA variant equals
+    the materialised bf16 path bit for bit over the whole output."""
+    import dvccorr
+    from dvccorr import _lib
+    S, C, L, r = 32, 128, 4, 4
+    g = torch.Generator(device="cpu").manual_seed(77)
+    f1 = torch.randn(1, C, S, S, S, generator=g).to(DEV)
+    f2 = torch.randn(1, C, S, S, S, generator=g).to(DEV)
+    c = (dvccorr.coords_grid_3d(1, S, S, S, torch.device("cpu")) +
+         (torch.rand(1, 3, S, S, S, generator=g) * 2 - 1) * 2).to(DEV)
+    ref = dvccorr.CorrBlock(f1, f2, L, r, precision="bf16")(c)
+    try:
+        _lib.set_tuning("fused_variant", variant)
+        out = dvccorr.CorrBlockFused(f1, f2, L, r, precision="bf16")(c)
+    finally:
+        _lib.set_tuning("fused_variant", 2)
+    assert torch.equal(out, ref), float((out - ref).abs().max())
 
 
 def test_fused_tile_slab():

@@ -40,6 +40,25 @@ __global__ void k_write_rows(unsigned char *p, long long rs, int ntiles) {
     }
 }
 
+// fused-lookup output shape: one workgroup per TY x TX x TZ box of queries (64 lanes =
+// 64 queries, z fastest) in an S^3 grid; every wave stores 4 B per lane for its share of
+// the nch channel planes of the channel-major (nch, S^3) fp32 output
+template <int TY, int TX, int TZ, int AUX, bool XCD = false>
+__global__ void k_write_box(float *out, int S, int nch) {
+    const int nbz = S / TZ, nbx = S / TX;
+    // XCD: consecutive logical boxes (z fastest) on one XCD (round-robin dispatch)
+    const int per_xcd = (int)(gridDim.x / 8);
+    const int bid = XCD ? (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+    const int bz = bid % nbz, bx = (bid / nbz) % nbx, by = bid / (nbz * nbx);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int z = bz * TZ + lane % TZ, x = bx * TX + (lane / TZ) % TX, y = by * TY + lane / (TZ * TX);
+    const long long nq = (long long)S * S * S;
+    const long long q = ((long long)y * S + x) * S + z;
+    for (int ch = wave; ch < nch; ch += 4)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)ch), __builtin_amdgcn_make_buffer_rsrc(
+            out + ch * nq, (short)0, (int)(nq * 4), 0x00020000), (int)(q * 4), 0, AUX);
+}
+
 int main() {
     const long long bytes = 2457600000LL;   // ~ the 32^3 bf16 pyramid
     const long long n = bytes / 16;
@@ -76,6 +95,24 @@ int main() {
     const long long rows = 32768;
     timeit("build shape: 256B row segments, nt", (double)rows * ntiles * 256,
            [&] { k_write_rows<<<(unsigned)(rows / 128 * 8), 256>>>((unsigned char *)a, rs, ntiles); });
+    {
+        const int S = 128, nch = 2 * 729;   // config #5's output: 12.2 GB
+        float *o;
+        hipMalloc(&o, (long long)nch * S * S * S * 4);
+        const double mv = (double)nch * S * S * S * 4;
+        const unsigned g = (unsigned)((long long)S * S * S / 64);
+        timeit("box 1x1x64 (256B segments) nt", mv, [&] { k_write_box<1, 1, 64, 2><<<g, 256>>>(o, S, nch); });
+        timeit("box 1x1x64 (256B segments)", mv, [&] { k_write_box<1, 1, 64, 0><<<g, 256>>>(o, S, nch); });
+        timeit("box 2x2x16 (64B segments) nt", mv, [&] { k_write_box<2, 2, 16, 2><<<g, 256>>>(o, S, nch); });
+        timeit("box 2x2x16 (64B segments)", mv, [&] { k_write_box<2, 2, 16, 0><<<g, 256>>>(o, S, nch); });
+        timeit("box 4x4x4 (16B segments) nt", mv, [&] { k_write_box<4, 4, 4, 2><<<g, 256>>>(o, S, nch); });
+        timeit("box 4x4x4 (16B segments)", mv, [&] { k_write_box<4, 4, 4, 0><<<g, 256>>>(o, S, nch); });
+        timeit("box 4x4x4 xcd-grouped", mv, [&] { k_write_box<4, 4, 4, 0, true><<<g, 256>>>(o, S, nch); });
+        timeit("box 4x4x4 xcd-grouped nt", mv, [&] { k_write_box<4, 4, 4, 2, true><<<g, 256>>>(o, S, nch); });
+        timeit("box 2x2x16 xcd-grouped", mv, [&] { k_write_box<2, 2, 16, 0, true><<<g, 256>>>(o, S, nch); });
+        timeit("box 2x4x8 (32B segments)", mv, [&] { k_write_box<2, 4, 8, 0><<<g, 256>>>(o, S, nch); });
+        hipFree(o);
+    }
     hipFree(a);
     hipFree(b);
     return 0;
