@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--impl", default="materialised", choices=["materialised", "fused"])
     ap.add_argument("--max-flow", type=float, default=2.0)
+    ap.add_argument("--convc1", nargs="?", const="fused", default=None, choices=["fused", "unfused"],
+                    help="each lookup also applies MotionEncoder.convc1 + ReLU: fused into the lookup "
+                         "(dvc_corr_lookup_proj) or unfused (lookup, then torch conv3d + relu on the GPU)")
     ap.add_argument("--gather-output", action="store_true", help="strong scaling: all-gather every lookup output")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm); gloo only for rehearsals")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
@@ -65,7 +68,7 @@ def parse():
     return ap.parse_args()
 
 
-def lookup_algorithmic_bytes(coords: torch.Tensor, dims, radius: int, store_bytes: int) -> float:
+def lookup_algorithmic_bytes(coords: torch.Tensor, dims, radius: int, store_bytes: int, out_bytes=None) -> float:
     """sum_q [ sum_l |W_l(q)| * store_bytes + 4 * L * (2r+1)^3 + 12 ].
 
     |W_l(q)| = prod_axes |[k - r, k + r + 1] intersect [0, S - 1]|, k = floor(coord / 2^l);
@@ -85,7 +88,8 @@ def lookup_algorithmic_bytes(coords: torch.Tensor, dims, radius: int, store_byte
             hi = torch.clamp(k + radius + 1, max=S - 1)
             tot = tot * torch.clamp(hi - lo + 1, min=0)
         win = win + tot.sum()
-    return float(win.item()) * store_bytes + nq * (4.0 * L * n3 + 12.0)
+    out_q = 4.0 * L * n3 if out_bytes is None else out_bytes   # --convc1: 96 fp32 per query instead
+    return float(win.item()) * store_bytes + nq * (out_q + 12.0)
 
 
 def cpu_baseline(args, f1, f2, coords_list):
@@ -162,6 +166,11 @@ def main():
     group = None
 
     ev = {"lookup": [], "build": []}
+    proj_w = proj_b = None
+    if args.convc1:   # random-init convc1 (Conv3d(L (2r+1)^3, 96, 1) default init range, update.py:222)
+        K = L * (2 * R + 1) ** 3
+        proj_w = ((torch.rand(96, K, generator=g) * 2 - 1) / K ** 0.5).to(dev)
+        proj_b = ((torch.rand(96, generator=g) * 2 - 1) / K ** 0.5).to(dev)
 
     def step(timed: bool):
         blk = ShardedCorrBlock(f1_slab, f2_slab, S, L, R, precision=args.precision, impl=args.impl,
@@ -172,7 +181,12 @@ def main():
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
-            blk(coords_slab[i])
+            if args.convc1 == "fused":
+                blk.lookup_convc1(coords_slab[i], proj_w, proj_b)
+            elif args.convc1 == "unfused":
+                torch.relu(torch.nn.functional.conv3d(blk(coords_slab[i]), proj_w.view(96, -1, 1, 1, 1), proj_b))
+            else:
+                blk(coords_slab[i])
             if timed:
                 e1.record(stream)
                 ev["lookup"].append((e0, e1))
@@ -204,7 +218,8 @@ def main():
     value = args.iters * nq_total * args.steps / elapsed
 
     # roofline of the dominant kernel (by time per step, rank 0's view)
-    lk_bytes = sum(lookup_algorithmic_bytes(c, dims, R, store_bytes if args.impl == "materialised" else 0)
+    lk_bytes = sum(lookup_algorithmic_bytes(c, dims, R, store_bytes if args.impl == "materialised" else 0,
+                                            96 * 4.0 if args.convc1 == "fused" else None)
                    for c in coords_slab) / len(coords_slab)
     unpadded = sum(h * w * d for (h, w, d) in dims)
     n_targets = S * S * S
@@ -218,16 +233,19 @@ def main():
     if os.path.exists(args.traffic_file):
         try:
             tf = json.load(open(args.traffic_file))
-            key = f"{args.impl}_{args.precision}_{S}_L{L}_r{R}_n{world if strong else 1}"
+            key = f"{args.impl}_{args.precision}_{S}_L{L}_r{R}_n{world if strong else 1}" + \
+                (f"_convc1_{args.convc1}" if args.convc1 else "")
             traffic = tf.get(key, {}).get("lookup_hbm_bytes_per_launch")
         except Exception:
             traffic = None
     if args.iters * lk_avg >= bd_avg or args.impl == "fused":
         achieved = lk_bytes / (lk_avg * 1e-3) / 1e9
         if args.impl == "materialised":
-            kname = "k_lookup_tile (dvc_corr_lookup)"
+            kname = {"fused": "k_lookup_tile<PROJ> (dvc_corr_lookup_proj, convc1 fused)",
+                     "unfused": "k_lookup_tile (dvc_corr_lookup) + torch conv3d/relu (timed together)"}.get(
+                         args.convc1, "k_lookup_tile (dvc_corr_lookup)")
         elif args.precision == "bf16" and 1 <= R <= 4:
-            kname = "k_fused_tile (dvc_corr_lookup_fused)"
+            kname = "k_fused_box (dvc_corr_lookup_fused)"
         else:
             kname = "k_fused_dots + k_lookup_win (dvc_corr_lookup_fused)"
         roof = {"kernel": kname,
@@ -260,7 +278,7 @@ def main():
             "scaling": "strong" if strong else "weak", "vs_baseline": None,
             "dtype": "bf16" if args.precision == "bf16" else "f32",
             "data": "synthetic: N(0,1) feature maps, coords = identity + U(-2,2), 12 coord fields per step",
-            "config": {"workload": f"corr build + {args.iters} lookups, {S}^3 x {C} fmaps ({args.encoder * S}^3 "
+            "config": {"workload": f"corr build + {args.iters} lookups{f' + convc1 ({args.convc1})' if args.convc1 else ''}, {S}^3 x {C} fmaps ({args.encoder * S}^3 "
                                    f"input, 1/{args.encoder} encoder), L={L}, r={R}, {args.impl}, {args.precision} build / fp32 lookup",
                        "global_batch": B if strong else B * world, "query_voxels": nq_total, "levels": L,
                        "radius": R,

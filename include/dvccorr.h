@@ -23,6 +23,8 @@
  *                             avg_pool3d, grid_sample) / the CUDA OTF         src/core/cuda/corr_otf_cuda.cu:247-441,
  *                             backward launcher                               :491-530
  *   dvc_sample3d           -- bilinear_sampler_3d                             src/core/corr.py:17-68
+ *   dvc_proj_pack,         -- CorrBlock.__call__ followed by the motion       src/core/corr.py:169-208 +
+ *   dvc_corr_lookup_proj      encoder's F.relu(self.convc1(corr))            src/core/update.py:219-222, 246
  *
  * Layouts (row-major, element counts):
  *   fmap           (B, C, H, W, D) float32, channels-first, contiguous   (reference layout)
@@ -138,6 +140,26 @@ size_t dvc_corr_backward_workspace_bytes(int B, int64_t Nq, int C, int H, int W,
 int dvc_corr_backward(const void *packed_q, const void *packed_t, const float *coords, const float *grad_out,
                       float *grad_fmap1, float *grad_fmap2, void *workspace, int B, int64_t Nq, int C, int H, int W,
                       int D, int num_levels, int radius, int convention, int dtype, void *stream);
+
+/* Lookup with the motion encoder's convc1 (1x1x1 Conv3d L*(2r+1)^3 -> 96, + ReLU,
+ * update.py:222, 246) fused into its epilogue: the L*(2r+1)^3-channel lookup output
+ * never reaches HBM.
+ *   dvc_proj_pack: convc1.weight viewed (96, L*(2r+1)^3) float32 -> packed bf16
+ *     weights (dvc_proj_packed_bytes) in the kernel's MFMA operand order for one
+ *     (num_levels, radius, convention); pack once per weight update.
+ *   dvc_corr_lookup_proj: out (B, 96, Nq) float32 = relu(W . lookup(coords) + bias),
+ *     bias (96) float32.  The lookup values and the weights enter bf16 MFMA with
+ *     float32 accumulation (tolerance 1e-2 max-normalised against the float32
+ *     reference).  Supported: radius 1..4, tile-kernel row widths, and for the legacy
+ *     convention W == D at every non-zero level (DVC_ERR_UNSUPPORTED otherwise). */
+#define DVC_PROJ_COUT 96
+#define DVC_PROJ_MAX_RADIUS 4
+size_t dvc_proj_packed_bytes(int num_levels, int radius);
+int dvc_proj_pack(const float *weight, void *packed, int cout, int num_levels, int radius, int convention,
+                  void *stream);
+int dvc_corr_lookup_proj(const void *corr, const float *coords, const void *packed_w, const float *bias, float *out,
+                         int B, int64_t Nq, int H, int W, int D, int num_levels, int radius, int convention,
+                         int store_dtype, void *stream);
 
 /* bilinear_sampler_3d: vol (B, C, Hv, Wv, Dv), pts (B, Nq, 3) in (h, w, d) -> out (B, C, Nq). */
 int dvc_sample3d(const float *vol, const float *pts, float *out, int B, int C, int Hv, int Wv, int Dv, int64_t Nq,

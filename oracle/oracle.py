@@ -132,6 +132,19 @@ def corr_lookup(fmap1, fmap2, coords, num_levels: int = 4, radius: int = 4, lega
     return np.ascontiguousarray(out.reshape(B, N, -1).transpose(0, 2, 1)).reshape(B, -1, H, W, D)
 
 
+def motion_convc1(lookup_out, weight, bias) -> np.ndarray:
+    """MotionEncoder's first layer on a lookup output: relu(conv1x1(corr, W) + b), float64.
+
+    Reference src/core/update.py:219-222 (Conv3d(L*(2r+1)**3, 96, kernel_size=1)) and :246
+    (F.relu(self.convc1(corr))).  lookup_out (B, K, H, W, D), weight (96, K[, 1, 1, 1]),
+    bias (96,) -> (B, 96, H, W, D)."""
+    x = np.asarray(lookup_out, np.float64)
+    B, K = x.shape[:2]
+    w = np.asarray(weight, np.float64).reshape(-1, K)
+    y = np.einsum("ok,bkn->bon", w, x.reshape(B, K, -1)) + np.asarray(bias, np.float64)[None, :, None]
+    return np.maximum(y, 0.0).reshape(B, w.shape[0], *x.shape[2:])
+
+
 def sample(vol, pts, legacy: bool = False) -> np.ndarray:
     """bilinear_sampler_3d: vol (B,C,H,W,D), pts (B,H',W',D',3) -> (B,C,H',W',D') float64."""
     v, p = _f32(vol), _f32(pts)

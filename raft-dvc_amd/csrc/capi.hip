@@ -30,7 +30,8 @@ template <typename T>
 __global__ void k_corr_pool(T *, long long, long long, long long, int, int, long long, int, int, int, int);
 template <typename T, int R, bool WINBUF, bool ALIGNED> __global__ void k_lookup_win(LookupArgs);
 template <typename T> __global__ void k_lookup_generic(LookupArgs);
-template <typename T, int R, bool NT, int ABL> __global__ void k_lookup_tile(LookupArgs);
+template <typename T, int R, bool NT, int ABL, bool PROJ> __global__ void k_lookup_tile(LookupArgs);
+__global__ void k_proj_pack(const float *, bf16_t *, int, int, int, long long);
 __global__ void k_sample3d(const float *, const float *, float *, int, int, int, int, int, long long, int);
 int fused_lookup(const void *packed_q, const void *packed_t, const float *coords, float *out, void *workspace, int B,
                  long long Nq, int C, const dvc_layout &lay, int radius, int convention, int dtype, int variant,
@@ -93,6 +94,7 @@ static int fill_lookup_args(LookupArgs &A, const dvc_layout &lay, const void *co
     A.ablate = g_lookup_ablate;
     A.order = g_lookup_order;
     A.ldpol = g_lookup_ldpol;
+    A.proj_w = nullptr; A.proj_b = nullptr; A.proj_out = nullptr;
     return DVC_OK;
 }
 
@@ -120,19 +122,19 @@ static void launch_tile_nt(const LookupArgs &A, hipStream_t s) {
     const unsigned threads = 64u * (unsigned)((2 * A.r + 3) / 3);
     if constexpr (std::is_same<T, bf16_t>::value && NT) {
         if (A.r == 4 && A.ablate >= 1 && A.ablate <= 3) {   // diagnostics only
-            if (A.ablate == 1) k_lookup_tile<T, 4, NT, 1><<<blocks, threads, 0, s>>>(A);
-            else if (A.ablate == 2) k_lookup_tile<T, 4, NT, 2><<<blocks, threads, 0, s>>>(A);
-            else k_lookup_tile<T, 4, NT, 3><<<blocks, threads, 0, s>>>(A);
+            if (A.ablate == 1) k_lookup_tile<T, 4, NT, 1, false><<<blocks, threads, 0, s>>>(A);
+            else if (A.ablate == 2) k_lookup_tile<T, 4, NT, 2, false><<<blocks, threads, 0, s>>>(A);
+            else k_lookup_tile<T, 4, NT, 3, false><<<blocks, threads, 0, s>>>(A);
             return;
         }
     }
     switch (A.r) {
-    case 1: k_lookup_tile<T, 1, NT, 0><<<blocks, threads, 0, s>>>(A); break;
-    case 2: k_lookup_tile<T, 2, NT, 0><<<blocks, threads, 0, s>>>(A); break;
-    case 3: k_lookup_tile<T, 3, NT, 0><<<blocks, threads, 0, s>>>(A); break;
-    case 4: k_lookup_tile<T, 4, NT, 0><<<blocks, threads, 0, s>>>(A); break;
-    case 5: k_lookup_tile<T, 5, NT, 0><<<blocks, threads, 0, s>>>(A); break;
-    case 6: k_lookup_tile<T, 6, NT, 0><<<blocks, threads, 0, s>>>(A); break;
+    case 1: k_lookup_tile<T, 1, NT, 0, false><<<blocks, threads, 0, s>>>(A); break;
+    case 2: k_lookup_tile<T, 2, NT, 0, false><<<blocks, threads, 0, s>>>(A); break;
+    case 3: k_lookup_tile<T, 3, NT, 0, false><<<blocks, threads, 0, s>>>(A); break;
+    case 4: k_lookup_tile<T, 4, NT, 0, false><<<blocks, threads, 0, s>>>(A); break;
+    case 5: k_lookup_tile<T, 5, NT, 0, false><<<blocks, threads, 0, s>>>(A); break;
+    case 6: k_lookup_tile<T, 6, NT, 0, false><<<blocks, threads, 0, s>>>(A); break;
     default: break;
     }
 }
@@ -450,6 +452,70 @@ int dvc_corr_lookup(const void *corr, const float *coords, float *out, int B, in
         }
     }
     return DVC_OK;
+}
+
+size_t dvc_proj_packed_bytes(int num_levels, int radius) {
+    if (num_levels < 1 || num_levels > DVC_MAX_LEVELS || radius < 1 || radius > DVC_PROJ_MAX_RADIUS) return 0;
+    const int n = 2 * radius + 1;
+    return (size_t)num_levels * n * ((n + 2) / 3) * DVC_PROJ_COUT * 32 * sizeof(bf16_t);
+}
+
+int dvc_proj_pack(const float *weight, void *packed, int cout, int num_levels, int radius, int convention,
+                  void *stream) {
+    if (!weight || !packed) return fail(DVC_ERR_INVALID, "proj_pack: null pointer");
+    if (cout != DVC_PROJ_COUT) return fail(DVC_ERR_UNSUPPORTED, "proj_pack: %d output channels (convc1 has %d)", cout,
+                                           DVC_PROJ_COUT);
+    if (num_levels < 1 || num_levels > DVC_MAX_LEVELS)
+        return fail(DVC_ERR_INVALID, "proj_pack: num_levels=%d outside [1, %d]", num_levels, DVC_MAX_LEVELS);
+    if (radius < 1 || radius > DVC_PROJ_MAX_RADIUS)
+        return fail(DVC_ERR_UNSUPPORTED, "proj_pack: radius %d outside [1, %d]", radius, DVC_PROJ_MAX_RADIUS);
+    if (convention != DVC_FIXED && convention != DVC_LEGACY)
+        return fail(DVC_ERR_INVALID, "proj_pack: bad convention %d", convention);
+    const long long total = (long long)(dvc_proj_packed_bytes(num_levels, radius) / sizeof(bf16_t));
+    k_proj_pack<<<(unsigned)ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(
+        weight, (bf16_t *)packed, num_levels, radius, convention == DVC_LEGACY, total);
+    return check_launch("proj_pack");
+}
+
+int dvc_corr_lookup_proj(const void *corr, const float *coords, const void *packed_w, const float *bias, float *out,
+                         int B, int64_t Nq, int H, int W, int D, int num_levels, int radius, int convention,
+                         int store_dtype, void *stream) {
+    dvc_layout lay;
+    int rc = dvc_layout_init(H, W, D, num_levels, 1, &lay);
+    if (rc) return rc;
+    if (!corr || !coords || !packed_w || !bias || !out) return fail(DVC_ERR_INVALID, "lookup_proj: null pointer");
+    if (B < 1 || Nq < 1) return fail(DVC_ERR_INVALID, "lookup_proj: B=%d Nq=%lld", B, (long long)Nq);
+    if (radius < 1 || radius > DVC_PROJ_MAX_RADIUS)
+        return fail(DVC_ERR_UNSUPPORTED, "lookup_proj: radius %d outside [1, %d]", radius, DVC_PROJ_MAX_RADIUS);
+    if (convention != DVC_FIXED && convention != DVC_LEGACY)
+        return fail(DVC_ERR_INVALID, "lookup_proj: bad convention %d", convention);
+    if (store_dtype != DVC_BF16 && store_dtype != DVC_F32)
+        return fail(DVC_ERR_INVALID, "lookup_proj: bad dtype %d", store_dtype);
+    LookupArgs A;
+    fill_lookup_args(A, lay, corr, coords, nullptr, B, Nq, radius, convention);
+    for (int l = 0; l < lay.num_levels; ++l)
+        if (A.generic[l] && !A.zero[l])
+            return fail(DVC_ERR_UNSUPPORTED, "lookup_proj: legacy level %d with W != D (%d, %d)", l, lay.W[l],
+                        lay.D[l]);
+    if (!tile_ok(A, store_dtype == DVC_BF16 ? 2 : 4))
+        return fail(DVC_ERR_UNSUPPORTED, "lookup_proj: rows of %lld elements too wide for the tile kernel",
+                    (long long)lay.row_stride);
+    A.proj_w = packed_w; A.proj_b = bias; A.proj_out = out;
+    A.ablate = 0;
+    const unsigned blocks = (unsigned)(B * A.nqb);
+    const unsigned threads = 64u * (unsigned)((2 * radius + 3) / 3 + 1);
+    hipStream_t s = (hipStream_t)stream;
+#define DVC_PROJ_LAUNCH(T)                                                                   \
+    switch (radius) {                                                                        \
+    case 1: k_lookup_tile<T, 1, true, 0, true><<<blocks, threads, 0, s>>>(A); break;        \
+    case 2: k_lookup_tile<T, 2, true, 0, true><<<blocks, threads, 0, s>>>(A); break;        \
+    case 3: k_lookup_tile<T, 3, true, 0, true><<<blocks, threads, 0, s>>>(A); break;        \
+    default: k_lookup_tile<T, 4, true, 0, true><<<blocks, threads, 0, s>>>(A); break;       \
+    }
+    if (store_dtype == DVC_BF16) { DVC_PROJ_LAUNCH(bf16_t) }
+    else { DVC_PROJ_LAUNCH(float) }
+#undef DVC_PROJ_LAUNCH
+    return check_launch("corr_lookup_proj");
 }
 
 size_t dvc_lookup_fused_workspace_bytes(int B, int64_t Nq, int num_levels, int radius) {

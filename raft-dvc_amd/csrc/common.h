@@ -44,6 +44,11 @@ struct LookupArgs {
     int order;                     // tile kernel: 1 = odd tiles walk the levels coarse-to-fine
     int ldpol;                     // tile kernel: cache-policy bits of the plane loads
     long long off[DVC_MAX_LEVELS];
+    // tile kernel with the motion encoder's convc1 fused (PROJ instances only):
+    // packed bf16 weights (dvc_proj_pack), bias[96], out (B, 96, Nq)
+    const void *proj_w;
+    const float *proj_b;
+    float *proj_out;
 };
 
 template <typename T> struct StoreT;

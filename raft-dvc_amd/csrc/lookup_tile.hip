@@ -85,15 +85,40 @@ template <int n> struct ZRun {
     float t;
 };
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// convc1 fusion (PROJ): the motion encoder's first layer, relu(conv1x1(corr, W) + b)
+// with 96 output channels (reference src/core/update.py:219-222, 246), applied to the
+// lookup's L*(2r+1)^3 channels without writing them to HBM.
+//   * the NWAVES lookup waves (producers) write each output row a (their (2r+1) x 3
+//     values per query) as bf16 into a [64 query][NWAVES x 32 k] LDS tile X instead of
+//     storing them; within a wave's 32-k slice, k = 2 (uu NP + i) + {0, 1} holds the
+//     pair (column uu, v = 2i, 2i + 1) and k = 2 NU NP + uu the tail v = n - 1.
+//   * one extra wave (consumer) multiplies X by the row's 96 x (NWAVES x 32) weight
+//     block on v_mfma_f32_16x16x32_bf16 (A = weights, 16 output channels; B = X, 16
+//     queries), accumulating D[96][64] over every row of every level in 96 VGPRs, and
+//     stores relu(D + b) once per tile.  The weights are pre-permuted into that k order
+//     and the MFMA A-operand lane layout (dvc_proj_pack), so any sampler convention is
+//     just a different permutation.
+//   * X is single-buffered: a barrier before the producers overwrite it (the consumer
+//     has read the previous row) plus the row barrier the lookup already has.
+struct ProjCfg {
+    static constexpr int COUT = 96, OT = COUT / 16, KW = 32;
+};
+
 // ABL (diagnostics only, never the product path): 1 = skip output stores, 2 = skip loads.
-template <typename T, int R, bool NT, int ABL>
-__global__ __launch_bounds__(64 * ((2 * R + 3) / 3), 2) void k_lookup_tile(LookupArgs A) {
+template <typename T, int R, bool NT, int ABL, bool PROJ>
+__global__ __launch_bounds__(64 * ((2 * R + 3) / 3 + (PROJ ? 1 : 0)), 2) void k_lookup_tile(LookupArgs A) {
     using C = TileCfg<T, R>;
     constexpr int n = C::n, NW = C::NW, ES = C::ES, CE = C::CE, NP = n / 2;
     constexpr long long n3 = (long long)n * n * n;
     constexpr int NU_LAST = n - C::COLS * (C::NWAVES - 1);   // output columns of the last wave
+    constexpr int XROW = C::NWAVES * ProjCfg::KW * 2 + 16;    // bytes per query row of X (+16: bank spread)
+    static_assert(!PROJ || C::COLS * n <= ProjCfg::KW, "PROJ: one wave's row values must fit a 32-k slice");
     __shared__ __attribute__((aligned(16))) unsigned char smem[C::LDS];
     __shared__ int tab[3][64];   // per query of the tile: ih, cs, za (element units)
+    __shared__ __attribute__((aligned(16))) unsigned char xs[PROJ ? 64 * XROW : 16];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -105,6 +130,68 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3), 2) void k_lookup_tile(Looku
     const long long q = A.q0 + qt + lane;
     const bool active = lane < nvalid;
     const long long Nq = A.Nq;
+    const bool rev = A.order && (blockIdx.x & 1);   // level order of this tile (see the level loop)
+
+    if constexpr (PROJ) {
+        if (wave == C::NWAVES) {   // the convc1 consumer wave
+            constexpr int OT = ProjCfg::OT, NWV = C::NWAVES;
+            const int m16 = lane & 15, h4 = lane >> 4;
+            f32x4 acc[OT][4];   // acc[ot][j][i] = D[o = 16 ot + 4 h4 + i][query 16 j + m16]
+#pragma unroll
+            for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[ot][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            const bf16x8 *wp = reinterpret_cast<const bf16x8 *>(A.proj_w) + lane;
+            for (int li = 0; li < A.nl; ++li) {
+                const int l = A.l0 + (rev ? A.nl - 1 - li : li);
+                if (A.zero[l] || A.generic[l]) continue;   // (the producers skip the same levels)
+                __syncthreads();
+                __syncthreads();   // level preamble: window table
+                __syncthreads();
+                __syncthreads();   // planes 0 and 1 staged
+                for (int a = 0; a < n; ++a) {
+                    // this row's weight block, [wave slice ks][16-channel tile ot][lane] x 8 bf16
+                    const bf16x8 *wr = wp + (long long)(l * n + a) * NWV * OT * 64;
+                    bf16x8 wa[NWV][OT];
+#pragma unroll
+                    for (int ks = 0; ks < NWV; ++ks)
+#pragma unroll
+                        for (int ot = 0; ot < OT; ++ot) wa[ks][ot] = wr[(ks * OT + ot) * 64];
+                    __syncthreads();   // the producers may overwrite X: row a-1 has been read
+                    __syncthreads();   // row a complete in X
+#pragma unroll
+                    for (int ks = 0; ks < NWV; ++ks) {
+                        bf16x8 xb[4];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            xb[j] = *reinterpret_cast<const bf16x8 *>(xs + (16 * j + m16) * XROW + ks * 64 + h4 * 16);
+#pragma unroll
+                        for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+                            for (int j = 0; j < 4; ++j)
+                                acc[ot][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[ks][ot], xb[j], acc[ot][j], 0,
+                                                                                     0, 0);
+                    }
+                }
+            }
+            // relu(D + b) -> out (B, 96, Nq); a wave store covers 16 consecutive queries of 4 channels
+            float *ob = A.proj_out + (long long)b * ProjCfg::COUT * Nq + A.q0 + qt;
+#pragma unroll
+            for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int o = 16 * ot + 4 * h4 + i;
+                    const float bo = A.proj_b[o];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int qq = 16 * j + m16;
+                        const float v = acc[ot][j][i] + bo;
+                        if (qq < nvalid) ob[(long long)o * Nq + qq] = v < 0.f ? 0.f : v;   // relu (NaN kept)
+                    }
+                }
+            return;
+        }
+    }
 
     // zero the LDS once: guards and strip padding are read (with zero weight) and must be finite
     for (int i = tid * 16; i < C::LDS; i += C::THREADS * 16) *reinterpret_cast<u32x4 *>(smem + i) = u32x4{0, 0, 0, 0};
@@ -143,6 +230,7 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3), 2) void k_lookup_tile(Looku
         constexpr int NU = decltype(nu_c)::value;
         float *obase = A.out + ((long long)b * A.Ltot + l) * n3 * Nq;   // wave-uniform
         if (A.zero[l]) {
+            if constexpr (PROJ) return;   // zero outputs add nothing to convc1
             for (int a = 0; a < n; ++a)
 #pragma unroll
                 for (int uu = 0; uu < NU; ++uu) {
@@ -288,6 +376,8 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3), 2) void k_lookup_tile(Looku
             // column by column: once window column k of plane a+1 is lerped, output
             // column k-1 is complete and plane a's column k-1 retires
             ZRun<n> zprev;
+            unsigned xr[NU * NP];   // PROJ: this row's value pairs as bf16x2
+            float xt[NU];           // PROJ: tails (v = n - 1)
 #pragma unroll
             for (int k = 0; k <= NU; ++k) {
                 ZRun<n> zcur;
@@ -304,18 +394,40 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3), 2) void k_lookup_tile(Looku
                         acc = __builtin_elementwise_fma(P10, zp[uu + 1].p[i], acc);
                         acc = __builtin_elementwise_fma(P01, zprev.p[i], acc);
                         acc = __builtin_elementwise_fma(P11, zcur.p[i], acc);
-                        store(rs, 2 * i, acc[0]);
-                        store(rs, 2 * i + 1, acc[1]);
+                        if constexpr (PROJ) {
+                            xr[uu * NP + i] = __builtin_bit_cast(unsigned, __builtin_convertvector(acc, bf16x2));
+                        } else {
+                            store(rs, 2 * i, acc[0]);
+                            store(rs, 2 * i + 1, acc[1]);
+                        }
                     }
                     float acc = p00 * zp[uu].t;
                     acc = __builtin_fmaf(p10, zp[uu + 1].t, acc);
                     acc = __builtin_fmaf(p01, zprev.t, acc);
                     acc = __builtin_fmaf(p11, zcur.t, acc);
-                    store(rs, n - 1, acc);
+                    if constexpr (PROJ) xt[uu] = acc;
+                    else store(rs, n - 1, acc);
                     zp[uu] = zprev;
                 }
                 zprev = zcur;
                 if (k == NU) zp[k] = zcur;
+            }
+            if constexpr (PROJ) {
+                // this wave's 32-k slice of the row: pairs, then the tails, then zeros
+                constexpr int T0 = NU * NP;
+                unsigned xw[ProjCfg::KW / 2];
+#pragma unroll
+                for (int d = 0; d < ProjCfg::KW / 2; ++d) xw[d] = d < T0 ? xr[d < T0 ? d : 0] : 0u;
+#pragma unroll
+                for (int p = 0; 2 * p < NU; ++p) {
+                    const f32x2 t2 = {xt[2 * p], 2 * p + 1 < NU ? xt[2 * p + 1 < NU ? 2 * p + 1 : 0] : 0.0f};
+                    xw[T0 + p] = __builtin_bit_cast(unsigned, __builtin_convertvector(t2, bf16x2));
+                }
+                __syncthreads();   // the consumer has read the previous row of X
+                u32x4 *dst = reinterpret_cast<u32x4 *>(xs + lane * XROW + wave * (ProjCfg::KW * 2));
+#pragma unroll
+                for (int j = 0; j < ProjCfg::KW / 8; ++j)
+                    dst[j] = u32x4{xw[4 * j], xw[4 * j + 1], xw[4 * j + 2], xw[4 * j + 3]};
             }
             if (a + 2 < NW) write_plane(a & 1, a + 2, st[a & 1]);   // plane a+2 into the slot of plane a (read in row a-1)
             __syncthreads();
@@ -324,7 +436,6 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3), 2) void k_lookup_tile(Looku
 
     // odd tiles walk the levels coarse-to-fine, so the two tiles sharing a CU mix the
     // gather-heavy fine levels with the store-heavy coarse ones
-    const bool rev = A.order && (blockIdx.x & 1);
     for (int li = 0; li < A.nl; ++li) {
         const int l = A.l0 + (rev ? A.nl - 1 - li : li);
         if (A.generic[l] && !A.zero[l]) continue;   // legacy level with W != D: k_lookup_generic
@@ -333,15 +444,57 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3), 2) void k_lookup_tile(Looku
     }
 }
 
-#define DVC_TILE_INST(T, R)                                            \
-    template __global__ void k_lookup_tile<T, R, false, 0>(LookupArgs); \
-    template __global__ void k_lookup_tile<T, R, true, 0>(LookupArgs);
+#define DVC_TILE_INST(T, R)                                                   \
+    template __global__ void k_lookup_tile<T, R, false, 0, false>(LookupArgs); \
+    template __global__ void k_lookup_tile<T, R, true, 0, false>(LookupArgs);
 DVC_TILE_INST(float, 1) DVC_TILE_INST(float, 2) DVC_TILE_INST(float, 3)
 DVC_TILE_INST(float, 4) DVC_TILE_INST(float, 5) DVC_TILE_INST(float, 6)
 DVC_TILE_INST(bf16_t, 1) DVC_TILE_INST(bf16_t, 2) DVC_TILE_INST(bf16_t, 3)
 DVC_TILE_INST(bf16_t, 4) DVC_TILE_INST(bf16_t, 5) DVC_TILE_INST(bf16_t, 6)
-template __global__ void k_lookup_tile<bf16_t, 4, true, 1>(LookupArgs);
-template __global__ void k_lookup_tile<bf16_t, 4, true, 2>(LookupArgs);
-template __global__ void k_lookup_tile<bf16_t, 4, true, 3>(LookupArgs);
+template __global__ void k_lookup_tile<bf16_t, 4, true, 1, false>(LookupArgs);
+template __global__ void k_lookup_tile<bf16_t, 4, true, 2, false>(LookupArgs);
+template __global__ void k_lookup_tile<bf16_t, 4, true, 3, false>(LookupArgs);
+// convc1-fused instances (radii whose (2r+1) x 3 row values fit one 32-k slice)
+#define DVC_TILE_PROJ(T, R) template __global__ void k_lookup_tile<T, R, true, 0, true>(LookupArgs);
+DVC_TILE_PROJ(float, 1) DVC_TILE_PROJ(float, 2) DVC_TILE_PROJ(float, 3) DVC_TILE_PROJ(float, 4)
+DVC_TILE_PROJ(bf16_t, 1) DVC_TILE_PROJ(bf16_t, 2) DVC_TILE_PROJ(bf16_t, 3) DVC_TILE_PROJ(bf16_t, 4)
+
+// Weight re-layout for the PROJ instances: W (96, L (2r+1)^3) fp32, the reference's
+// convc1.weight viewed (96, L*(2r+1)^3) (update.py:222) -> bf16 in the consumer's
+// MFMA A-operand order [l][a][wave][ot][lane][8].  Lane (m16, h4) of tile ot holds
+// channel o = 16 ot + m16 at the slice positions k = 8 h4 .. 8 h4 + 7 (k order above);
+// positions past the wave's values are 0.  Reference channel of (l, a, u, v):
+// l (2r+1)^3 + a (2r+1)^2 + u chstep_u + v chstep_v (corr.py:188-208).
+__global__ void k_proj_pack(const float *__restrict__ w, bf16_t *__restrict__ out, int L, int r, int legacy,
+                            long long total) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int n = 2 * r + 1, NP = n / 2, COLS = 3, NWV = (n + COLS - 1) / COLS, OT = ProjCfg::OT;
+    const int e = (int)(idx & 7);
+    long long t = idx >> 3;
+    const int lane = (int)(t & 63); t >>= 6;
+    const int ot = (int)(t % OT); t /= OT;
+    const int w8 = (int)(t % NWV); t /= NWV;
+    const int a = (int)(t % n); t /= n;
+    const int l = (int)t;
+    const int o = 16 * ot + (lane & 15);
+    const int kk = 8 * (lane >> 4) + e;
+    const int NU = w8 < NWV - 1 ? COLS : n - COLS * (NWV - 1);
+    int uu = -1, v = 0;
+    if (kk < 2 * NU * NP) {
+        uu = kk / (2 * NP);
+        v = kk % (2 * NP);
+    } else if (kk < 2 * NU * NP + NU) {
+        uu = kk - 2 * NU * NP;
+        v = n - 1;
+    }
+    float val = 0.0f;
+    if (uu >= 0) {
+        const int u = w8 * COLS + uu;
+        const long long ch = (long long)l * n * n * n + (long long)a * n * n + (legacy ? u + v * n : u * n + v);
+        val = w[(long long)o * L * n * n * n + ch];
+    }
+    out[idx] = f32_to_bf16(val);
+}
 
 }  // namespace dvc

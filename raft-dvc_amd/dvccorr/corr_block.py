@@ -152,6 +152,30 @@ class CorrBlock(_Block):
                          self.legacy_wd_swap, self._dt)
         return out.view(B, -1, H, W, D)
 
+    def lookup_convc1(self, coords: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+        """F.relu(convc1(self(coords))) -> (B, 96, H, W, D) fp32 with convc1 fused into the lookup.
+
+        The motion encoder's first layer (update.py:219-222, 246: Conv3d(L*(2r+1)^3, 96, 1) + ReLU)
+        runs on bf16 MFMA inside the lookup kernel, so the L*(2r+1)^3-channel tensor never reaches
+        HBM (dvc_corr_lookup_proj; tolerance 1e-2 max-normalised, bf16 operands, fp32 accumulation).
+        When gradients are needed, or for radii/conventions the fused kernel does not cover, it is
+        the unfused composition F.relu(F.conv3d(self(coords), weight, bias)) on the GPU."""
+        self._check_coords(coords)
+        B, _, H, W, D = self.shape
+        w = weight.reshape(weight.shape[0], -1)
+        fused_ok = (not (torch.is_grad_enabled() and (weight.requires_grad or bias.requires_grad or
+                                                      self._grad_fmaps is not None))
+                    and 1 <= self.radius <= ops._lib.PROJ_MAX_RADIUS and w.shape[0] == ops._lib.PROJ_COUT
+                    and not (self.legacy_wd_swap and any(lw != ld and min(lh, lw, ld) > 1
+                                                         for lh, lw, ld in self._lay.levels())))
+        if not fused_ok:
+            out = self(coords)
+            return torch.relu(torch.nn.functional.conv3d(out, w.reshape(w.shape[0], -1, 1, 1, 1), bias))
+        packed = ops.proj_pack_cached(weight, self.num_levels, self.radius, self.legacy_wd_swap)
+        out = ops.lookup_proj(self._corr, coords.reshape(B, 3, H * W * D), packed, bias, H, W, D,
+                              self.num_levels, self.radius, self.legacy_wd_swap, self._dt)
+        return out.view(B, -1, H, W, D)
+
 
 class CorrBlockFused(_Block):
     """On-the-fly lookup (no correlation volume), any sampler convention.

@@ -10,6 +10,8 @@ straight to libdvccorr.so (no CPU fallback).  Shapes follow include/dvccorr.h:
     lookup(corr, coords (B, 3, Nq) f32, ...)           -> (B, L*(2r+1)^3, Nq)  f32
     lookup_fused(q, t, coords, ...)                    -> (B, L*(2r+1)^3, Nq)  f32
     sample3d(vol (B, C, Hv, Wv, Dv), pts (B, Nq, 3))   -> (B, C, Nq)           f32
+    proj_pack(convc1 weight (96, L*(2r+1)^3) f32, ...) -> packed bf16 weights
+    lookup_proj(corr, coords, packed_w, bias, ...)     -> (B, 96, Nq)          f32
 """
 from __future__ import annotations
 
@@ -120,6 +122,55 @@ def lookup(corr: torch.Tensor, coords: torch.Tensor, H: int, W: int, D: int, num
     return out
 
 
+def proj_pack(weight: torch.Tensor, num_levels: int, radius: int, legacy: bool) -> torch.Tensor:
+    """convc1.weight (96, L*(2r+1)^3[, 1, 1, 1]) -> the fused kernel's packed bf16 operand (dvc_proj_pack)."""
+    _need_cuda(weight)
+    w = _f32c(weight.detach().reshape(weight.shape[0], -1))
+    nbytes = lib().dvc_proj_packed_bytes(num_levels, radius)
+    if nbytes == 0:
+        raise NotImplementedError(f"proj_pack: L={num_levels} r={radius} not supported (radius 1..4)")
+    if w.shape[1] != num_levels * (2 * radius + 1) ** 3:
+        raise ValueError(f"convc1 weight has {w.shape[1]} input channels; the lookup has "
+                         f"{num_levels * (2 * radius + 1) ** 3}")
+    out = torch.empty((nbytes // 2,), dtype=torch.bfloat16, device=w.device)
+    check(lib().dvc_proj_pack(_ptr(w), _ptr(out), w.shape[0], num_levels, radius,
+                              DVC_LEGACY if legacy else DVC_FIXED, _stream(w)), "proj_pack")
+    return out
+
+
+_PACK_CACHE: dict = {}
+
+
+def proj_pack_cached(weight: torch.Tensor, num_levels: int, radius: int, legacy: bool) -> torch.Tensor:
+    """proj_pack, re-packed only when the weight tensor (storage or in-place version) changes: the packing
+    is once per optimiser step, not once per lookup."""
+    key = (weight.data_ptr(), weight._version, tuple(weight.shape), weight.device, num_levels, radius, bool(legacy))
+    hit = _PACK_CACHE.get(key)
+    if hit is None:
+        if len(_PACK_CACHE) >= 8:
+            _PACK_CACHE.clear()
+        hit = _PACK_CACHE[key] = proj_pack(weight, num_levels, radius, legacy)
+    return hit
+
+
+def lookup_proj(corr: torch.Tensor, coords: torch.Tensor, packed_w: torch.Tensor, bias: torch.Tensor, H: int, W: int,
+                D: int, num_levels: int, radius: int, legacy: bool, store_dtype: int,
+                out: torch.Tensor = None) -> torch.Tensor:
+    """relu(convc1(lookup(coords))) -> (B, 96, Nq) f32, the lookup never written (dvc_corr_lookup_proj)."""
+    _need_cuda(corr, coords, packed_w, bias)
+    B, Nq, _ = corr.shape
+    c = _f32c(coords)
+    b = _f32c(bias)
+    if b.numel() != _lib.PROJ_COUT:
+        raise ValueError(f"convc1 bias must have {_lib.PROJ_COUT} entries; got {b.numel()}")
+    if out is None:
+        out = torch.empty((B, _lib.PROJ_COUT, Nq), dtype=torch.float32, device=corr.device)
+    check(lib().dvc_corr_lookup_proj(_ptr(corr), _ptr(c), _ptr(packed_w), _ptr(b), _ptr(out), B, Nq, H, W, D,
+                                     num_levels, radius, DVC_LEGACY if legacy else DVC_FIXED, store_dtype,
+                                     _stream(corr)), "corr_lookup_proj")
+    return out
+
+
 def lookup_fused(packed_q: torch.Tensor, packed_t: torch.Tensor, coords: torch.Tensor, C: int, H: int, W: int,
                  D: int, num_levels: int, radius: int, legacy: bool, dtype: int, out: torch.Tensor = None,
                  workspace: torch.Tensor = None) -> torch.Tensor:
@@ -175,4 +226,5 @@ def sample3d(vol: torch.Tensor, pts: torch.Tensor, legacy: bool) -> torch.Tensor
 
 
 __all__ = ["pack_queries", "pack_targets", "build", "pool", "lookup", "lookup_fused", "corr_backward", "sample3d",
+           "proj_pack", "proj_pack_cached", "lookup_proj",
            "fused_workspace", "dtype_code", "layout", "_lib"]

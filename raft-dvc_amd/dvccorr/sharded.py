@@ -100,6 +100,14 @@ class HipRows:
         return ops.lookup_fused(self.q, self.t, coords_flat, C, H, W, D, self.L, self.R, self.legacy, self.dt,
                                 workspace=self.ws)
 
+    def lookup_convc1(self, coords_flat: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+        """relu(convc1(lookup)) of this rank's rows, convc1 fused into the lookup (materialised only)."""
+        C, H, W, D = self.dims
+        if self.impl != "materialised":
+            raise NotImplementedError("convc1 fusion is implemented for the materialised pyramid")
+        packed = ops.proj_pack_cached(weight, self.L, self.R, self.legacy)
+        return ops.lookup_proj(self.corr, coords_flat, packed, bias, H, W, D, self.L, self.R, self.legacy, self.dt)
+
 
 class ShardedCorrBlock:
     """CorrBlock over this rank's H-slab of query voxels (fmap1 / coords slabs, full fmap2 gathered).
@@ -146,6 +154,18 @@ class ShardedCorrBlock:
         if tuple(coords_slab.shape) != (B, 3, Hs, W, D):
             raise ValueError(f"coords slab must be {(B, 3, Hs, W, D)}; got {tuple(coords_slab.shape)}")
         out = self.rows.lookup(coords_slab.reshape(B, 3, Hs * W * D)).view(B, -1, Hs, W, D)
+        if self.gather_output:
+            out = gather_slabs(out, self.H, self.group)
+        return out
+
+    def lookup_convc1(self, coords_slab: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+        """relu(convc1(self(coords_slab))) -> (B, 96, h1-h0, W, D) (or the full H with gather_output): the
+        motion encoder's first layer (update.py:222, 246) fused into the lookup; the gathered output is
+        96 channels instead of L*(2r+1)^3."""
+        B, C, Hs, W, D = self.shape
+        if tuple(coords_slab.shape) != (B, 3, Hs, W, D):
+            raise ValueError(f"coords slab must be {(B, 3, Hs, W, D)}; got {tuple(coords_slab.shape)}")
+        out = self.rows.lookup_convc1(coords_slab.reshape(B, 3, Hs * W * D), weight, bias).view(B, -1, Hs, W, D)
         if self.gather_output:
             out = gather_slabs(out, self.H, self.group)
         return out

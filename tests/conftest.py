@@ -72,3 +72,19 @@ def oracle_grads(f1, f2, coords, G, L, r, legacy):
     out = torch_cpu.corr_lookup(t1, t2, torch.from_numpy(np.ascontiguousarray(coords)), L, r, legacy)
     (out * torch.from_numpy(np.ascontiguousarray(G))).sum().backward()
     return t1.grad.numpy(), t2.grad.numpy()
+
+
+def proj_inputs(g):
+    """Regenerate a proj_* fixture's inputs (tests/golden/gen_proj_golden.py): fmaps, coords, convc1 weight
+    (96, L (2r+1)^3) and bias, L, r, legacy."""
+    import prng
+    B, C, H, W, D, L, r = (int(v) for v in g["shape"])
+    seed = int(g["seed"][0])
+    f1 = prng.normal(seed, (B, C, H, W, D))
+    f2 = prng.normal(seed + 1, (B, C, H, W, D))
+    coords = prng.flow_coords(seed + 2, B, H, W, D, float(g["max_flow"][0]))
+    K = L * (2 * r + 1) ** 3
+    bound = 1.0 / np.sqrt(K)
+    w = prng.uniform(seed + 3, (96, K), -bound, bound)
+    b = prng.uniform(seed + 4, (96,), -bound, bound)
+    return f1, f2, coords, w, b, L, r, bool(g["legacy"][0])

@@ -133,3 +133,17 @@ def test_plumbing_fixture_consistent():
     for it in (0, 5, 11):
         got = orc.corr_lookup(g["fmap1"], g["fmap2"], g["coords"][it], 4, 4, False, rows=g["rows"])
         assert orc.rel_err(got, g["out_rows"][it]) < 2e-6
+
+
+PROJ_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "proj_*.npz")))
+
+
+@pytest.mark.parametrize("case", PROJ_CASES)
+def test_convc1_oracle_matches_reference(case):
+    """oracle lookup + motion_convc1 against the reference's CorrBlock + MotionEncoder.convc1 + ReLU
+    (tests/golden/gen_proj_golden.py): pins the channel order of the fused projection."""
+    from conftest import proj_inputs
+    g = load_golden(case + ".npz")
+    f1, f2, coords, w, b, L, r, legacy = proj_inputs(g)
+    ref = orc.motion_convc1(orc.corr_lookup(f1, f2, coords, L, r, legacy), w, b)
+    assert orc.rel_err(ref, g["out"]) < 1e-5
