@@ -141,6 +141,7 @@ def main():
             tdist.init_process_group(args.dist_backend)
     import dvccorr
     from dvccorr import ops
+    from dvccorr import _lib
     from dvccorr.sharded import LOCAL, ShardedCorrBlock, slab_bounds
 
     S, C, L, R = args.size, args.channels, args.levels, args.radius
@@ -266,6 +267,33 @@ def main():
     build_info = {"avg_ms": round(bd_avg, 4), "GB/s": round(bd_bytes / (bd_avg * 1e-3) / 1e9, 1) if bd_avg else None,
                   "TFLOP/s": round(bd_flops / (bd_avg * 1e-3) / 1e12, 1) if bd_avg and bd_flops else None}
 
+    # per-iteration tail (raft_dvc.py:482-485), outside the timed region:
+    # coords1 += delta_flow; flow_up = upflow_3d(coords1 - coords0) to the input size, one k_upflow pass
+    tail = None
+    with torch.no_grad():
+        T = args.encoder * S
+        c1 = coords_slab[0][:, :, :].reshape(B, 3, -1, S, S)
+        dfl = (coords_slab[-1] - coords_slab[0]).reshape(c1.shape)
+        h_lo = c1.shape[2]
+        for _ in range(3):
+            dvccorr.flow_step(c1, dfl, (h_lo * args.encoder, T, T))
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        outs = [(torch.empty_like(c1), torch.empty((B, 3, h_lo * args.encoder, T, T), device=dev))
+                for _ in range(2)]
+        a.record(stream)
+        for k in range(20):   # back-to-back on the stream (C ABI direct: no per-call allocation)
+            n_, u_ = outs[k % 2]
+            _lib.check(_lib.lib().dvc_flow_step(c1.data_ptr(), dfl.data_ptr(), n_.data_ptr(), u_.data_ptr(), B,
+                                                h_lo, S, S, h_lo * args.encoder, T, T, stream.cuda_stream))
+        b.record(stream)
+        torch.cuda.synchronize()
+        tail_ms = a.elapsed_time(b) / 20
+        lo_b = 3 * 4 * c1[0, 0].numel() * B
+        tail_bytes = 3 * lo_b + lo_b * args.encoder ** 3      # read coords1 + delta, write coords1; write flow_up
+        tail = {"kernel": "k_upflow<DELTA,SUBGRID> (dvc_flow_step)", "avg_ms": round(tail_ms, 4),
+                "algorithmic_bytes": tail_bytes,
+                "GB/s": round(tail_bytes / (tail_ms * 1e-3) / 1e9, 1)}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, f1, f2, coords_list)
@@ -289,6 +317,7 @@ def main():
             "roofline": roof,
             "build": build_info,
             "lookup_avg_ms": round(lk_avg, 4),
+            "flow_step": tail,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

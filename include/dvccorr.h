@@ -25,6 +25,9 @@
  *   dvc_sample3d           -- bilinear_sampler_3d                             src/core/corr.py:17-68
  *   dvc_proj_pack,         -- CorrBlock.__call__ followed by the motion       src/core/corr.py:169-208 +
  *   dvc_corr_lookup_proj      encoder's F.relu(self.convc1(corr))            src/core/update.py:219-222, 246
+ *   dvc_coords_grid        -- coords_grid_3d                                 src/core/corr.py:71-99
+ *   dvc_upflow             -- upflow_3d(flow, target_shape)                  src/core/corr.py:211-253
+ *   dvc_flow_step          -- coords1 + delta_flow; upflow_3d(coords1 - coords0)  src/core/raft_dvc.py:482-485
  *
  * Layouts (row-major, element counts):
  *   fmap           (B, C, H, W, D) float32, channels-first, contiguous   (reference layout)
@@ -164,6 +167,21 @@ int dvc_corr_lookup_proj(const void *corr, const float *coords, const void *pack
 /* bilinear_sampler_3d: vol (B, C, Hv, Wv, Dv), pts (B, Nq, 3) in (h, w, d) -> out (B, C, Nq). */
 int dvc_sample3d(const float *vol, const float *pts, float *out, int B, int C, int Hv, int Wv, int Dv, int64_t Nq,
                  int convention, void *stream);
+
+/* Per-iteration flow bookkeeping of RAFTDVC.forward, float32:
+ *   dvc_coords_grid  coords (B, 3, H, W, D) = identity grid          src/core/corr.py:71-99
+ *   dvc_upflow       flow_up (B, C, H, W, D) = upflow_3d(flow (B, C, h, w, d),
+ *                    target_shape=(H, W, D)); C >= 3, channels 0..2 scaled by H/h, W/w, D/d
+ *                                                                     src/core/corr.py:211-253
+ *   dvc_flow_step    coords1_out = coords1 + delta_flow (delta_flow nullable: + 0) and
+ *                    flow_up = upflow_3d(coords1_out - coords0, (H, W, D)), coords0 the
+ *                    identity grid, in one pass                      src/core/raft_dvc.py:482-485
+ *                    (coords1_out nullable; outputs must not alias inputs). */
+int dvc_coords_grid(float *coords, int B, int H, int W, int D, void *stream);
+int dvc_upflow(const float *flow, float *flow_up, int B, int C, int h, int w, int d, int H, int W, int D,
+               void *stream);
+int dvc_flow_step(const float *coords1, const float *delta_flow, float *coords1_out, float *flow_up, int B, int h,
+                  int w, int d, int H, int W, int D, void *stream);
 
 /* Kernel-variant knob for A/B timing (process-wide, not thread-safe):
  *   "lookup_variant" 0 = unaligned 16-byte run loads, 1 = aligned chunks + v_perm shifter;

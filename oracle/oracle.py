@@ -158,6 +158,64 @@ def sample(vol, pts, legacy: bool = False) -> np.ndarray:
     return out
 
 
+def coords_grid_3d(B: int, H: int, W: int, D: int) -> np.ndarray:
+    """Identity grid (B, 3, H, W, D) float32, channel c = index along axis c (corr.py:91-97)."""
+    g = np.stack(np.meshgrid(np.arange(H), np.arange(W), np.arange(D), indexing="ij"), 0).astype(np.float32)
+    return np.ascontiguousarray(np.broadcast_to(g[None], (B, 3, H, W, D)))
+
+
+def _axis_weights(n_in: int, n_out: int):
+    """ATen CPU linear-upsample indices/weights, align_corners=True, in float32
+    (area_pixel_compute_scale + compute_source_index_and_lambda), the arithmetic
+    behind F.interpolate(mode='trilinear', align_corners=True) at corr.py:234-239."""
+    ratio = np.float32(n_in - 1) / np.float32(n_out - 1) if n_out > 1 else np.float32(0.0)
+    src = np.float32(ratio) * np.arange(n_out, dtype=np.float32)
+    i0 = src.astype(np.int64)
+    i1 = i0 + (i0 < n_in - 1)
+    l1 = np.clip(src - i0.astype(np.float32), np.float32(0), np.float32(1)).astype(np.float32)
+    return i0, i1, (np.float32(1) - l1).astype(np.float32), l1
+
+
+def upflow_3d(flow, target_shape) -> np.ndarray:
+    """upflow_3d (src/core/corr.py:211-253) restated in float32 numpy: trilinear,
+    align_corners=True, nested h-outer (ATen's Interpolate<n>), then channel c < 3
+    times float32(target/source) along axis c (corr.py:242-251)."""
+    f = _f32(flow)
+    B, C, h, w, d = f.shape
+    H, W, D = target_shape
+    yi0, yi1, yl0, yl1 = _axis_weights(h, H)
+    xi0, xi1, xl0, xl1 = _axis_weights(w, W)
+    zi0, zi1, zl0, zl1 = _axis_weights(d, D)
+
+    def along_z(a):           # (B, C, h', w', d) -> (B, C, h', w', D)
+        return a[..., zi0] * zl0 + a[..., zi1] * zl1
+
+    def along_x(a0, a1):
+        return a0 * xl0[:, None] + a1 * xl1[:, None]
+
+    def plane(yi):             # (B, C, W, D) for source rows yi
+        a = f[:, :, yi]        # (B, C, H, w, d)
+        zx0 = along_z(a[:, :, :, xi0])
+        zx1 = along_z(a[:, :, :, xi1])
+        return along_x(zx0, zx1)
+
+    out = plane(yi0) * yl0[:, None, None] + plane(yi1) * yl1[:, None, None]
+    scale = [np.float32(H / h), np.float32(W / w), np.float32(D / d)]
+    for c in range(min(C, 3)):
+        out[:, c] *= scale[c]
+    return out.astype(np.float32)
+
+
+def flow_step(coords1, delta_flow, target_shape):
+    """raft_dvc.py:482-485: coords1 + delta_flow, and upflow_3d(coords1 - coords0)."""
+    c1 = _f32(coords1)
+    if delta_flow is not None:
+        c1 = (c1 + _f32(delta_flow)).astype(np.float32)
+    B, _, h, w, d = c1.shape
+    flow = (c1 - coords_grid_3d(B, h, w, d)).astype(np.float32)
+    return c1, upflow_3d(flow, target_shape)
+
+
 def rel_err(out, ref) -> float:
     """max|out - ref| / max|ref| -- the tolerance metric of SURVEY.md 8(c)."""
     out = np.asarray(out, np.float64)

@@ -42,6 +42,10 @@ int corr_backward(const void *packed_q, const void *packed_t, const float *coord
                   const dvc_layout &lay, int radius, int convention, int dtype, hipStream_t s, char *err,
                   size_t errlen);
 size_t backward_workspace_bytes(int B, long long Nq, const dvc_layout &lay, int radius);
+__global__ void k_coords_grid(float *, long long, int, int, int);
+template <bool DELTA, bool SUBGRID, int VEC>
+__global__ void k_upflow(const float *, const float *, float *, float *, long long, int, int, int, int, int, int, int,
+                         float, float, float, float, float, float);
 }  // namespace dvc
 
 using namespace dvc;
@@ -572,6 +576,69 @@ int dvc_sample3d(const float *vol, const float *pts, float *out, int B, int C, i
     k_sample3d<<<(unsigned)ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(vol, pts, out, B, C, Hv, Wv, Dv, Nq,
                                                                           convention == DVC_LEGACY);
     return check_launch("sample3d");
+}
+
+int dvc_coords_grid(float *coords, int B, int H, int W, int D, void *stream) {
+    if (!coords) return fail(DVC_ERR_INVALID, "coords_grid: null pointer");
+    if (B < 1 || H < 1 || W < 1 || D < 1) return fail(DVC_ERR_INVALID, "coords_grid: bad shape");
+    const long long total = (long long)B * 3 * H * W * D;
+    const unsigned blocks = (unsigned)std::min<long long>(ceil_div(total, 256), 65536);
+    k_coords_grid<<<blocks, 256, 0, (hipStream_t)stream>>>(coords, B, H, W, D);
+    return check_launch("coords_grid");
+}
+
+// ATen's align_corners=True source ratio (float), 0 for a size-1 output.
+static float upflow_ratio(int in, int out) { return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.0f; }
+
+static bool overlaps(const void *a, size_t na, const void *b, size_t nb) {
+    const char *pa = (const char *)a, *pb = (const char *)b;
+    return a && b && pa < pb + nb && pb < pa + na;
+}
+
+static int launch_upflow(const float *lo, const float *delta, float *lo_out, float *up, int B, int C, int h, int w,
+                         int d, int H, int W, int D, bool subgrid, void *stream, const char *what) {
+    if (!lo || !up) return fail(DVC_ERR_INVALID, "%s: null pointer", what);
+    if (B < 1 || C < 3 || h < 1 || w < 1 || d < 1 || H < 1 || W < 1 || D < 1)
+        return fail(DVC_ERR_INVALID, "%s: bad shape B=%d C=%d (%d,%d,%d)->(%d,%d,%d) (C must be >= 3, corr.py:249-251)",
+                    what, B, C, h, w, d, H, W, D);
+    const size_t lo_bytes = (size_t)B * C * h * w * d * sizeof(float);
+    const size_t up_bytes = (size_t)B * C * H * W * D * sizeof(float);
+    if (overlaps(up, up_bytes, lo, lo_bytes) || overlaps(up, up_bytes, delta, lo_bytes) ||
+        overlaps(lo_out, lo_bytes, lo, lo_bytes) || overlaps(lo_out, lo_bytes, delta, lo_bytes) ||
+        overlaps(lo_out, lo_bytes, up, up_bytes))
+        return fail(DVC_ERR_INVALID, "%s: output buffers must not alias the inputs", what);
+    if ((long long)W * D >= (1LL << 31) || H > 65535 || (long long)B * C > 65535)
+        return fail(DVC_ERR_UNSUPPORTED, "%s: output (%d,%d,%d) x B*C=%lld exceeds the launch grid", what, H, W, D,
+                    (long long)B * C);
+    const int vec = (D % 4 == 0) ? 4 : 1;   // 16-byte stores when every plane row is 16-byte aligned
+    const dim3 blocks((unsigned)ceil_div((long long)W * D, 256LL * vec), (unsigned)ceil_div(H, 4), (unsigned)(B * C));
+    const float rh = upflow_ratio(h, H), rw = upflow_ratio(w, W), rd = upflow_ratio(d, D);
+    // flow_up[:, c] *= target/in (a Python float, applied in float32), corr.py:242-251
+    const float sh = (float)((double)H / h), sw = (float)((double)W / w), sd = (float)((double)D / d);
+    hipStream_t s = (hipStream_t)stream;
+#define DVC_UPFLOW(DL, SG, V)                                                                                      \
+    k_upflow<DL, SG, V><<<blocks, 256, 0, s>>>(lo, DL ? delta : nullptr, SG ? lo_out : nullptr, up, B, C, h, w, d, \
+                                               H, W, D, rh, rw, rd, sh, sw, sd)
+    if (!subgrid) {
+        if (vec == 4) DVC_UPFLOW(false, false, 4); else DVC_UPFLOW(false, false, 1);
+    } else if (delta) {
+        if (vec == 4) DVC_UPFLOW(true, true, 4); else DVC_UPFLOW(true, true, 1);
+    } else {
+        if (vec == 4) DVC_UPFLOW(false, true, 4); else DVC_UPFLOW(false, true, 1);
+    }
+#undef DVC_UPFLOW
+    return check_launch(what);
+}
+
+int dvc_upflow(const float *flow, float *flow_up, int B, int C, int h, int w, int d, int H, int W, int D,
+               void *stream) {
+    return launch_upflow(flow, nullptr, nullptr, flow_up, B, C, h, w, d, H, W, D, false, stream, "upflow");
+}
+
+int dvc_flow_step(const float *coords1, const float *delta_flow, float *coords1_out, float *flow_up, int B, int h,
+                  int w, int d, int H, int W, int D, void *stream) {
+    return launch_upflow(coords1, delta_flow, coords1_out, flow_up, B, 3, h, w, d, H, W, D, true, stream,
+                         "flow_step");
 }
 
 }  // extern "C"

@@ -9,9 +9,9 @@ from __future__ import annotations
 
 from ._lib import LIB_PATH, DvcError, layout
 from .corr_block import (CorrBlock, CorrBlockFused, CorrBlockOnTheFly, bilinear_sampler_3d, coords_grid_3d,
-                         make_corr_block, resolve_precision)
+                         flow_step, make_corr_block, resolve_precision, upflow_3d)
 
 __version__ = "0.1.0"
 
 __all__ = ["CorrBlock", "CorrBlockFused", "CorrBlockOnTheFly", "bilinear_sampler_3d", "coords_grid_3d",
-           "make_corr_block", "resolve_precision", "layout", "DvcError", "LIB_PATH"]
+           "upflow_3d", "flow_step", "make_corr_block", "resolve_precision", "layout", "DvcError", "LIB_PATH"]

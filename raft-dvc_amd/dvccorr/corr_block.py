@@ -8,6 +8,8 @@ Same constructor and call contract as the reference (zachtong/RAFT-DVC):
                       use_checkpoint)                                         src/core/corr_otf.py:51-94
     bilinear_sampler_3d(vol, coords, legacy_wd_swap=False)                    src/core/corr.py:17-68
     coords_grid_3d(batch, ht, wd, dp, device)                                 src/core/corr.py:71-99
+    upflow_3d(flow, target_shape=None, scale_factor=8)                        src/core/corr.py:211-253
+    flow_step(coords1, delta_flow, target_shape) -> (coords1', flow_up)       src/core/raft_dvc.py:482-485
 
 so RAFTDVC.forward (raft_dvc.py:369-450), the trainer and the evaluation
 scripts can use them unchanged.  The work is done by libdvccorr.so (gfx950
@@ -39,7 +41,7 @@ from . import ops
 from ._lib import layout
 
 __all__ = ["CorrBlock", "CorrBlockFused", "CorrBlockOnTheFly", "bilinear_sampler_3d", "coords_grid_3d",
-           "make_corr_block", "resolve_precision"]
+           "upflow_3d", "flow_step", "make_corr_block", "resolve_precision"]
 
 
 def resolve_precision(fmap: torch.Tensor, precision: Optional[str]) -> str:
@@ -239,10 +241,37 @@ def bilinear_sampler_3d(vol: torch.Tensor, coords: torch.Tensor, legacy_wd_swap:
 
 
 def coords_grid_3d(batch: int, ht: int, wd: int, dp: int, device: torch.device) -> torch.Tensor:
-    """Identity grid (B, 3, H, W, D), channel c = index along axis c (h, w, d)."""
+    """Identity grid (B, 3, H, W, D), channel c = index along axis c (h, w, d).
+
+    On the GPU this is k_coords_grid (dvc_coords_grid); a CPU device (input
+    generation in tests and bench) builds the same integers with torch.
+    """
+    if torch.device(device).type == "cuda":
+        return ops.coords_grid(batch, ht, wd, dp, device)
     axes = [torch.arange(s, device=device, dtype=torch.float32) for s in (ht, wd, dp)]
     grid = torch.stack(torch.meshgrid(*axes, indexing="ij"), dim=0)
     return grid.unsqueeze(0).expand(batch, 3, ht, wd, dp).contiguous()
+
+
+def upflow_3d(flow: torch.Tensor, target_shape=None, scale_factor: int = 8) -> torch.Tensor:
+    """upflow_3d (src/core/corr.py:211-253): trilinear, align_corners=True, channels 0..2
+    scaled by target/source size per axis -- one k_upflow pass (dvc_upflow)."""
+    if target_shape is None:
+        _, _, h, w, d = flow.shape
+        target_shape = (h * scale_factor, w * scale_factor, d * scale_factor)
+    return ops.upflow(flow, target_shape)
+
+
+def flow_step(coords1: torch.Tensor, delta_flow: Optional[torch.Tensor], target_shape):
+    """RAFTDVC.forward's per-iteration tail (raft_dvc.py:482-485) in one k_upflow pass:
+
+        coords1 = coords1 + delta_flow
+        flow_up = upflow_3d(coords1 - coords0, target_shape=target_shape)
+
+    coords0 is the identity grid (raft_dvc.py:293), formed in registers.  Returns
+    (coords1, flow_up); the input coords1 is not modified.
+    """
+    return ops.flow_step(coords1, delta_flow, target_shape)
 
 
 def make_corr_block(impl: str, fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int = 4, radius: int = 4,

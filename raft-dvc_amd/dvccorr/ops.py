@@ -12,6 +12,9 @@ straight to libdvccorr.so (no CPU fallback).  Shapes follow include/dvccorr.h:
     sample3d(vol (B, C, Hv, Wv, Dv), pts (B, Nq, 3))   -> (B, C, Nq)           f32
     proj_pack(convc1 weight (96, L*(2r+1)^3) f32, ...) -> packed bf16 weights
     lookup_proj(corr, coords, packed_w, bias, ...)     -> (B, 96, Nq)          f32
+    coords_grid(B, H, W, D, device)                    -> (B, 3, H, W, D)      f32
+    upflow(flow (B, C, h, w, d), (H, W, D))            -> (B, C, H, W, D)      f32
+    flow_step(coords1, delta (B, 3, h, w, d), (H,W,D)) -> coords1 + delta, upflow(coords1 + delta - coords0)
 """
 from __future__ import annotations
 
@@ -225,6 +228,47 @@ def sample3d(vol: torch.Tensor, pts: torch.Tensor, legacy: bool) -> torch.Tensor
     return out
 
 
+def coords_grid(B: int, H: int, W: int, D: int, device) -> torch.Tensor:
+    out = torch.empty((B, 3, H, W, D), dtype=torch.float32, device=device)
+    _need_cuda(out)
+    check(lib().dvc_coords_grid(_ptr(out), B, H, W, D, _stream(out)), "coords_grid")
+    return out
+
+
+def upflow(flow: torch.Tensor, target_shape) -> torch.Tensor:
+    _need_cuda(flow)
+    f = _f32c(flow)
+    if f.dim() != 5:
+        raise ValueError(f"upflow_3d expects (B, C, H, W, D), got {tuple(f.shape)}")
+    B, C, h, w, d = f.shape
+    H, W, D = (int(v) for v in target_shape)
+    out = torch.empty((B, C, H, W, D), dtype=torch.float32, device=f.device)
+    check(lib().dvc_upflow(_ptr(f), _ptr(out), B, C, h, w, d, H, W, D, _stream(f)), "upflow")
+    return out
+
+
+def flow_step(coords1: torch.Tensor, delta_flow, target_shape):
+    """(coords1 + delta_flow, upflow_3d(coords1 + delta_flow - coords0, target_shape)) in one pass."""
+    _need_cuda(coords1)
+    c = _f32c(coords1)
+    if c.dim() != 5 or c.shape[1] != 3:
+        raise ValueError(f"coords1 must be (B, 3, H, W, D), got {tuple(c.shape)}")
+    B, _, h, w, d = c.shape
+    H, W, D = (int(v) for v in target_shape)
+    dl = None
+    if delta_flow is not None:
+        _need_cuda(delta_flow)
+        dl = _f32c(delta_flow)
+        if dl.shape != c.shape:
+            raise ValueError(f"delta_flow {tuple(dl.shape)} does not match coords1 {tuple(c.shape)}")
+    new = torch.empty_like(c)
+    up = torch.empty((B, 3, H, W, D), dtype=torch.float32, device=c.device)
+    check(lib().dvc_flow_step(_ptr(c), None if dl is None else _ptr(dl), _ptr(new), _ptr(up), B, h, w, d, H, W, D,
+                              _stream(c)), "flow_step")
+    return new, up
+
+
 __all__ = ["pack_queries", "pack_targets", "build", "pool", "lookup", "lookup_fused", "corr_backward", "sample3d",
            "proj_pack", "proj_pack_cached", "lookup_proj",
+           "coords_grid", "upflow", "flow_step",
            "fused_workspace", "dtype_code", "layout", "_lib"]
