@@ -45,7 +45,7 @@ size_t backward_workspace_bytes(int B, long long Nq, const dvc_layout &lay, int 
 __global__ void k_coords_grid(float *, long long, int, int, int);
 template <bool DELTA, bool SUBGRID, int VEC>
 __global__ void k_upflow(const float *, const float *, float *, float *, long long, int, int, int, int, int, int, int,
-                         float, float, float, float, float, float);
+                         float, float, float, float, float, float, int, int, int);
 }  // namespace dvc
 
 using namespace dvc;
@@ -62,6 +62,8 @@ static int g_build_variant = 1;      // 1 = two-barrier bf16-store kernel (k_bui
 // fused lookup kernel where the MFMA path applies: 2 = k_fused_box 2x2x16, 8 waves (default),
 // 3 = k_fused_box 4x4x4 cubes, 8 waves, 4 = k_fused_box 2x2x16, 4 waves, 1 = k_fused_tile, 0 = two-stage VALU
 static int g_fused_variant = 2;
+static int g_upflow_rows = 8;        // output rows per k_upflow work item
+static int g_upflow_wgs = 1024;      // k_upflow grid (workgroups striding over the items)
 static int g_fused_ablate = 0;       // diagnostics only: 1 = skip output stores, 2 = skip window dots (cube kernel)
 
 static int fail(int code, const char *fmt, ...) {
@@ -200,6 +202,16 @@ int dvc_set_tuning(const char *key, int value) {
     if (!strcmp(key, "build_variant")) {
         if (value < 0 || value > 1) return fail(DVC_ERR_INVALID, "set_tuning: build_variant %d", value);
         g_build_variant = value;
+        return DVC_OK;
+    }
+    if (!strcmp(key, "upflow_rows")) {
+        if (value < 1 || value > 64) return fail(DVC_ERR_INVALID, "set_tuning: upflow_rows %d outside [1, 64]", value);
+        g_upflow_rows = value;
+        return DVC_OK;
+    }
+    if (!strcmp(key, "upflow_wgs")) {
+        if (value < 1) return fail(DVC_ERR_INVALID, "set_tuning: upflow_wgs %d < 1", value);
+        g_upflow_wgs = value;
         return DVC_OK;
     }
     if (!strcmp(key, "fused_ablate")) {
@@ -607,18 +619,20 @@ static int launch_upflow(const float *lo, const float *delta, float *lo_out, flo
         overlaps(lo_out, lo_bytes, lo, lo_bytes) || overlaps(lo_out, lo_bytes, delta, lo_bytes) ||
         overlaps(lo_out, lo_bytes, up, up_bytes))
         return fail(DVC_ERR_INVALID, "%s: output buffers must not alias the inputs", what);
-    if ((long long)W * D >= (1LL << 31) || H > 65535 || (long long)B * C > 65535)
-        return fail(DVC_ERR_UNSUPPORTED, "%s: output (%d,%d,%d) x B*C=%lld exceeds the launch grid", what, H, W, D,
+    if ((long long)W * D >= (1LL << 31) || (long long)B * C >= (1LL << 31))
+        return fail(DVC_ERR_UNSUPPORTED, "%s: output plane (%d,%d) x B*C=%lld exceeds 32-bit item indices", what, W, D,
                     (long long)B * C);
     const int vec = (D % 4 == 0) ? 4 : 1;   // 16-byte stores when every plane row is 16-byte aligned
-    const dim3 blocks((unsigned)ceil_div((long long)W * D, 256LL * vec), (unsigned)ceil_div(H, 4), (unsigned)(B * C));
+    const int nx = (int)ceil_div((long long)W * D, 256LL * vec), rows = std::min(g_upflow_rows, H);
+    const int ny = (int)ceil_div(H, rows);
+    const unsigned blocks = (unsigned)std::min<long long>((long long)nx * ny * B * C, g_upflow_wgs);
     const float rh = upflow_ratio(h, H), rw = upflow_ratio(w, W), rd = upflow_ratio(d, D);
     // flow_up[:, c] *= target/in (a Python float, applied in float32), corr.py:242-251
     const float sh = (float)((double)H / h), sw = (float)((double)W / w), sd = (float)((double)D / d);
     hipStream_t s = (hipStream_t)stream;
 #define DVC_UPFLOW(DL, SG, V)                                                                                      \
     k_upflow<DL, SG, V><<<blocks, 256, 0, s>>>(lo, DL ? delta : nullptr, SG ? lo_out : nullptr, up, B, C, h, w, d, \
-                                               H, W, D, rh, rw, rd, sh, sw, sd)
+                                               H, W, D, rh, rw, rd, sh, sw, sd, nx, ny, rows)
     if (!subgrid) {
         if (vec == 4) DVC_UPFLOW(false, false, 4); else DVC_UPFLOW(false, false, 1);
     } else if (delta) {

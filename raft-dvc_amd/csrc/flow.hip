@@ -86,30 +86,51 @@ __device__ __forceinline__ float upflow_value(const float *__restrict__ lo, cons
     return __builtin_fmaf(ay.l1, acc_y[1], ay.l0 * acc_y[0]) * scale;
 }
 
-constexpr int kUpRows = 4;   // output rows (oy) per workgroup
+constexpr int kZRun = 5;     // low-res z values covering 4 consecutive outputs when upsampling (ratio <= 1)
+
+__device__ __forceinline__ float pick5(const float (&v)[kZRun], int j) {
+    return j == 0 ? v[0] : (j == 1 ? v[1] : (j == 2 ? v[2] : (j == 3 ? v[3] : v[4])));
+}
+
+// Row cache of the z-run path: T[k] = the x- and z-interpolated value of low-res row y
+// for this lane's 4 outputs -- exactly acc_y[ty] of upflow_value, so the rounding is
+// identical; each low-res (y, x) row is gathered once (kZRun loads) per lane and row.
+template <bool DELTA, bool SUBGRID>
+__device__ __forceinline__ void upflow_row(const float *__restrict__ lo, const float *__restrict__ delta,
+                                           long long base, int c, int y, int w, int d, int zlo, const AxisW &ax,
+                                           const AxisW (&az)[4], float (&T)[4]) {
+    float acc_x[2][4];
+#pragma unroll
+    for (int tx = 0; tx < 2; ++tx) {
+        const int x = tx ? ax.i1 : ax.i0;
+        const long long row = base + ((long long)y * w + x) * d;
+        float v[kZRun];
+#pragma unroll
+        for (int j = 0; j < kZRun; ++j) {
+            const int zz = min(zlo + j, d - 1);   // clamped entries are never picked
+            v[j] = lo_value<DELTA, SUBGRID>(lo, delta, row + zz, c, y, x, zz);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            acc_x[tx][k] = __builtin_fmaf(az[k].l1, pick5(v, az[k].i1 - zlo), az[k].l0 * pick5(v, az[k].i0 - zlo));
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) T[k] = __builtin_fmaf(ax.l1, acc_x[1][k], ax.l0 * acc_x[0][k]);
+}
 
 // up (B, C, H, W, D) = upflow_3d(lo (+ delta) (- coords0)); channels 0..2 scaled.
 // lo_out (nullable) receives lo + delta at low resolution (the updated coords1).
 // Grid: x = chunks of one output (W, D) plane (256 lanes x VEC consecutive z),
-// y = groups of kUpRows output rows, z = b*C + c; the h-axis weights and the channel
+// y = groups of `rows` output rows, z = b*C + c; the h-axis weights and the channel
 // are uniform per workgroup, lanes store VEC consecutive z (16-byte stores for VEC 4,
-// D % 4 == 0), and each workgroup covers kUpRows rows so the grid stays ~1-2 K groups.
+// D % 4 == 0), and each workgroup covers `rows` consecutive rows (dvc_set_tuning "upflow_rows").
 template <bool DELTA, bool SUBGRID, int VEC>
-__global__ __launch_bounds__(256) void k_upflow(const float *__restrict__ lo, const float *__restrict__ delta,
-                                                float *__restrict__ lo_out, float *__restrict__ up, long long B, int C,
-                                                int h, int w, int d, int H, int W, int D, float rh, float rw, float rd,
-                                                float sh, float sw, float sd) {
-    const int bc = blockIdx.z;
+__device__ __forceinline__ void upflow_item(const float *__restrict__ lo, const float *__restrict__ delta,
+                                            float *__restrict__ up, int bc, int xc, int y0, int rows, int C, int h,
+                                            int w, int d, int H, int W, int D, float rh, float rw, float rd, float sh,
+                                            float sw, float sd) {
     const int c = bc % C;
-    if (lo_out != nullptr) {   // coords1 + delta, spread over the whole grid
-        const long long total_lo = B * C * (long long)h * w * d;
-        const long long nthr = (long long)gridDim.x * gridDim.y * gridDim.z * blockDim.x;
-        for (long long i = (((long long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * blockDim.x +
-                           threadIdx.x;
-             i < total_lo; i += nthr)
-            lo_out[i] = DELTA ? lo[i] + delta[i] : lo[i];
-    }
-    const int p = (blockIdx.x * blockDim.x + threadIdx.x) * VEC;   // first z of this lane's VEC outputs
+    const int p = (xc * (int)blockDim.x + (int)threadIdx.x) * VEC;   // first z of this lane's VEC outputs
     if (p >= W * D) return;
     const int ox = p / D, oz0 = p - ox * D;
     const float scale = c == 0 ? sh : (c == 1 ? sw : (c == 2 ? sd : 1.0f));
@@ -119,8 +140,42 @@ __global__ __launch_bounds__(256) void k_upflow(const float *__restrict__ lo, co
     for (int k = 0; k < VEC; ++k) az[k] = axis_weights(oz0 + k, d, rd);
     const long long base = (long long)bc * h * w * d;
     const long long plane = (long long)W * D;
-    const int y0 = blockIdx.y * kUpRows;
-    for (int oy = y0; oy < y0 + kUpRows && oy < H; ++oy) {
+    // upsampling in z: z-run loads + low-res row cache (per-lane guard: the run must cover every corner)
+    if (VEC == 4 && rd <= 1.0f && az[VEC - 1].i1 - az[0].i0 < kZRun) {
+        const AxisW (&az4)[4] = *reinterpret_cast<const AxisW(*)[4]>(&az[0]);
+        const int zlo = az[0].i0;
+        int cy0 = -1, cy1 = -1;
+        float T0[4], T1[4];
+        for (int oy = y0; oy < y0 + rows && oy < H; ++oy) {
+            const AxisW ay = axis_weights(oy, h, rh);
+            if (ay.i0 != cy0) {
+                if (ay.i0 == cy1) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) T0[k] = T1[k];
+                } else {
+                    upflow_row<DELTA, SUBGRID>(lo, delta, base, c, ay.i0, w, d, zlo, ax, az4, T0);
+                }
+                cy0 = ay.i0;
+            }
+            if (ay.i1 != cy1) {
+                if (ay.i1 == cy0) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) T1[k] = T0[k];
+                } else {
+                    upflow_row<DELTA, SUBGRID>(lo, delta, base, c, ay.i1, w, d, zlo, ax, az4, T1);
+                }
+                cy1 = ay.i1;
+            }
+            float4 v;
+            v.x = __builtin_fmaf(ay.l1, T1[0], ay.l0 * T0[0]) * scale;
+            v.y = __builtin_fmaf(ay.l1, T1[1], ay.l0 * T0[1]) * scale;
+            v.z = __builtin_fmaf(ay.l1, T1[2], ay.l0 * T0[2]) * scale;
+            v.w = __builtin_fmaf(ay.l1, T1[3], ay.l0 * T0[3]) * scale;
+            *reinterpret_cast<float4 *>(up + ((long long)bc * H + oy) * plane + p) = v;
+        }
+        return;
+    }
+    for (int oy = y0; oy < y0 + rows && oy < H; ++oy) {
         const AxisW ay = axis_weights(oy, h, rh);
         float *dst = up + ((long long)bc * H + oy) * plane + p;
         if (VEC == 4) {
@@ -136,17 +191,47 @@ __global__ __launch_bounds__(256) void k_upflow(const float *__restrict__ lo, co
     }
 }
 
+// up (B, C, H, W, D) = upflow_3d(lo (+ delta) (- coords0)); channels 0..2 scaled.
+// lo_out (nullable) receives lo + delta at low resolution (the updated coords1).
+// Work items: (chunk of one output (W, D) plane = 256 lanes x VEC consecutive z,
+// group of `rows` output rows, b*C + c), chunk fastest; a grid of ~1-2 K
+// workgroups strides over them (the workgroup dispatcher, not HBM, limits a
+// one-item-per-workgroup grid here: 6 K groups took 47 us, 768 took 15 us).  The
+// h-axis weights and the channel are uniform per item, lanes store VEC
+// consecutive z (16-byte stores for VEC 4, D % 4 == 0).
+template <bool DELTA, bool SUBGRID, int VEC>
+__global__ __launch_bounds__(256) void k_upflow(const float *__restrict__ lo, const float *__restrict__ delta,
+                                                float *__restrict__ lo_out, float *__restrict__ up, long long B, int C,
+                                                int h, int w, int d, int H, int W, int D, float rh, float rw, float rd,
+                                                float sh, float sw, float sd, int nx, int ny, int rows) {
+    if (lo_out != nullptr) {   // coords1 + delta, spread over the whole grid
+        const long long total_lo = B * C * (long long)h * w * d;
+        const long long nthr = (long long)gridDim.x * blockDim.x;
+        for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total_lo; i += nthr)
+            lo_out[i] = DELTA ? lo[i] + delta[i] : lo[i];
+    }
+    const long long nitems = (long long)nx * ny * B * C;
+    for (long long it = blockIdx.x; it < nitems; it += gridDim.x) {
+        const int xc = (int)(it % nx);
+        const long long r = it / nx;
+        const int yg = (int)(r % ny);
+        const int bc = (int)(r / ny);
+        upflow_item<DELTA, SUBGRID, VEC>(lo, delta, up, bc, xc, yg * rows, rows, C, h, w, d, H, W, D, rh, rw, rd, sh,
+                                         sw, sd);
+    }
+}
+
 template __global__ void k_upflow<false, false, 1>(const float *, const float *, float *, float *, long long, int,
-    int, int, int, int, int, int, float, float, float, float, float, float);
+    int, int, int, int, int, int, float, float, float, float, float, float, int, int, int);
 template __global__ void k_upflow<false, true, 1>(const float *, const float *, float *, float *, long long, int,
-    int, int, int, int, int, int, float, float, float, float, float, float);
+    int, int, int, int, int, int, float, float, float, float, float, float, int, int, int);
 template __global__ void k_upflow<true, true, 1>(const float *, const float *, float *, float *, long long, int,
-    int, int, int, int, int, int, float, float, float, float, float, float);
+    int, int, int, int, int, int, float, float, float, float, float, float, int, int, int);
 template __global__ void k_upflow<false, false, 4>(const float *, const float *, float *, float *, long long, int,
-    int, int, int, int, int, int, float, float, float, float, float, float);
+    int, int, int, int, int, int, float, float, float, float, float, float, int, int, int);
 template __global__ void k_upflow<false, true, 4>(const float *, const float *, float *, float *, long long, int,
-    int, int, int, int, int, int, float, float, float, float, float, float);
+    int, int, int, int, int, int, float, float, float, float, float, float, int, int, int);
 template __global__ void k_upflow<true, true, 4>(const float *, const float *, float *, float *, long long, int,
-    int, int, int, int, int, int, float, float, float, float, float, float);
+    int, int, int, int, int, int, float, float, float, float, float, float, int, int, int);
 
 }  // namespace dvc
