@@ -45,8 +45,20 @@ __all__ = ["CorrBlock", "CorrBlockFused", "CorrBlockOnTheFly", "bilinear_sampler
 
 
 def resolve_precision(fmap: torch.Tensor, precision: Optional[str]) -> str:
+    """Storage/MFMA precision of the pyramid.  Explicit argument > DVCCORR_PRECISION >
+    AMP policy > input dtype.
+
+    AMP policy: the reference's Trainer runs RAFTDVC.forward under
+    torch.amp.autocast('cuda') (trainer.py:249-252), so its CorrBlock matmul and
+    avg_pool3d produce an fp16 pyramid (corr.py:155-167) even though the fmaps are
+    cast to float32 first (raft_dvc.py:366-367), while grid_sample autocasts back to
+    float32.  Inside an enabled CUDA autocast region this block likewise builds and
+    stores 16-bit (bf16: same 2 bytes per value, fp32 range) and returns float32
+    lookups; outside it, float32 fmaps build in exact f32."""
     if precision is None:
         precision = os.environ.get("DVCCORR_PRECISION") or None
+    if precision is None and fmap.is_cuda and torch.is_autocast_enabled("cuda"):
+        precision = "bf16"
     if precision is None:
         precision = "fp32" if fmap.dtype == torch.float32 else "bf16"
     ops.dtype_code(precision)

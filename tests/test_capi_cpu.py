@@ -141,3 +141,19 @@ def test_coords_grid_matches_reference_fixture():
     import dvccorr
     g = dvccorr.coords_grid_3d(2, 3, 4, 5, torch.device("cpu"))
     np.testing.assert_array_equal(g.numpy(), prng.identity_coords(2, 3, 4, 5))
+
+
+def test_precision_policy_host_logic(monkeypatch):
+    """Explicit precision > DVCCORR_PRECISION > AMP (CUDA autocast, GPU-tested) > input dtype."""
+    import dvccorr
+    monkeypatch.delenv("DVCCORR_PRECISION", raising=False)
+    f32, b16 = torch.zeros(1), torch.zeros(1, dtype=torch.bfloat16)
+    assert dvccorr.resolve_precision(f32, None) == "fp32"
+    assert dvccorr.resolve_precision(b16, None) == "bf16"
+    assert dvccorr.resolve_precision(torch.zeros(1, dtype=torch.float16), None) == "bf16"
+    assert dvccorr.resolve_precision(f32, "bf16") == "bf16"
+    monkeypatch.setenv("DVCCORR_PRECISION", "bf16")
+    assert dvccorr.resolve_precision(f32, None) == "bf16"
+    assert dvccorr.resolve_precision(b16, "fp32") == "fp32"
+    with pytest.raises(ValueError):
+        dvccorr.resolve_precision(f32, "fp8")

@@ -89,6 +89,35 @@ def test_grad_bf16_build():
         assert e1 <= BF16_TOL and e2 <= BF16_TOL, (kind, e1, e2)
 
 
+def test_amp_policy_forward_and_grads():
+    """AMP dtype policy: under torch.amp.autocast('cuda') (the reference Trainer,
+    trainer.py:249-252) float32 fmaps (raft_dvc.py:366-367) build a 16-bit pyramid,
+    lookups come back float32 and gradients reach both fmaps in float32; values within
+    the bf16 tolerance of the reference's float32 outputs and gradients."""
+    import dvccorr
+    g = load_golden("grad_equiv_L2_r4_rand.npz")
+    f1, f2, coords, G, L, r, legacy = grad_inputs(g)
+    ref = orc.corr_lookup(f1, f2, coords, L, r, legacy)
+    for cls in (dvccorr.CorrBlock, dvccorr.CorrBlockFused):
+        t1 = torch.from_numpy(f1).to(DEV).requires_grad_(True)
+        t2 = torch.from_numpy(f2).to(DEV).requires_grad_(True)
+        with torch.amp.autocast("cuda"):
+            blk = cls(t1, t2, L, r, legacy_wd_swap=legacy)
+            out = blk(torch.from_numpy(coords).to(DEV))
+            loss = (out * torch.from_numpy(G).to(DEV)).sum()
+        assert blk.precision == "bf16" and out.dtype == torch.float32
+        loss.backward()
+        assert t1.grad.dtype == torch.float32 and t2.grad.dtype == torch.float32
+        assert orc.rel_err(out.detach().cpu().numpy(), ref) <= BF16_TOL
+        e1, e2 = orc.rel_err(t1.grad.cpu().numpy(), g["grad_f1"]), orc.rel_err(t2.grad.cpu().numpy(), g["grad_f2"])
+        assert e1 <= BF16_TOL and e2 <= BF16_TOL, (cls.__name__, e1, e2)
+    # outside autocast the same fp32 inputs build in exact f32; an explicit precision always wins
+    assert dvccorr.CorrBlock(torch.from_numpy(f1).to(DEV), torch.from_numpy(f2).to(DEV), L, r).precision == "fp32"
+    with torch.amp.autocast("cuda"):
+        assert dvccorr.CorrBlock(torch.from_numpy(f1).to(DEV), torch.from_numpy(f2).to(DEV), L, r,
+                                 precision="fp32").precision == "fp32"
+
+
 def test_grad_reproducible_and_accumulates():
     """Bitwise reproducible (fixed summation order, no atomics); two lookups on one block (the GRU loop calls
     it 12x) accumulate like two independent calls."""
