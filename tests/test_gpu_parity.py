@@ -381,3 +381,42 @@ def test_fused_tile_slab():
     q = ops.pack_queries(f1[:, :, h0:h1].reshape(1, C, -1), dt)
     part = ops.lookup_fused(q, t, c[:, :, h0:h1].reshape(1, 3, -1), C, H, W, D, L, r, False, dt)
     assert torch.equal(part, full.view(1, -1, H, W, D)[:, :, h0:h1].reshape(1, -1, (h1 - h0) * W * D))
+
+
+def test_graph_captured_iteration_loop():
+    """The 12 GRU-iteration lookups + flow tails captured once in a HIP graph
+    (torch.cuda.CUDAGraph over the C ABI: stream-ordered, allocation-free launches)
+    and replayed on new coordinates give the eager results bit for bit."""
+    import dvccorr
+    S, C, L, r, iters = 16, 64, 4, 4, 12
+    f1 = torch.from_numpy(prng.normal(900, (1, C, S, S, S))).to(DEV)
+    f2 = torch.from_numpy(prng.normal(901, (1, C, S, S, S))).to(DEV)
+    blk = dvccorr.CorrBlock(f1, f2, L, r, precision="bf16")
+    deltas = [torch.from_numpy(prng.uniform(910 + i, (1, 3, S, S, S), -0.5, 0.5)).to(DEV) for i in range(iters)]
+    c_static = torch.from_numpy(prng.flow_coords(902, 1, S, S, S, 2.0)).to(DEV)
+
+    def loop(c):
+        outs = []
+        for i in range(iters):
+            outs.append(blk(c))
+            c, up = dvccorr.flow_step(c, deltas[i], (4 * S, 4 * S, 4 * S))
+        return outs, c, up
+
+    with torch.no_grad():
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            loop(c_static)   # warm-up outside capture
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            g_outs, g_c, g_up = loop(c_static)
+        new_c = torch.from_numpy(prng.flow_coords(903, 1, S, S, S, 3.0)).to(DEV)
+        c_static.copy_(new_c)
+        g.replay()
+        torch.cuda.synchronize()
+        e_outs, e_c, e_up = loop(new_c)
+        torch.cuda.synchronize()
+    for a, b in zip(g_outs, e_outs):
+        assert torch.equal(a, b)
+    assert torch.equal(g_c, e_c) and torch.equal(g_up, e_up)
