@@ -63,6 +63,7 @@ def parse():
                     help="N>1: weak = one volume pair per rank (global batch N); strong = one pair's query "
                          "voxels sharded by H slabs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--tune", default="", help="diagnostics: comma list key=value of dvc_set_tuning knobs")
     ap.add_argument("--cpu-rows", type=int, default=4096, help="query rows of the bounded CPU sample")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
     return ap.parse_args()
@@ -143,6 +144,9 @@ def main():
     from dvccorr import ops
     from dvccorr import _lib
     from dvccorr.sharded import LOCAL, ShardedCorrBlock, slab_bounds
+    for kv in filter(None, args.tune.split(",")):
+        k, v = kv.split("=")
+        _lib.set_tuning(k, int(v))
 
     S, C, L, R = args.size, args.channels, args.levels, args.radius
     B = 1
