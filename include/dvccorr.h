@@ -183,9 +183,13 @@ int dvc_upflow(const float *flow, float *flow_up, int B, int C, int h, int w, in
 int dvc_flow_step(const float *coords1, const float *delta_flow, float *coords1_out, float *flow_up, int B, int h,
                   int w, int d, int H, int W, int D, void *stream);
 
-/* Kernel-variant knob for A/B timing (process-wide, not thread-safe):
- *   "lookup_variant" 0 = unaligned 16-byte run loads, 1 = aligned chunks + v_perm shifter;
- *   "lookup_ablate"  diagnostics only, invalidates outputs: 1 = skip stores, 2 = skip loads. */
+/* Diagnostics hook for A/B timing.  The product kernel selection is a fixed table;
+ * an override set here is THREAD-LOCAL (it changes only the calling host thread's
+ * launches, on any stream), so the library holds no process-wide mutable state.
+ *   "lookup_variant" 2 = LDS-staged tile kernel (default), 0 = walk with unaligned
+ *                    16-byte run loads, 1 = walk with aligned chunks + v_perm shifter;
+ *   "fused_variant", "build_variant", "upflow_rows", ... see capi.hip;
+ *   "*_ablate"       diagnostics only, invalidates outputs. */
 int dvc_set_tuning(const char *key, int value);
 
 const char *dvc_last_error(void);

@@ -35,12 +35,25 @@ constexpr int kBQ = 128, kBP = 128;
 // Prefetch load hidden from hipcc's waitcnt bookkeeping (see the loop below): the
 // compiler cannot carry store counts across the loop back-edge and would otherwise
 // drain every epilogue store (s_waitcnt vmcnt(0)) before the next tile's LDS write.
+//
+// HIDDEN is only safe while the kernel does not spill: the compiler treats the asm
+// destination as written when the asm statement retires, so under register pressure
+// it may spill that VGPR or hand it to another value while the load is still in
+// flight, and the late load then overwrites whatever lives there (an address, in the
+// C_pad = 256 fault of round 1: k_build_bf16_2b<32> spilled 268 VGPRs).  Instances
+// with NCH > 16 therefore use ordinary loads the compiler tracks (Hidden<NCH>).
+template <int NCH> struct Hidden { static constexpr bool value = NCH <= 16; };
+
+template <bool HIDDEN>
 __device__ __forceinline__ void asm_load16(u32x4 &dst, const void *p) {
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(p) : "memory");
+    if constexpr (HIDDEN) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(p) : "memory");
+    else dst = *reinterpret_cast<const u32x4 *>(p);
 }
 // Same, from a wave-uniform base (SGPR pair) plus a 32-bit per-lane byte offset.
+template <bool HIDDEN>
 __device__ __forceinline__ void asm_load16_s(u32x4 &dst, const void *base, int off) {
-    asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(dst) : "v"(off), "s"(base) : "memory");
+    if constexpr (HIDDEN) asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(dst) : "v"(off), "s"(base) : "memory");
+    else dst = *reinterpret_cast<const u32x4 *>(reinterpret_cast<const unsigned char *>(base) + off);
 }
 // After the counted wait: make every prefetch register opaque at this point so no
 // consumer is scheduled above the wait (guide 5.7, form (ii)).
@@ -108,7 +121,7 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict_
 #pragma unroll
         for (int i = 0; i < PF; ++i) {
             const int id = i * 256 + t;
-            asm_load16(pf[i], Tb + (p0 + id / nch) * Cp + (id % nch) * 8);
+            asm_load16<Hidden<NCH>::value>(pf[i], Tb + (p0 + id / nch) * Cp + (id % nch) * 8);
         }
     }
     // vector-memory ops issued after the prefetch in one iteration: the epilogue stores
@@ -140,7 +153,7 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict_
 #pragma unroll
             for (int i = 0; i < PF; ++i) {
                 const int id = i * 256 + t;
-                asm_load16(pf[i], Tb + (pn + id / nch) * Cp + (id % nch) * 8);
+                asm_load16<Hidden<NCH>::value>(pf[i], Tb + (pn + id / nch) * Cp + (id % nch) * 8);
             }
         }
 
@@ -304,7 +317,7 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16_2b(const bf16_t *__restri
         const long long cc = ct < ncol_tiles ? ct : ncol_tiles - 1;
         const bf16_t *tile = Tb + (col_begin + cc * kBP) * Cp;   // wave-uniform base
 #pragma unroll
-        for (int i = 0; i < PF; ++i) asm_load16_s(pf[i], tile, toff[i]);
+        for (int i = 0; i < PF; ++i) asm_load16_s<Hidden<NCH>::value>(pf[i], tile, toff[i]);
     };
     auto put = [&](u32x4 (&pf)[PF]) {
 #pragma unroll
@@ -437,11 +450,15 @@ __global__ __launch_bounds__(256, 1) void k_build_f32(const float *__restrict__ 
                                                       long long t_batch_rows, long long row_stride,
                                                       long long col_begin, long long col_end, int nchunk,
                                                       float scale) {
+    // K is staged in chunks of at most 128 channels (LDS: 64 x KC + 128 x KC floats).
+    // Cp <= 128: one chunk, the query tile stays resident across column tiles.  Wider
+    // features (C = 160..256) re-stage both tiles per chunk; the accumulation is still
+    // one k-ordered fmaf chain per output, so the result does not depend on KC.
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int nsl = Cp / 2;                       // 8-byte slots per row
-    const int msk = (nsl >= 32 ? 32 : nsl) - 1;
+    const int KC = Cp < 128 ? Cp : 128;
+    const bool resident = Cp <= 128;
     u32x2 *sQ = reinterpret_cast<u32x2 *>(smem);
-    u32x2 *sT = sQ + kFQ * nsl;
+    u32x2 *sT = sQ + kFQ * (KC / 2);
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int b = blockIdx.z;
     const long long qtile = blockIdx.x / nchunk;
@@ -450,44 +467,55 @@ __global__ __launch_bounds__(256, 1) void k_build_f32(const float *__restrict__ 
     const float *Qb = Q + (long long)b * Nq * Cp;
     const float *Tb = T + (long long)b * t_batch_rows * Cp;
 
-    for (int id = t; id < kFQ * nsl; id += 256) {
-        const int row = id / nsl, s = id - row * nsl;
-        u32x2 v = {0u, 0u};
-        if (q0 + row < Nq) v = *reinterpret_cast<const u32x2 *>(Qb + (q0 + row) * Cp + 2 * s);
-        sQ[row * nsl + (s ^ (row & msk))] = v;
-    }
+    // 8-byte slots of one K chunk [k0, k0 + kc): nsl = kc / 2 per row, XOR swizzled
+    auto stage_q = [&](int k0, int nsl, int msk) {
+        for (int id = t; id < kFQ * nsl; id += 256) {
+            const int row = id / nsl, s = id - row * nsl;
+            u32x2 v = {0u, 0u};
+            if (q0 + row < Nq) v = *reinterpret_cast<const u32x2 *>(Qb + (q0 + row) * Cp + k0 + 2 * s);
+            sQ[row * nsl + (s ^ (row & msk))] = v;
+        }
+    };
+    if (resident) stage_q(0, Cp / 2, (Cp / 2 >= 32 ? 32 : Cp / 2) - 1);
     const long long ncol_tiles = (col_end - col_begin + kFP - 1) / kFP;
     const int h = lane >> 5, r32 = lane & 31;
 
     for (long long ct = chunk; ct < ncol_tiles; ct += nchunk) {
         const long long p0 = col_begin + ct * kFP;
-        __syncthreads();
-        for (int id = t; id < kFP * nsl; id += 256) {
-            const int row = id / nsl, s = id - row * nsl;
-            sT[row * nsl + (s ^ (row & msk))] = *reinterpret_cast<const u32x2 *>(Tb + (p0 + row) * Cp + 2 * s);
-        }
-        __syncthreads();
         f32x16 acc[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int k = 0; k < 16; ++k) acc[j][k] = 0.0f;
-        const int arow = 32 * w + r32;
-        for (int kt = 0; kt < Cp / 4; ++kt) {
-            const int s = 2 * kt + h;
-            const u32x2 av = sT[arow * nsl + (s ^ (arow & msk))];
-            u32x2 bv[2];
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int row = 32 * j + r32;
-                bv[j] = sQ[row * nsl + (s ^ (row & msk))];
+        for (int k0 = 0; k0 < Cp; k0 += KC) {
+            const int kc = Cp - k0 < KC ? Cp - k0 : KC;
+            const int nsl = kc / 2;
+            const int msk = (nsl >= 32 ? 32 : nsl) - 1;
+            __syncthreads();   // previous chunk / staging image fully read
+            if (!resident) stage_q(k0, nsl, msk);
+            for (int id = t; id < kFP * nsl; id += 256) {
+                const int row = id / nsl, s = id - row * nsl;
+                sT[row * nsl + (s ^ (row & msk))] =
+                    *reinterpret_cast<const u32x2 *>(Tb + (p0 + row) * Cp + k0 + 2 * s);
             }
+            __syncthreads();
+            const int arow = 32 * w + r32;
+            for (int kt = 0; kt < kc / 4; ++kt) {
+                const int s = 2 * kt + h;
+                const u32x2 av = sT[arow * nsl + (s ^ (arow & msk))];
+                u32x2 bv[2];
 #pragma unroll
-            for (int u = 0; u < 2; ++u)
+                for (int j = 0; j < 2; ++j) {
+                    const int row = 32 * j + r32;
+                    bv[j] = sQ[row * nsl + (s ^ (row & msk))];
+                }
 #pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(av[u]), __uint_as_float(bv[j][u]),
-                                                                  acc[j], 0, 0, 0);
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(av[u]),
+                                                                      __uint_as_float(bv[j][u]), acc[j], 0, 0, 0);
+            }
         }
         __syncthreads();
         // staging [64 q][32 chunks of 4 cols] f32 in sT, chunk' = chunk ^ (q & 31)

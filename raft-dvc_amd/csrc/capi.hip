@@ -51,20 +51,23 @@ __global__ void k_upflow(const float *, const float *, float *, float *, long lo
 using namespace dvc;
 
 static thread_local char g_err[512] = "";
-static int g_lookup_variant = -1;   // tuning knobs (dvc_set_tuning)
-static int g_lookup_ablate = 0;
-static int g_lookup_nt = 1;          // nontemporal output stores in the tile kernel
-static int g_lookup_order = 1;       // tile kernel level order (LookupArgs::order)
-static int g_lookup_ldpol = 0;       // tile kernel load cache policy (LookupArgs::ldpol)
-static int g_build_ablate = 0;       // diagnostics only: k_build_bf16 ablation instance
-static int g_build_stpol = 0;        // cache-policy bits of the build's output stores
-static int g_build_variant = 1;      // 1 = two-barrier bf16-store kernel (k_build_bf16_2b), 0 = k_build_bf16
+// Kernel selection.  The defaults below are the product configuration (an immutable
+// table); dvc_set_tuning is a diagnostics hook whose overrides are THREAD-LOCAL, so a
+// tuning call on one host thread never changes the kernels another thread launches.
+static thread_local int g_lookup_variant = -1;   // tuning knobs (dvc_set_tuning)
+static thread_local int g_lookup_ablate = 0;
+static thread_local int g_lookup_nt = 1;          // nontemporal output stores in the tile kernel
+static thread_local int g_lookup_order = 1;       // tile kernel level order (LookupArgs::order)
+static thread_local int g_lookup_ldpol = 0;       // tile kernel load cache policy (LookupArgs::ldpol)
+static thread_local int g_build_ablate = 0;       // diagnostics only: k_build_bf16 ablation instance
+static thread_local int g_build_stpol = 0;        // cache-policy bits of the build's output stores
+static thread_local int g_build_variant = 1;      // 1 = two-barrier bf16-store kernel (k_build_bf16_2b), 0 = k_build_bf16
 // fused lookup kernel where the MFMA path applies: 2 = k_fused_box 2x2x16, 8 waves (default),
 // 3 = k_fused_box 4x4x4 cubes, 8 waves, 4 = k_fused_box 2x2x16, 4 waves, 1 = k_fused_tile, 0 = two-stage VALU
-static int g_fused_variant = 2;
-static int g_upflow_rows = 8;        // output rows per k_upflow work item
-static int g_upflow_wgs = 1024;      // k_upflow grid (workgroups striding over the items)
-static int g_fused_ablate = 0;       // diagnostics only: 1 = skip output stores, 2 = skip window dots (cube kernel)
+static thread_local int g_fused_variant = 2;
+static thread_local int g_upflow_rows = 8;        // output rows per k_upflow work item
+static thread_local int g_upflow_wgs = 1024;      // k_upflow grid (workgroups striding over the items)
+static thread_local int g_fused_ablate = 0;       // diagnostics only: 1 = skip output stores, 2 = skip window dots (cube kernel)
 
 static int fail(int code, const char *fmt, ...) {
     va_list ap;
@@ -101,6 +104,7 @@ static int fill_lookup_args(LookupArgs &A, const dvc_layout &lay, const void *co
     A.order = g_lookup_order;
     A.ldpol = g_lookup_ldpol;
     A.proj_w = nullptr; A.proj_b = nullptr; A.proj_out = nullptr;
+    A.split_levels = 0;
     return DVC_OK;
 }
 
@@ -122,9 +126,15 @@ static bool tile_ok(const LookupArgs &A, size_t esz) {
     return A.r >= 1 && A.r <= 6 && (long long)64 * A.row_stride * (long long)esz < (1LL << 31) - 4096;
 }
 
+// Fewer query tiles than 2 x the 256 CUs (e.g. one rank's 4096-row slab at config #3: 64 tiles) leave most
+// of the chip idle; then each workgroup takes one (tile, level) pair instead of a tile's whole level loop.
+static constexpr long long kSplitTiles = 512;
+
 template <typename T, bool NT>
-static void launch_tile_nt(const LookupArgs &A, hipStream_t s) {
-    const unsigned blocks = (unsigned)(A.B * A.nqb);
+static void launch_tile_nt(const LookupArgs &A0, hipStream_t s) {
+    LookupArgs A = A0;
+    A.split_levels = (long long)A.B * A.nqb < kSplitTiles && A.nl > 1;
+    const dim3 blocks((unsigned)(A.B * A.nqb), A.split_levels ? (unsigned)A.nl : 1u);
     const unsigned threads = 64u * (unsigned)((2 * A.r + 3) / 3);
     if constexpr (std::is_same<T, bf16_t>::value && NT) {
         if (A.r == 4 && A.ablate >= 1 && A.ablate <= 3) {   // diagnostics only
@@ -345,9 +355,11 @@ int dvc_corr_build(const void *packed_q, const void *packed_t, void *corr, int B
         return fail(DVC_ERR_INVALID, "build: bad column range [%lld, %lld) for row_stride %lld", (long long)col_begin,
                     (long long)col_end, lay.row_stride);
     const int Cp = lay.c_pad;
-    // C_pad 256 faulted once on the GPU (bf16 build or fused tile, tests/test_gpu_parity.py, round 1): refused
-    // until it is isolated; every configuration of the reference uses C = 128
-    if (Cp > 128) return fail(DVC_ERR_UNSUPPORTED, "build: C=%d > 128 not supported", C);
+    // bf16 tiles keep [128][Cp] query and target tiles in LDS: C_pad <= 256 (160 KB per CU).  The C_pad = 256
+    // fault of round 1 was k_build_bf16_2b<32> spilling the destinations of its hidden prefetch loads; those
+    // instances now use compiler-visible loads (build_gemm.hip, Hidden<NCH>).
+    if (in_dtype == DVC_BF16 && Cp > 256) return fail(DVC_ERR_UNSUPPORTED, "build: bf16 C=%d > 256 not supported", C);
+    if (Cp > 1024) return fail(DVC_ERR_UNSUPPORTED, "build: C=%d > 1024 not supported", C);
     const float scale = 1.0f / sqrtf((float)C);   // corr / sqrt(C) (corr.py:165)
     hipStream_t s = (hipStream_t)stream;
     const long long ncol_tiles = ceil_div(col_end - col_begin, 128);
@@ -394,7 +406,8 @@ int dvc_corr_build(const void *packed_q, const void *packed_t, void *corr, int B
     } else if (in_dtype == DVC_F32) {
         if (store_dtype != DVC_F32)
             return fail(DVC_ERR_UNSUPPORTED, "build: float32 inputs need a float32 store");
-        const size_t lds = (size_t)64 * Cp * 4 + std::max<size_t>((size_t)128 * Cp * 4, 32768);
+        const size_t KC = std::min(Cp, 128);   // channels per LDS chunk (k_build_f32)
+        const size_t lds = (size_t)64 * KC * 4 + std::max<size_t>((size_t)128 * KC * 4, 32768);
         static bool attr = false;
         if (!attr) {
             (void)hipFuncSetAttribute((const void *)k_build_f32, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);

@@ -43,6 +43,8 @@ struct LookupArgs {
     int ablate;                    // diagnostics only: 1 = skip output stores, 2 = skip run loads
     int order;                     // tile kernel: 1 = odd tiles walk the levels coarse-to-fine
     int ldpol;                     // tile kernel: cache-policy bits of the plane loads
+    int split_levels;              // tile kernel: one level per workgroup (blockIdx.y), for launches whose
+                                   // query tiles alone cannot fill the chip (one rank's slab)
     long long off[DVC_MAX_LEVELS];
     // tile kernel with the motion encoder's convc1 fused (PROJ instances only):
     // packed bf16 weights (dvc_proj_pack), bias[96], out (B, 96, Nq)

@@ -130,7 +130,7 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3 + (PROJ ? 1 : 0)), 2) void k_
     const long long q = A.q0 + qt + lane;
     const bool active = lane < nvalid;
     const long long Nq = A.Nq;
-    const bool rev = A.order && (blockIdx.x & 1);   // level order of this tile (see the level loop)
+    const bool rev = A.order && !A.split_levels && (blockIdx.x & 1);   // level order (see the level loop)
 
     if constexpr (PROJ) {
         if (wave == C::NWAVES) {   // the convc1 consumer wave
@@ -436,7 +436,9 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3 + (PROJ ? 1 : 0)), 2) void k_
 
     // odd tiles walk the levels coarse-to-fine, so the two tiles sharing a CU mix the
     // gather-heavy fine levels with the store-heavy coarse ones
-    for (int li = 0; li < A.nl; ++li) {
+    const int li0 = A.split_levels ? (int)blockIdx.y : 0;
+    const int li1 = A.split_levels ? li0 + 1 : A.nl;
+    for (int li = li0; li < li1; ++li) {
         const int l = A.l0 + (rev ? A.nl - 1 - li : li);
         if (A.generic[l] && !A.zero[l]) continue;   // legacy level with W != D: k_lookup_generic
         if (NU_LAST == C::COLS || wave < C::NWAVES - 1) level(l, std::integral_constant<int, C::COLS>{});

@@ -24,11 +24,21 @@ bf16 MFMA and stores bf16 (tolerance 1e-2), halving the HBM traffic; the
 default follows the input dtype (fp16/bf16 inputs -> bf16), overridable with
 the DVCCORR_PRECISION environment variable.
 
-Backward: when a feature map requires grad, every call is an autograd node whose
-backward runs dvc_corr_backward (sparse per-query window gradients, no dense
-d(corr), no atomics) and returns d fmap1 / d fmap2; coordinates get no gradient,
-as RAFTDVC.forward detaches them (raft_dvc.py:441).  Twelve calls on one block
-accumulate in autograd like the reference's twelve grid_sample calls.
+Backward: when a feature map requires grad, every call is the differentiable
+operator dvccorr::lookup_ad (library.py) whose registered autograd formula runs
+dvc_corr_backward (sparse per-query window gradients, no dense d(corr), no
+atomics) and returns d fmap1 / d fmap2; coordinates get no gradient, as
+RAFTDVC.forward detaches them (raft_dvc.py:441).  Twelve calls on one block
+accumulate in autograd like the reference's twelve grid_sample calls, and
+torch.utils.checkpoint(block, coords, use_reentrant=False) (checkpoint_corr,
+raft_dvc.py:446-448) recomputes the lookup in the backward pass.
+
+Capacity: the materialised pyramid is B * N * row_stride values; CorrBlock
+checks it against the device's free HBM before allocating and raises
+torch.cuda.OutOfMemoryError naming the on-the-fly block instead (the
+reference's Trainer catches that error, trainer.py:287-304);
+make_corr_block("mi355x_auto", ...) picks the fused block when the volume
+does not fit.
 """
 from __future__ import annotations
 
@@ -37,11 +47,11 @@ from typing import List, Optional
 
 import torch
 
-from . import ops
+from . import library, ops
 from ._lib import layout
 
 __all__ = ["CorrBlock", "CorrBlockFused", "CorrBlockOnTheFly", "bilinear_sampler_3d", "coords_grid_3d",
-           "upflow_3d", "flow_step", "make_corr_block", "resolve_precision"]
+           "upflow_3d", "flow_step", "make_corr_block", "resolve_precision", "pyramid_bytes", "hbm_available"]
 
 
 def resolve_precision(fmap: torch.Tensor, precision: Optional[str]) -> str:
@@ -69,33 +79,31 @@ def _wants_grad(*ts: torch.Tensor) -> bool:
     return torch.is_grad_enabled() and any(t.requires_grad for t in ts)
 
 
-class _LookupFn(torch.autograd.Function):
-    """One lookup call as an autograd node (reference: autograd through corr.py:141-208).
+def _check_backward_support(lay, C: int, radius: int, legacy: bool) -> None:
+    """Raise at construction (not after twelve forward lookups) when dvc_corr_backward cannot
+    differentiate this block (include/dvccorr.h: radius 1..6, C <= 128)."""
+    if not 1 <= radius <= 6:
+        raise NotImplementedError(f"dvccorr backward supports radius 1..6, got {radius}")
+    if lay.c_pad > 128:
+        raise NotImplementedError(f"dvccorr backward supports C <= 128 feature channels, got {C}")
 
-    forward: the block's lookup kernels; backward: dvc_corr_backward -> (d fmap1, d fmap2).
-    Coordinates get no gradient (RAFTDVC.forward detaches them, raft_dvc.py:441)."""
 
-    @staticmethod
-    def forward(ctx, coords, fmap1, fmap2, blk):
-        ctx.blk = blk
-        ctx.legacy = blk.legacy_wd_swap
-        ctx.dtypes = (fmap1.dtype, fmap2.dtype)
-        ctx.save_for_backward(coords)
-        return blk._lookup(coords)
+def pyramid_bytes(B: int, C: int, H: int, W: int, D: int, num_levels: int, precision: str = "fp32") -> int:
+    """HBM bytes of the materialised pyramid CorrBlock allocates (B x N rows of row_stride values)."""
+    lay = layout(H, W, D, num_levels, C)
+    esz = 2 if precision == "bf16" else 4
+    return B * H * W * D * lay.row_stride * esz + 2 * ops.GUARD_BYTES
 
-    @staticmethod
-    def backward(ctx, grad_out):
-        (coords,) = ctx.saved_tensors
-        blk = ctx.blk
-        B, C, H, W, D = blk.shape
-        N = H * W * D
-        d1, d2 = ops.corr_backward(blk._q, blk._t, coords.reshape(B, 3, N), grad_out.reshape(B, -1, N), C, H, W, D,
-                                   blk.num_levels, blk.radius, ctx.legacy, blk._dt)
-        return None, d1.view(B, C, H, W, D).to(ctx.dtypes[0]), d2.to(ctx.dtypes[1]), None
+
+def hbm_available(device) -> int:
+    """Bytes a new allocation can get: free device memory plus the caching allocator's unused reserve."""
+    device = torch.device(device)
+    free, _total = torch.cuda.mem_get_info(device)
+    return int(free + torch.cuda.memory_reserved(device) - torch.cuda.memory_allocated(device))
 
 
 class _Block:
-    """Shared __call__: coords check, then the kernels (wrapped in _LookupFn when grad is needed)."""
+    """Shared __call__: coords check, then the dvccorr operators (lookup_ad when grad is needed)."""
 
     def _check_coords(self, coords: torch.Tensor) -> None:
         B, _, H, W, D = self.shape
@@ -104,9 +112,14 @@ class _Block:
 
     def __call__(self, coords: torch.Tensor) -> torch.Tensor:
         self._check_coords(coords)
+        B, C, H, W, D = self.shape
+        flat = coords.reshape(B, 3, H * W * D)
         if self._grad_fmaps is not None and torch.is_grad_enabled():
-            return _LookupFn.apply(coords, *self._grad_fmaps, self)
-        return self._lookup(coords)
+            out = library.lookup_ad(*self._grad_fmaps, getattr(self, "_corr", None), self._q, self._t, flat, C, H,
+                                    W, D, self.num_levels, self.radius, self.legacy_wd_swap, self._dt)
+        else:
+            out = self._lookup_flat(flat)
+        return out.view(B, -1, H, W, D)
 
 
 def _check_fmaps(fmap1: torch.Tensor, fmap2: torch.Tensor) -> None:
@@ -132,20 +145,30 @@ class CorrBlock(_Block):
         self.precision = resolve_precision(fmap1, precision)
         self._dt = ops.dtype_code(self.precision)
         self._grad_fmaps = (fmap1, fmap2) if _wants_grad(fmap1, fmap2) else None
+        if self._grad_fmaps is not None:
+            _check_backward_support(self._lay, C, radius, legacy_wd_swap)
+        if build not in ("gemm", "pool"):
+            raise ValueError(f"build must be 'gemm' or 'pool', got {build!r}")
+        ops._need_cuda(fmap1, fmap2)
+        need = pyramid_bytes(B, C, H, W, D, num_levels, self.precision)
+        avail = hbm_available(fmap1.device)
+        if need > avail:
+            raise torch.cuda.OutOfMemoryError(
+                f"dvccorr.CorrBlock: the materialised {self.precision} pyramid of ({H},{W},{D}) x {num_levels} levels "
+                f"needs {need / 2**30:.1f} GiB, {avail / 2**30:.1f} GiB of HBM is available; use "
+                f"CorrBlockFused (corr_impl 'mi355x_fused' / 'mi355x_auto'), which never materialises it")
         q = ops.pack_queries(fmap1.detach().reshape(B, C, H * W * D), self._dt)
         t = ops.pack_targets(fmap2.detach(), num_levels, self._dt)
         # the backward needs the packed operands (O(C * voxels)): keep them only then
         self._q, self._t = (q, t) if self._grad_fmaps is not None else (None, None)
         if build == "gemm":       # every level from the pooled targets, one launch
-            self._corr = ops.build(q, t, C, H, W, D, num_levels, self._dt, self._dt)
+            self._corr = library.build(q, t, C, H, W, D, num_levels, self._dt)
         elif build == "pool":     # the reference's op order: level 0 GEMM, then avg-pool the volume
             corr = ops.alloc_corr(B, H * W * D, self._lay.row_stride, self._dt, q.device, zero=True)
             ops.build(q, t, C, H, W, D, num_levels, self._dt, self._dt, 0, self._lay.level_elems[0], out=corr)
             for l in range(num_levels - 1):
                 ops.pool(corr, H, W, D, num_levels, l, self._dt)
             self._corr = corr
-        else:
-            raise ValueError(f"build must be 'gemm' or 'pool', got {build!r}")
 
     @property
     def corr_pyramid(self) -> List[torch.Tensor]:
@@ -160,25 +183,28 @@ class CorrBlock(_Block):
             views.append(v)
         return views
 
-    def _lookup(self, coords: torch.Tensor) -> torch.Tensor:
-        B, _, H, W, D = self.shape
-        out = ops.lookup(self._corr, coords.reshape(B, 3, H * W * D), H, W, D, self.num_levels, self.radius,
-                         self.legacy_wd_swap, self._dt)
-        return out.view(B, -1, H, W, D)
+    def _lookup_flat(self, coords_flat: torch.Tensor) -> torch.Tensor:
+        _, _, H, W, D = self.shape
+        return library.lookup(self._corr, coords_flat, H, W, D, self.num_levels, self.radius, self.legacy_wd_swap,
+                              self._dt)
 
     def lookup_convc1(self, coords: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
         """F.relu(convc1(self(coords))) -> (B, 96, H, W, D) fp32 with convc1 fused into the lookup.
 
         The motion encoder's first layer (update.py:219-222, 246: Conv3d(L*(2r+1)^3, 96, 1) + ReLU)
-        runs on bf16 MFMA inside the lookup kernel, so the L*(2r+1)^3-channel tensor never reaches
-        HBM (dvc_corr_lookup_proj; tolerance 1e-2 max-normalised, bf16 operands, fp32 accumulation).
-        When gradients are needed, or for radii/conventions the fused kernel does not cover, it is
-        the unfused composition F.relu(F.conv3d(self(coords), weight, bias)) on the GPU."""
+        runs on bf16 MFMA inside the lookup kernel of a bf16 block, so the L*(2r+1)^3-channel tensor
+        never reaches HBM (dvc_corr_lookup_proj; tolerance 1e-2 max-normalised, bf16 operands, fp32
+        accumulation).  An fp32 block (tolerance 1e-5), gradients, or radii/conventions the fused
+        kernel does not cover take the composition F.relu(F.conv3d(self(coords), weight, bias)) on
+        the GPU."""
         self._check_coords(coords)
         B, _, H, W, D = self.shape
         w = weight.reshape(weight.shape[0], -1)
-        fused_ok = (not (torch.is_grad_enabled() and (weight.requires_grad or bias.requires_grad or
-                                                      self._grad_fmaps is not None))
+        # fp32 blocks keep the reference's fp32 convc1 (update.py:246): the fused kernel's bf16 MFMA
+        # operands would cost ~5e-3 relative error, so they take the exact composition below
+        fused_ok = (self.precision == "bf16"
+                    and not (torch.is_grad_enabled() and (weight.requires_grad or bias.requires_grad or
+                                                          self._grad_fmaps is not None))
                     and 1 <= self.radius <= ops._lib.PROJ_MAX_RADIUS and w.shape[0] == ops._lib.PROJ_COUT
                     and not (self.legacy_wd_swap and any(lw != ld and min(lh, lw, ld) > 1
                                                          for lh, lw, ld in self._lay.levels())))
@@ -210,15 +236,15 @@ class CorrBlockFused(_Block):
         self.precision = resolve_precision(fmap1, precision)
         self._dt = ops.dtype_code(self.precision)
         self._grad_fmaps = (fmap1, fmap2) if _wants_grad(fmap1, fmap2) else None
+        if self._grad_fmaps is not None:
+            _check_backward_support(self._lay, C, radius, legacy_wd_swap)
         self._q = ops.pack_queries(fmap1.detach().reshape(B, C, H * W * D), self._dt)
         self._t = ops.pack_targets(fmap2.detach(), num_levels, self._dt)
-        self._ws = ops.fused_workspace(B, H * W * D, num_levels, radius, fmap1.device)
 
-    def _lookup(self, coords: torch.Tensor) -> torch.Tensor:
-        B, C, H, W, D = self.shape
-        out = ops.lookup_fused(self._q, self._t, coords.reshape(B, 3, H * W * D), C, H, W, D, self.num_levels,
-                               self.radius, self.legacy_wd_swap, self._dt, workspace=self._ws)
-        return out.view(B, -1, H, W, D)
+    def _lookup_flat(self, coords_flat: torch.Tensor) -> torch.Tensor:
+        _, C, H, W, D = self.shape
+        return library.lookup_fused(self._q, self._t, coords_flat, C, H, W, D, self.num_levels, self.radius,
+                                    self.legacy_wd_swap, self._dt)
 
 
 class CorrBlockOnTheFly(CorrBlockFused):
@@ -244,9 +270,16 @@ class CorrBlockOnTheFly(CorrBlockFused):
 
 
 def bilinear_sampler_3d(vol: torch.Tensor, coords: torch.Tensor, legacy_wd_swap: bool = False) -> torch.Tensor:
-    """vol (B, C, H, W, D), coords (B, H', W', D', 3) in (h, w, d) -> (B, C, H', W', D')."""
+    """vol (B, C, H, W, D), coords (B, H', W', D', 3) in (h, w, d) -> (B, C, H', W', D').
+
+    Forward only (k_sample3d): the reference uses it inside CorrBlock, which this package
+    differentiates as a whole; a standalone call on inputs that require grad raises instead of
+    silently returning a tensor with no autograd history."""
     if vol.ndim != 5 or coords.ndim != 5 or coords.shape[-1] != 3 or coords.shape[0] != vol.shape[0]:
         raise ValueError(f"bad shapes vol {tuple(vol.shape)} coords {tuple(coords.shape)}")
+    if _wants_grad(vol, coords):
+        raise NotImplementedError("dvccorr.bilinear_sampler_3d has no backward; call it under torch.no_grad() "
+                                  "or use the reference's F.grid_sample path for gradients")
     B, C = vol.shape[:2]
     out = ops.sample3d(vol, coords.reshape(B, -1, 3), legacy_wd_swap)
     return out.view(B, C, *coords.shape[1:4])
@@ -265,12 +298,64 @@ def coords_grid_3d(batch: int, ht: int, wd: int, dp: int, device: torch.device) 
     return grid.unsqueeze(0).expand(batch, 3, ht, wd, dp).contiguous()
 
 
+def _upflow_adjoint(grad_up: torch.Tensor, lo_shape) -> torch.Tensor:
+    """Adjoint of upflow_3d: the per-axis scale of channels 0..2 (corr.py:242-251), then the
+    transpose of trilinear align_corners=True interpolation (ATen's upsample_trilinear3d_backward,
+    the op autograd runs for the reference's F.interpolate at corr.py:234-239)."""
+    B, C, h, w, d = lo_shape
+    H, W, D = grad_up.shape[2:]
+    g = grad_up.float().clone()
+    for c, s in enumerate((H / h, W / w, D / d)[:min(C, 3)]):
+        g[:, c] *= s
+    return torch.ops.aten.upsample_trilinear3d_backward(g, [H, W, D], [B, C, h, w, d], True, None, None, None)
+
+
+class _UpflowFn(torch.autograd.Function):
+    """upflow_3d with the reference's gradient (flow_predictions carry the loss back to delta_flow
+    and the update block, raft_dvc.py:482-486): forward k_upflow, backward its adjoint."""
+
+    @staticmethod
+    def forward(ctx, flow, target_shape):
+        ctx.lo_shape = tuple(flow.shape)
+        ctx.in_dtype = flow.dtype
+        return ops.upflow(flow, target_shape)
+
+    @staticmethod
+    def backward(ctx, grad_up):
+        return _upflow_adjoint(grad_up, ctx.lo_shape).to(ctx.in_dtype), None
+
+
+class _FlowStepFn(torch.autograd.Function):
+    """flow_step with gradients: d coords1 = d delta = d coords1' + adjoint(d flow_up)
+    (coords1' = coords1 + delta_flow, flow_up = upflow_3d(coords1' - coords0))."""
+
+    @staticmethod
+    def forward(ctx, coords1, delta_flow, target_shape):
+        ctx.lo_shape = tuple(coords1.shape)
+        ctx.dtypes = (coords1.dtype, None if delta_flow is None else delta_flow.dtype)
+        return ops.flow_step(coords1, delta_flow, target_shape)
+
+    @staticmethod
+    def backward(ctx, g_coords, g_up):
+        g = torch.zeros(ctx.lo_shape, dtype=torch.float32, device=(g_up if g_up is not None else g_coords).device)
+        if g_coords is not None:
+            g = g + g_coords.float()
+        if g_up is not None:
+            g = g + _upflow_adjoint(g_up, ctx.lo_shape)
+        d1 = g.to(ctx.dtypes[0]) if ctx.needs_input_grad[0] else None
+        d2 = g.to(ctx.dtypes[1]) if ctx.needs_input_grad[1] else None
+        return d1, d2, None
+
+
 def upflow_3d(flow: torch.Tensor, target_shape=None, scale_factor: int = 8) -> torch.Tensor:
     """upflow_3d (src/core/corr.py:211-253): trilinear, align_corners=True, channels 0..2
-    scaled by target/source size per axis -- one k_upflow pass (dvc_upflow)."""
+    scaled by target/source size per axis -- one k_upflow pass (dvc_upflow).  Differentiable."""
     if target_shape is None:
         _, _, h, w, d = flow.shape
         target_shape = (h * scale_factor, w * scale_factor, d * scale_factor)
+    target_shape = tuple(int(v) for v in target_shape)
+    if _wants_grad(flow):
+        return _UpflowFn.apply(flow, target_shape)
     return ops.upflow(flow, target_shape)
 
 
@@ -281,8 +366,12 @@ def flow_step(coords1: torch.Tensor, delta_flow: Optional[torch.Tensor], target_
         flow_up = upflow_3d(coords1 - coords0, target_shape=target_shape)
 
     coords0 is the identity grid (raft_dvc.py:293), formed in registers.  Returns
-    (coords1, flow_up); the input coords1 is not modified.
+    (coords1, flow_up); the input coords1 is not modified.  Differentiable w.r.t.
+    coords1 and delta_flow (the flow loss reaches the update block through flow_up).
     """
+    target_shape = tuple(int(v) for v in target_shape)
+    if _wants_grad(coords1, *(() if delta_flow is None else (delta_flow,))):
+        return _FlowStepFn.apply(coords1, delta_flow, target_shape)
     return ops.flow_step(coords1, delta_flow, target_shape)
 
 
@@ -292,6 +381,8 @@ def make_corr_block(impl: str, fmap1: torch.Tensor, fmap2: torch.Tensor, num_lev
 
     impl "mi355x"        -> CorrBlock (materialised pyramid, fixed or legacy convention)
     impl "mi355x_fused"  -> CorrBlockFused (on-the-fly, fixed or legacy convention)
+    impl "mi355x_auto"   -> CorrBlock when its pyramid fits the free HBM (with 10 % headroom for the
+                            rest of the step), else CorrBlockFused (failure detection)
     """
     if sampler_version not in (1, 2):
         raise ValueError(f"Invalid corr_sampler_version: {sampler_version!r}. Must be 1 (legacy W<->D-swapped) "
@@ -301,4 +392,12 @@ def make_corr_block(impl: str, fmap1: torch.Tensor, fmap2: torch.Tensor, num_lev
         return CorrBlock(fmap1, fmap2, num_levels, radius, legacy_wd_swap=legacy, **kw)
     if impl == "mi355x_fused":
         return CorrBlockFused(fmap1, fmap2, num_levels, radius, legacy_wd_swap=legacy, **kw)
-    raise ValueError(f"Invalid corr_impl for dvccorr: {impl!r}. Must be 'mi355x' or 'mi355x_fused'")
+    if impl == "mi355x_auto":
+        _check_fmaps(fmap1, fmap2)
+        B, C, H, W, D = fmap1.shape
+        prec = resolve_precision(fmap1, kw.get("precision"))
+        fits = pyramid_bytes(B, C, H, W, D, num_levels, prec) <= 0.9 * hbm_available(fmap1.device)
+        cls = CorrBlock if fits else CorrBlockFused
+        kw = {k: v for k, v in kw.items() if cls is CorrBlock or k != "build"}
+        return cls(fmap1, fmap2, num_levels, radius, legacy_wd_swap=legacy, **kw)
+    raise ValueError(f"Invalid corr_impl for dvccorr: {impl!r}. Must be 'mi355x', 'mi355x_fused' or 'mi355x_auto'")

@@ -145,15 +145,21 @@ _PACK_CACHE: dict = {}
 
 
 def proj_pack_cached(weight: torch.Tensor, num_levels: int, radius: int, legacy: bool) -> torch.Tensor:
-    """proj_pack, re-packed only when the weight tensor (storage or in-place version) changes: the packing
-    is once per optimiser step, not once per lookup."""
-    key = (weight.data_ptr(), weight._version, tuple(weight.shape), weight.device, num_levels, radius, bool(legacy))
+    """proj_pack, re-packed only when the weight changes: the packing is once per optimiser step, not once
+    per lookup.  Entries belong to the weight tensor OBJECT (a weak reference, checked on every hit, and a
+    finalizer that drops the entry), plus its in-place version counter and shape, so a new weight that
+    lands on a freed weight's address never reuses the old packing."""
+    import weakref
+    key = (id(weight), num_levels, radius, bool(legacy))
     hit = _PACK_CACHE.get(key)
-    if hit is None:
-        if len(_PACK_CACHE) >= 8:
-            _PACK_CACHE.clear()
-        hit = _PACK_CACHE[key] = proj_pack(weight, num_levels, radius, legacy)
-    return hit
+    state = (weight._version, tuple(weight.shape), weight.device, weight.data_ptr())
+    if hit is not None and hit[0]() is weight and hit[1] == state:
+        return hit[2]
+    packed = proj_pack(weight, num_levels, radius, legacy)
+    if hit is None or hit[0]() is not weight:
+        weakref.finalize(weight, _PACK_CACHE.pop, key, None)
+    _PACK_CACHE[key] = (weakref.ref(weight), state, packed)
+    return packed
 
 
 def lookup_proj(corr: torch.Tensor, coords: torch.Tensor, packed_w: torch.Tensor, bias: torch.Tensor, H: int, W: int,

@@ -64,9 +64,11 @@ def gather_slabs(slab: torch.Tensor, H: int, group=None, dim: int = 2) -> torch.
         slab = torch.cat([slab, slab.new_zeros(shape)], dim=dim)
     slab = slab.contiguous()
     buf = slab.new_empty((world,) + tuple(slab.shape))
-    try:
+    # one collective, chosen from the group's backend (identical on every rank, so the ranks'
+    # collective sequences cannot diverge); a failing collective raises on every rank
+    if dist.get_backend(group) == "nccl":      # RCCL: one fused all-gather into the contiguous buffer
         dist.all_gather_into_tensor(buf, slab, group=group)
-    except (RuntimeError, NotImplementedError, ValueError):
+    else:                                      # gloo (CPU tests): list form
         dist.all_gather(list(buf.unbind(0)), slab, group=group)
     parts = []
     for r in range(world):
@@ -123,6 +125,10 @@ class ShardedCorrBlock:
                  radius: int = 4, legacy_wd_swap: bool = False, *, precision: Optional[str] = None,
                  impl: str = "materialised", group=None, gather_output: bool = False, build_events=None,
                  backend=HipRows):
+        if torch.is_grad_enabled() and (fmap1_slab.requires_grad or fmap2_slab.requires_grad):
+            raise NotImplementedError("ShardedCorrBlock is forward-only (inference and benchmarking): its "
+                                      "lookups have no autograd node; build it under torch.no_grad() or use "
+                                      "CorrBlock per rank for training")
         if fmap1_slab.shape != fmap2_slab.shape or fmap1_slab.ndim != 5:
             raise ValueError(f"slabs must be matching 5-D tensors; got {tuple(fmap1_slab.shape)} vs "
                              f"{tuple(fmap2_slab.shape)}")
