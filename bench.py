@@ -3,30 +3,41 @@
 
 Metric (BASELINE.json): corr build+lookup voxel-queries/s, 128^3 pair, 1/4
 encoder (32^3 x 128-channel feature maps), L=4, r=4, bf16-MFMA build, fp32
-lookup.  One step = one RAFTDVC forward's worth of correlation work:
-    [N>1: all-gather of the fmap2 slabs over RCCL]
+lookup, on 1/2/4/8 GPUs.  One step = one RAFTDVC forward's worth of
+correlation work (corr.py:116-208 called as raft_dvc.py:414-450 calls it):
+    [N>1: RCCL all-gather of the fmap2 H-slabs]                  fmap2 replication
     pack queries + pack target pyramid + build (all levels)      CorrBlock.__init__
     12 lookups with 12 different coordinate fields               12 x CorrBlock.__call__
-value = 12 * (query voxels, all ranks) * steps / wall time (whole job).
+value = 12 * (query voxels of the whole job) * steps / wall time.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...
+    torchrun --nproc-per-node N bench.py --gpus N ...     (what the driver runs)
 
-Multi-GPU: the units are voxel-queries and they are independent.
-Default --scaling weak: every rank owns its own volume pair (global batch = N),
-so per-GPU work is fixed and there is no data-path collective (only the
-timing barrier / max-reduce).  --scaling strong shards ONE pair's query voxels
-by H slabs (ShardedCorrBlock: one RCCL all-gather of the fmap2 slabs per
-forward), the north star's layout for 256^3 inputs (--size 64).
+`--gpus N` without a torchrun environment spawns torch.distributed.run with N
+ranks as a child process (this parent never touches the GPU) and exits with
+its code.
+
+Multi-GPU, default --scaling strong: ONE volume pair's query
+voxels are split into N H-slabs, one per rank; each rank all-gathers the fmap2
+slabs (RCCL, the data-path collective), builds only its own rows of every
+level and looks up its own queries; lookups stay shard-resident.  The per-rank
+step after the collective is replayed as a HIP graph (--no-graph: eager).
+At N>1 the line also carries `scaling_detail`, measured in the same job:
+T1 (rank 0 alone on the whole problem), the strong layout with every lookup
+all-gathered (--gather-output), weak scaling (one pair per rank) and config #4
+(256^3 input, 1/4 encoder: 64^3 fmaps) strong-scaled, each with E(n) =
+T1 / (n * Tn).
 
 Prints one JSON line (rank 0) with roofline (dominant kernel, HIP-event timed
-on its stream) and cpu_baseline (oracle/torch_cpu.py on the host, rank 0, N=1).
+on its stream) and cpu_baseline (oracle/torch_cpu.py on the host, N=1).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -40,7 +51,7 @@ BF16_PEAK_TFS = 2500.0         # dense bf16 MFMA
 F32_PEAK_TFS = 157.3           # f32 MFMA / vector
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -59,14 +70,35 @@ def parse():
                          "(dvc_corr_lookup_proj) or unfused (lookup, then torch conv3d + relu on the GPU)")
     ap.add_argument("--gather-output", action="store_true", help="strong scaling: all-gather every lookup output")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm); gloo only for rehearsals")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="N>1: weak = one volume pair per rank (global batch N); strong = one pair's query "
-                         "voxels sharded by H slabs")
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="N>1: strong = one pair's query voxels sharded by H slabs (default); weak = one volume "
+                         "pair per rank (global batch N)")
+    ap.add_argument("--graph", dest="graph", action="store_true", default=True,
+                    help="replay each rank's post-collective step as a HIP graph (default)")
+    ap.add_argument("--no-graph", dest="graph", action="store_false")
+    ap.add_argument("--no-extras", action="store_true", help="N>1: skip scaling_detail (T1, gather, weak, cfg #4)")
+    ap.add_argument("--cfg4-steps", type=int, default=3, help="N>1: timed steps of the config #4 extra (0: off)")
+    ap.add_argument("--shard-of", type=int, default=1,
+                    help="diagnostics on one GPU: time rank --shard-rank's slab of an N-way split alone "
+                         "(its per-rank compute; fmap2 is given whole, no collective)")
+    ap.add_argument("--shard-rank", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--tune", default="", help="diagnostics: comma list key=value of dvc_set_tuning knobs")
     ap.add_argument("--cpu-rows", type=int, default=4096, help="query rows of the bounded CPU sample")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def spawn(args) -> int:
+    """`bench.py --gpus N` outside torchrun: launch N ranks with torch.distributed.run as a child process."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"bench.py: spawning {args.gpus} ranks: {' '.join(cmd[1:])}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
 
 
 def lookup_algorithmic_bytes(coords: torch.Tensor, dims, radius: int, store_bytes: int, out_bytes=None) -> float:
@@ -93,11 +125,23 @@ def lookup_algorithmic_bytes(coords: torch.Tensor, dims, radius: int, store_byte
     return float(win.item()) * store_bytes + nq * (out_q + 12.0)
 
 
+def cpu_threads() -> int:
+    """Host threads for the CPU baseline: the job's CPU share where the environment states it
+    (OMP_NUM_THREADS on the GPU box), else every CPU the process may run on."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
 def cpu_baseline(args, f1, f2, coords_list):
-    """oracle/torch_cpu.py (the reference op sequence) on a bounded row sample, host cores."""
+    """oracle/torch_cpu.py (the reference op sequence) on a bounded row sample, host cores; min of 3 runs."""
     sys.path.insert(0, ROOT)
     from oracle import torch_cpu
-    nthreads = min(16, os.cpu_count() or 1)
+    nthreads = cpu_threads()
     torch.set_num_threads(nthreads)
     f1c, f2c = f1.float().cpu(), f2.float().cpu()
     cc = [c.cpu() for c in coords_list]
@@ -107,28 +151,163 @@ def cpu_baseline(args, f1, f2, coords_list):
     q0, q1 = 0, rows
     pyr = torch_cpu.build_rows(f1c, f2c, args.levels, q0, q1)           # warmup (allocations)
     torch_cpu.lookup_rows(pyr, cc[0], args.radius, False, q0, q1)
-    t0 = time.perf_counter()
-    pyr = torch_cpu.build_rows(f1c, f2c, args.levels, q0, q1)
-    t_build = time.perf_counter() - t0
-    nl = 3
-    t0 = time.perf_counter()
-    for i in range(nl):
+    tb, tl = [], []
+    for i in range(3):
+        t0 = time.perf_counter()
+        pyr = torch_cpu.build_rows(f1c, f2c, args.levels, q0, q1)
+        tb.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
         torch_cpu.lookup_rows(pyr, cc[i], args.radius, False, q0, q1)
-    t_lookup = (time.perf_counter() - t0) / nl
+        tl.append(time.perf_counter() - t0)
+    t_build, t_lookup = min(tb), min(tl)
     t_step = t_build + args.iters * t_lookup
     return {
         "value": args.iters * rows / t_step, "unit": "voxel-queries/s", "cores": nthreads, "kind": "port",
-        "sample": (f"oracle/torch_cpu.py (reference op sequence, bit-identical to corr.py), fp32, query rows "
-                   f"[0,{rows}) of {N}: build {t_build * 1e3:.0f} ms + {args.iters} x lookup "
-                   f"{t_lookup * 1e3:.0f} ms (mean of {nl}); rows are independent, rate is per row"),
+        "host_cpus": os.cpu_count(),
+        "sample": (f"oracle/torch_cpu.py (reference op sequence, bit-identical to corr.py), fp32, {nthreads} "
+                   f"threads, query rows [0,{rows}) of {N}: build {t_build * 1e3:.0f} ms + {args.iters} x lookup "
+                   f"{t_lookup * 1e3:.0f} ms (min of 3 runs); rows are independent, rate is per row"),
     }
+
+
+class Runner:
+    """One rank's correlation step: [all-gather of the fmap2 slabs] + pack/build + `iters` lookups.
+
+    The collective runs eagerly on the current stream; everything after it is optionally captured once
+    as a HIP graph (torch.cuda.CUDAGraph over the stream-ordered, allocation-free C ABI) and replayed,
+    which removes the host launch cost of the 15 launches per step when the per-rank work is small."""
+
+    def __init__(self, f1_slab, f2_slab, coords_slabs, H, args, group, world, gather_output=False,
+                 graph=True, proj=None):
+        from dvccorr.sharded import LOCAL
+        self.args, self.group, self.H = args, group, H
+        self.world = 1 if group == LOCAL else world
+        self.gather_output = gather_output and self.world > 1
+        B, C = f1_slab.shape[:2]
+        self.f1_flat = f1_slab.reshape(B, C, -1).contiguous()
+        self.f2_slab = f2_slab.contiguous()
+        self.coords = [c.reshape(B, 3, -1).contiguous() for c in coords_slabs]
+        self.slab_shape = tuple(f1_slab.shape)
+        self.proj = proj
+        self.buf = None
+        if self.world > 1:
+            from dvccorr.sharded import all_gather_slab
+            self.buf = all_gather_slab(self.f2_slab, H, group)      # allocates the static receive buffer
+        self.use_graph = graph and not self.gather_output
+        self.graph = None
+        self.outs = None
+
+    def collective(self):
+        if self.world > 1:
+            from dvccorr.sharded import all_gather_slab
+            all_gather_slab(self.f2_slab, self.H, self.group, buf=self.buf)
+
+    def compute(self, ev=None, stream=None):
+        from dvccorr.sharded import HipRows, assemble_slabs, gather_slabs
+        a = self.args
+        f2 = assemble_slabs(self.buf, self.H) if self.world > 1 else self.f2_slab
+        if ev is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        rows = HipRows(self.f1_flat, f2, a.levels, a.radius, False, a.precision, a.impl)
+        if ev is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record(stream)
+            ev["build"].append((e0, e1))
+        outs = []
+        for c in self.coords:
+            if ev is not None:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            if a.convc1 == "fused":
+                o = rows.lookup_convc1(c, *self.proj)
+            elif a.convc1 == "unfused":
+                o = rows.lookup(c)
+                o = torch.relu(torch.nn.functional.conv1d(o, self.proj[0].view(96, -1, 1), self.proj[1]))
+            else:
+                o = rows.lookup(c)
+            if ev is not None:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record(stream)
+                ev["lookup"].append((e0, e1))
+            if self.gather_output:
+                B = o.shape[0]
+                o = gather_slabs(o.view(B, o.shape[1], -1, *self.slab_shape[3:]), self.H, self.group)
+            outs.append(o)
+        return outs
+
+    def capture(self):
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            self.compute()                         # warm-up outside the capture (library load, attributes)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.outs = self.compute()
+
+    def step(self):
+        self.collective()
+        if self.use_graph:
+            if self.graph is None:
+                self.capture()
+            self.graph.replay()
+        else:
+            self.outs = self.compute()
+
+    def release(self):
+        self.graph = None
+        self.outs = None
+        self.buf = None
+
+
+def timed(runner, steps, warmup, dist, dev, participate=True):
+    """warmup untimed steps, then `steps` timed ones bracketed by barrier + synchronize; max over ranks."""
+    def barrier():
+        if dist:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    with torch.no_grad():
+        if participate:
+            for _ in range(warmup):
+                runner.step()
+        barrier()
+        t0 = time.perf_counter()
+        if participate:
+            for _ in range(steps):
+                runner.step()
+        barrier()
+        elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev if torch.distributed.get_backend() == "nccl" else "cpu")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def gpu_inputs(S, C, iters, max_flow, seed, dev):
+    """Seeded inputs generated on the GPU (identical on every rank of one node)."""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    f1 = torch.randn(1, C, S, S, S, device=dev, generator=g)
+    f2 = torch.randn(1, C, S, S, S, device=dev, generator=g)
+    ax = torch.arange(S, device=dev, dtype=torch.float32)
+    base = torch.stack(torch.meshgrid(ax, ax, ax, indexing="ij"))[None]
+    coords = [base + (torch.rand(1, 3, S, S, S, device=dev, generator=g) * 2 - 1) * max_flow for _ in range(iters)]
+    return f1, f2, coords
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     dist = world > 1
     if os.environ.get("DVCCORR_BENCH_ONE_DEVICE") == "1":   # rehearsal of N ranks on a 1-GPU box
         local = 0
@@ -140,87 +319,67 @@ def main():
             tdist.init_process_group("nccl", device_id=dev)
         else:
             tdist.init_process_group(args.dist_backend)
+        assert tdist.get_world_size() == args.gpus, (tdist.get_world_size(), args.gpus)
     import dvccorr
-    from dvccorr import ops
     from dvccorr import _lib
-    from dvccorr.sharded import LOCAL, ShardedCorrBlock, slab_bounds
+    from dvccorr.sharded import LOCAL, slab_bounds
     for kv in filter(None, args.tune.split(",")):
         k, v = kv.split("=")
         _lib.set_tuning(k, int(v))
 
     S, C, L, R = args.size, args.channels, args.levels, args.radius
     B = 1
-    strong = args.scaling == "strong" and dist
-    # weak scaling: each rank's own pair (seeded by rank); strong: every rank generates the same pair
+    strong = args.scaling == "strong"
+    shard_diag = args.shard_of > 1 and not dist
+    # strong: every rank generates the same pair; weak: each rank its own (seeded by rank)
     g = torch.Generator(device="cpu").manual_seed(1234 + (0 if strong else rank))
     f1 = torch.randn(B, C, S, S, S, generator=g)
     f2 = torch.randn(B, C, S, S, S, generator=g)
     base = dvccorr.coords_grid_3d(B, S, S, S, torch.device("cpu"))
     coords_list = [base + (torch.rand(B, 3, S, S, S, generator=g) * 2 - 1) * args.max_flow
                    for _ in range(args.iters)]
-    h0, h1 = slab_bounds(S, world, rank) if strong else (0, S)
+    if shard_diag:
+        h0, h1 = slab_bounds(S, args.shard_of, args.shard_rank)
+    else:
+        h0, h1 = slab_bounds(S, world, rank) if (strong and dist) else (0, S)
     f1_slab = f1[:, :, h0:h1].contiguous().to(dev)
-    f2_slab = f2[:, :, h0:h1].contiguous().to(dev)
+    f2_slab = (f2 if shard_diag else f2[:, :, h0:h1]).contiguous().to(dev)
     coords_slab = [c[:, :, h0:h1].contiguous().to(dev) for c in coords_list]
     nq_local = (h1 - h0) * S * S
-    nq_total = S * S * S * (1 if strong else world)   # query voxels of the whole job
+    nq_total = S * S * S * (1 if strong else world) if not shard_diag else nq_local
     lay = dvccorr.layout(S, S, S, L, C)
     dims = lay.levels()
     store_bytes = 2 if args.precision == "bf16" else 4
     stream = torch.cuda.current_stream(dev)
-    group = None
+    group = None if (strong and dist) else LOCAL
 
-    ev = {"lookup": [], "build": []}
-    proj_w = proj_b = None
+    proj = None
     if args.convc1:   # random-init convc1 (Conv3d(L (2r+1)^3, 96, 1) default init range, update.py:222)
         K = L * (2 * R + 1) ** 3
-        proj_w = ((torch.rand(96, K, generator=g) * 2 - 1) / K ** 0.5).to(dev)
-        proj_b = ((torch.rand(96, generator=g) * 2 - 1) / K ** 0.5).to(dev)
+        proj = (((torch.rand(96, K, generator=g) * 2 - 1) / K ** 0.5).to(dev),
+                ((torch.rand(96, generator=g) * 2 - 1) / K ** 0.5).to(dev))
 
-    def step(timed: bool):
-        blk = ShardedCorrBlock(f1_slab, f2_slab, S, L, R, precision=args.precision, impl=args.impl,
-                               group=group if strong else LOCAL, gather_output=args.gather_output,
-                               build_events=ev["build"] if timed else None)
-        for i in range(args.iters):
-            if timed:
-                e0 = torch.cuda.Event(enable_timing=True)
-                e1 = torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-            if args.convc1 == "fused":
-                blk.lookup_convc1(coords_slab[i], proj_w, proj_b)
-            elif args.convc1 == "unfused":
-                torch.relu(torch.nn.functional.conv3d(blk(coords_slab[i]), proj_w.view(96, -1, 1, 1, 1), proj_b))
-            else:
-                blk(coords_slab[i])
-            if timed:
-                e1.record(stream)
-                ev["lookup"].append((e0, e1))
+    runner = Runner(f1_slab, f2_slab, coords_slab, S, args, group, world, gather_output=args.gather_output,
+                    graph=args.graph, proj=proj)
+    elapsed = timed(runner, args.steps, args.warmup, dist, dev)
+    runner.release()
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = args.iters * nq_total * args.steps / elapsed
 
-    def barrier():
-        if dist:
-            torch.distributed.barrier()
-        torch.cuda.synchronize()
-
+    # per-kernel HIP-event timing on the launch stream: eager steps after the timed region
+    ev = {"lookup": [], "build": []}
     with torch.no_grad():
-        for _ in range(args.warmup):
-            step(False)
-        barrier()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step(True)
-        barrier()
-        elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], device=dev if args.dist_backend == "nccl" else "cpu")
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
-
+        er = Runner(f1_slab, f2_slab, coords_slab, S, args, group, world, graph=False, proj=proj)
+        for k in range(4):
+            er.collective()
+            er.compute(ev if k > 0 else None, stream)
+        torch.cuda.synchronize()
+        er.release()
+        del er
     lk_ms = [a.elapsed_time(b) for a, b in ev["lookup"]]
     bd_ms = [a.elapsed_time(b) for a, b in ev["build"]]
     lk_avg = sum(lk_ms) / max(len(lk_ms), 1)
     bd_avg = sum(bd_ms) / max(len(bd_ms), 1)
-    ms_per_step = elapsed * 1e3 / args.steps
-    value = args.iters * nq_total * args.steps / elapsed
 
     # roofline of the dominant kernel (by time per step, rank 0's view)
     lk_bytes = sum(lookup_algorithmic_bytes(c, dims, R, store_bytes if args.impl == "materialised" else 0,
@@ -243,11 +402,12 @@ def main():
             traffic = tf.get(key, {}).get("lookup_hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    lk_roof = lk_bytes / (lk_avg * 1e-3) / 1e9 if lk_avg else 0.0
     if args.iters * lk_avg >= bd_avg or args.impl == "fused":
-        achieved = lk_bytes / (lk_avg * 1e-3) / 1e9
+        achieved = lk_roof
         if args.impl == "materialised":
             kname = {"fused": "k_lookup_tile<PROJ> (dvc_corr_lookup_proj, convc1 fused)",
-                     "unfused": "k_lookup_tile (dvc_corr_lookup) + torch conv3d/relu (timed together)"}.get(
+                     "unfused": "k_lookup_tile (dvc_corr_lookup) + torch conv/relu (timed together)"}.get(
                          args.convc1, "k_lookup_tile (dvc_corr_lookup)")
         elif args.precision == "bf16" and 1 <= R <= 4:
             kname = "k_fused_box (dvc_corr_lookup_fused)"
@@ -267,16 +427,58 @@ def main():
         achieved = bd_bytes / (bd_avg * 1e-3) / 1e9
         roof = {"kernel": "build (pack + k_build_bf16/f32)", "bound": "hbm", "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "algorithmic_bytes_per_launch": bd_bytes, "avg_launch_ms": round(bd_avg, 4)}
+                "algorithmic_bytes_per_launch": bd_bytes, "avg_launch_ms": round(bd_avg, 4),
+                "lookup": {"achieved": round(lk_roof, 1), "frac": round(lk_roof / HBM_PEAK_GBS, 4),
+                           "algorithmic_bytes_per_launch": lk_bytes, "avg_launch_ms": round(lk_avg, 4)}}
     build_info = {"avg_ms": round(bd_avg, 4), "GB/s": round(bd_bytes / (bd_avg * 1e-3) / 1e9, 1) if bd_avg else None,
                   "TFLOP/s": round(bd_flops / (bd_avg * 1e-3) / 1e12, 1) if bd_avg and bd_flops else None}
 
-    # per-iteration tail (raft_dvc.py:482-485), outside the timed region:
-    # coords1 += delta_flow; flow_up = upflow_3d(coords1 - coords0) to the input size, one k_upflow pass
-    tail = None
+    tail = flow_tail(args, coords_slab, S, B, dev, stream, _lib, dvccorr)
+
+    detail = None
+    if dist and strong and not args.no_extras:
+        detail = scaling_detail(args, f1, f2, coords_list, ms_per_step, world, rank, dev, dist, group, proj)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not shard_diag:
+        cpu = cpu_baseline(args, f1, f2, coords_list)
+
+    if rank == 0:
+        par = (f"query-voxel H-slabs x{world}, RCCL all-gather of fmap2 per step" if (strong and dist) else
+               f"one volume pair per rank x{world} (no data-path collective)" if dist else "single GPU")
+        if shard_diag:
+            par = f"diagnostic: rank {args.shard_rank}'s slab of a {args.shard_of}-way split alone (no collective)"
+        line = {
+            "metric": f"corr build+lookup voxel-queries/s ({args.encoder * S}^3 pair, 1/{args.encoder} encoder)",
+            "value": value, "unit": "voxel-queries/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+            "scaling": "strong" if strong else "weak", "vs_baseline": None,
+            "dtype": "bf16" if args.precision == "bf16" else "f32",
+            "data": "synthetic: N(0,1) feature maps, coords = identity + U(-2,2), 12 coord fields per step",
+            "config": {"workload": f"corr build + {args.iters} lookups{f' + convc1 ({args.convc1})' if args.convc1 else ''}, {S}^3 x {C} fmaps ({args.encoder * S}^3 "
+                                   f"input, 1/{args.encoder} encoder), L={L}, r={R}, {args.impl}, {args.precision} build / fp32 lookup",
+                       "global_batch": B if strong else B * world, "query_voxels": nq_total, "levels": L,
+                       "radius": R, "parallelism": par + (", output all-gather" if args.gather_output else ""),
+                       "step_replay": "hip graph after the collective" if runner.use_graph else "eager"},
+            "roofline": roof,
+            "build": build_info,
+            "lookup_avg_ms": round(lk_avg, 4),
+            "flow_step": tail,
+            "cpu_baseline": cpu,
+        }
+        if detail is not None:
+            line["scaling_detail"] = detail
+        print(json.dumps(line), flush=True)
+    if dist:
+        torch.distributed.destroy_process_group()
+
+
+def flow_tail(args, coords_slab, S, B, dev, stream, _lib, dvccorr):
+    """Per-iteration tail (raft_dvc.py:482-485), outside the timed region:
+    coords1 += delta_flow; flow_up = upflow_3d(coords1 - coords0) to the input size, one k_upflow pass."""
     with torch.no_grad():
         T = args.encoder * S
-        c1 = coords_slab[0][:, :, :].reshape(B, 3, -1, S, S)
+        c1 = coords_slab[0].reshape(B, 3, -1, S, S)
         dfl = (coords_slab[-1] - coords_slab[0]).reshape(c1.shape)
         h_lo = c1.shape[2]
         for _ in range(3):
@@ -294,39 +496,73 @@ def main():
         tail_ms = a.elapsed_time(b) / 20
         lo_b = 3 * 4 * c1[0, 0].numel() * B
         tail_bytes = 3 * lo_b + lo_b * args.encoder ** 3      # read coords1 + delta, write coords1; write flow_up
-        tail = {"kernel": "k_upflow<DELTA,SUBGRID> (dvc_flow_step)", "avg_ms": round(tail_ms, 4),
-                "algorithmic_bytes": tail_bytes,
-                "GB/s": round(tail_bytes / (tail_ms * 1e-3) / 1e9, 1)}
+        return {"kernel": "k_upflow<DELTA,SUBGRID> (dvc_flow_step)", "avg_ms": round(tail_ms, 4),
+                "algorithmic_bytes": tail_bytes, "GB/s": round(tail_bytes / (tail_ms * 1e-3) / 1e9, 1)}
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, f1, f2, coords_list)
 
-    if rank == 0:
-        line = {
-            "metric": f"corr build+lookup voxel-queries/s ({args.encoder * S}^3 pair, 1/{args.encoder} encoder)",
-            "value": value, "unit": "voxel-queries/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-            "scaling": "strong" if strong else "weak", "vs_baseline": None,
-            "dtype": "bf16" if args.precision == "bf16" else "f32",
-            "data": "synthetic: N(0,1) feature maps, coords = identity + U(-2,2), 12 coord fields per step",
-            "config": {"workload": f"corr build + {args.iters} lookups{f' + convc1 ({args.convc1})' if args.convc1 else ''}, {S}^3 x {C} fmaps ({args.encoder * S}^3 "
-                                   f"input, 1/{args.encoder} encoder), L={L}, r={R}, {args.impl}, {args.precision} build / fp32 lookup",
-                       "global_batch": B if strong else B * world, "query_voxels": nq_total, "levels": L,
-                       "radius": R,
-                       "parallelism": (f"query-voxel H-slabs x{world}" if strong else
-                                       f"one volume pair per rank x{world} (no data-path collective)") +
-                                      (", output all-gather" if
-                                                                          args.gather_output else "")},
-            "roofline": roof,
-            "build": build_info,
-            "lookup_avg_ms": round(lk_avg, 4),
-            "flow_step": tail,
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(line), flush=True)
-    if dist:
-        torch.distributed.destroy_process_group()
+def scaling_detail(args, f1, f2, coords_list, ms_strong, world, rank, dev, dist, group, proj):
+    """N>1, measured in the same job: T1 (rank 0 alone, whole problem), strong with the output all-gather,
+    weak (one pair per rank) and config #4 (64^3 fmaps) strong-scaled; E(n) = T1 / (n Tn)."""
+    from dvccorr.sharded import LOCAL, slab_bounds
+    S = args.size
+    steps, warm = args.steps, max(1, args.warmup)
+    out = {"note": "E = T1 / (n * Tn); T1 = rank 0 alone on the whole problem, same job, same kernels"}
+    # T1: rank 0 runs the unsharded step, the other ranks wait at the barriers
+    full = [c.to(dev) for c in coords_list] if rank == 0 else None
+    r1 = Runner(f1.to(dev), f2.to(dev), full, S, args, LOCAL, world, graph=args.graph, proj=proj) \
+        if rank == 0 else None
+    t1 = timed(r1, steps, warm, dist, dev, participate=rank == 0) * 1e3 / steps
+    if r1 is not None:
+        r1.release()
+    del r1
+    torch.cuda.empty_cache()
+    out["cfg3_t1_ms"] = round(t1, 4)
+    out["cfg3_strong_resident"] = {"ms_per_step": round(ms_strong, 4), "E": round(t1 / (world * ms_strong), 4)}
+    h0, h1 = slab_bounds(S, world, rank)
+    f1s, f2s = f1[:, :, h0:h1].contiguous().to(dev), f2[:, :, h0:h1].contiguous().to(dev)
+    cs = [c[:, :, h0:h1].contiguous().to(dev) for c in coords_list]
+    rg = Runner(f1s, f2s, cs, S, args, group, world, gather_output=True, graph=False, proj=proj)
+    tg = timed(rg, steps, warm, dist, dev) * 1e3 / steps
+    rg.release()
+    out["cfg3_strong_gather_output"] = {"ms_per_step": round(tg, 4), "E": round(t1 / (world * tg), 4)}
+    # weak: every rank its own whole pair (the same pair here; no collective)
+    rw = Runner(f1.to(dev), f2.to(dev), [c.to(dev) for c in coords_list], S, args, LOCAL, world, graph=args.graph,
+                proj=proj)
+    tw = timed(rw, steps, warm, dist, dev) * 1e3 / steps
+    rw.release()
+    del rw
+    torch.cuda.empty_cache()
+    out["cfg3_weak"] = {"ms_per_step": round(tw, 4), "E": round(t1 / tw, 4),
+                        "value": round(args.iters * S ** 3 * world / (tw * 1e-3), 1)}
+    if args.cfg4_steps > 0 and args.impl == "materialised" and args.convc1 is None:
+        out["cfg4"] = cfg4_strong(args, world, rank, dev, dist, group)
+    return out
+
+
+def cfg4_strong(args, world, rank, dev, dist, group):
+    """Config #4 (256^3 input, 1/4 encoder: 64^3 x 128 fmaps, L=4, r=4, bf16): T1 on rank 0 alone (157 GB
+    pyramid) and the H-slab layout on every rank (157/n GB each)."""
+    from dvccorr.sharded import LOCAL, slab_bounds
+    S, steps = 64, args.cfg4_steps
+    a4 = parse([f"--size={S}", f"--channels={args.channels}", f"--levels={args.levels}", f"--radius={args.radius}",
+                f"--iters={args.iters}", f"--precision={args.precision}"])
+    f1, f2, coords = gpu_inputs(S, args.channels, args.iters, args.max_flow, 4004, dev)
+    r1 = Runner(f1, f2, coords, S, a4, LOCAL, world, graph=False) if rank == 0 else None
+    t1 = timed(r1, steps, 1, dist, dev, participate=rank == 0) * 1e3 / steps
+    if r1 is not None:
+        r1.release()
+    del r1
+    torch.cuda.empty_cache()
+    h0, h1 = slab_bounds(S, world, rank)
+    rn = Runner(f1[:, :, h0:h1].contiguous(), f2[:, :, h0:h1].contiguous(),
+                [c[:, :, h0:h1].contiguous() for c in coords], S, a4, group, world, graph=args.graph)
+    tn = timed(rn, steps, 1, dist, dev) * 1e3 / steps
+    rn.release()
+    del rn
+    torch.cuda.empty_cache()
+    return {"workload": "64^3 x 128 fmaps (256^3 input, 1/4 encoder), L=4, r=4, bf16, build + 12 lookups",
+            "t1_ms": round(t1, 3), "tn_ms": round(tn, 3), "E": round(t1 / (world * tn), 4),
+            "value": round(args.iters * S ** 3 / (tn * 1e-3), 1), "steps": steps}
 
 
 if __name__ == "__main__":

@@ -147,11 +147,11 @@ int dvc_corr_backward(const void *packed_q, const void *packed_t, const float *c
 /* Lookup with the motion encoder's convc1 (1x1x1 Conv3d L*(2r+1)^3 -> 96, + ReLU,
  * update.py:222, 246) fused into its epilogue: the L*(2r+1)^3-channel lookup output
  * never reaches HBM.
- *   dvc_proj_pack: convc1.weight viewed (96, L*(2r+1)^3) float32 -> packed bf16
+ *   dvc_proj_pack: convc1.weight viewed (96, L*(2r+1)^3) float32 -> packed fp16
  *     weights (dvc_proj_packed_bytes) in the kernel's MFMA operand order for one
  *     (num_levels, radius, convention); pack once per weight update.
  *   dvc_corr_lookup_proj: out (B, 96, Nq) float32 = relu(W . lookup(coords) + bias),
- *     bias (96) float32.  The lookup values and the weights enter bf16 MFMA with
+ *     bias (96) float32.  The lookup values and the weights enter fp16 MFMA with
  *     float32 accumulation (tolerance 1e-2 max-normalised against the float32
  *     reference).  Supported: radius 1..4, tile-kernel row widths, and for the legacy
  *     convention W == D at every non-zero level (DVC_ERR_UNSUPPORTED otherwise). */

@@ -30,7 +30,7 @@ template <typename T>
 __global__ void k_corr_pool(T *, long long, long long, long long, int, int, long long, int, int, int, int);
 template <typename T, int R, bool WINBUF, bool ALIGNED> __global__ void k_lookup_win(LookupArgs);
 template <typename T> __global__ void k_lookup_generic(LookupArgs);
-template <typename T, int R, bool NT, int ABL, bool PROJ> __global__ void k_lookup_tile(LookupArgs);
+template <typename T, int R, bool NT, int ABL, bool PROJ, int ACH> __global__ void k_lookup_tile(LookupArgs);
 __global__ void k_proj_pack(const float *, bf16_t *, int, int, int, long long);
 __global__ void k_sample3d(const float *, const float *, float *, int, int, int, int, int, long long, int);
 int fused_lookup(const void *packed_q, const void *packed_t, const float *coords, float *out, void *workspace, int B,
@@ -127,32 +127,46 @@ static bool tile_ok(const LookupArgs &A, size_t esz) {
 }
 
 // Fewer query tiles than 2 x the 256 CUs (e.g. one rank's 4096-row slab at config #3: 64 tiles) leave most
-// of the chip idle; then each workgroup takes one (tile, level) pair instead of a tile's whole level loop.
-static constexpr long long kSplitTiles = 512;
+// of the chip idle; then each workgroup takes one (tile, level) pair instead of a tile's whole level loop,
+// and if that is still short of 4 workgroups per CU, one (tile, level, 3-row chunk) triple (ACH = 3:
+// each chunk reads 4 of the 2r+2 window planes).
+static constexpr long long kSplitTiles = 512, kSplitRows = 1024;
+
+template <typename T, bool NT, int ACH>
+static void launch_tile_r(const LookupArgs &A, dim3 blocks, unsigned threads, hipStream_t s) {
+    switch (A.r) {
+    case 1: k_lookup_tile<T, 1, NT, 0, false, ACH><<<blocks, threads, 0, s>>>(A); break;
+    case 2: k_lookup_tile<T, 2, NT, 0, false, ACH><<<blocks, threads, 0, s>>>(A); break;
+    case 3: k_lookup_tile<T, 3, NT, 0, false, ACH><<<blocks, threads, 0, s>>>(A); break;
+    case 4: k_lookup_tile<T, 4, NT, 0, false, ACH><<<blocks, threads, 0, s>>>(A); break;
+    case 5: k_lookup_tile<T, 5, NT, 0, false, ACH><<<blocks, threads, 0, s>>>(A); break;
+    case 6: k_lookup_tile<T, 6, NT, 0, false, ACH><<<blocks, threads, 0, s>>>(A); break;
+    default: break;
+    }
+}
 
 template <typename T, bool NT>
 static void launch_tile_nt(const LookupArgs &A0, hipStream_t s) {
     LookupArgs A = A0;
-    A.split_levels = (long long)A.B * A.nqb < kSplitTiles && A.nl > 1;
-    const dim3 blocks((unsigned)(A.B * A.nqb), A.split_levels ? (unsigned)A.nl : 1u);
+    const long long tiles = (long long)A.B * A.nqb;
+    A.split_levels = tiles < kSplitTiles && A.nl > 1;
+    const int n = 2 * A.r + 1;
+    const bool split_rows = NT && tiles * (A.split_levels ? A.nl : 1) < kSplitRows && n > 3;
+    const dim3 blocks((unsigned)tiles, A.split_levels ? (unsigned)A.nl : 1u, split_rows ? (unsigned)((n + 2) / 3) : 1u);
     const unsigned threads = 64u * (unsigned)((2 * A.r + 3) / 3);
     if constexpr (std::is_same<T, bf16_t>::value && NT) {
         if (A.r == 4 && A.ablate >= 1 && A.ablate <= 3) {   // diagnostics only
-            if (A.ablate == 1) k_lookup_tile<T, 4, NT, 1, false><<<blocks, threads, 0, s>>>(A);
-            else if (A.ablate == 2) k_lookup_tile<T, 4, NT, 2, false><<<blocks, threads, 0, s>>>(A);
-            else k_lookup_tile<T, 4, NT, 3, false><<<blocks, threads, 0, s>>>(A);
+            const dim3 b1((unsigned)tiles, blocks.y);
+            if (A.ablate == 1) k_lookup_tile<T, 4, NT, 1, false, 0><<<b1, threads, 0, s>>>(A);
+            else if (A.ablate == 2) k_lookup_tile<T, 4, NT, 2, false, 0><<<b1, threads, 0, s>>>(A);
+            else k_lookup_tile<T, 4, NT, 3, false, 0><<<b1, threads, 0, s>>>(A);
             return;
         }
     }
-    switch (A.r) {
-    case 1: k_lookup_tile<T, 1, NT, 0, false><<<blocks, threads, 0, s>>>(A); break;
-    case 2: k_lookup_tile<T, 2, NT, 0, false><<<blocks, threads, 0, s>>>(A); break;
-    case 3: k_lookup_tile<T, 3, NT, 0, false><<<blocks, threads, 0, s>>>(A); break;
-    case 4: k_lookup_tile<T, 4, NT, 0, false><<<blocks, threads, 0, s>>>(A); break;
-    case 5: k_lookup_tile<T, 5, NT, 0, false><<<blocks, threads, 0, s>>>(A); break;
-    case 6: k_lookup_tile<T, 6, NT, 0, false><<<blocks, threads, 0, s>>>(A); break;
-    default: break;
+    if constexpr (NT) {
+        if (split_rows) { launch_tile_r<T, NT, 3>(A, blocks, threads, s); return; }
     }
+    launch_tile_r<T, NT, 0>(A, blocks, threads, s);
 }
 
 template <typename T, bool AL>
@@ -363,7 +377,13 @@ int dvc_corr_build(const void *packed_q, const void *packed_t, void *corr, int B
     const float scale = 1.0f / sqrtf((float)C);   // corr / sqrt(C) (corr.py:165)
     hipStream_t s = (hipStream_t)stream;
     const long long ncol_tiles = ceil_div(col_end - col_begin, 128);
-    const int nchunk = (int)std::min<long long>(8, ncol_tiles);
+    // column chunks per query tile: 8 (one per XCD: blocks b, b + 8, ... share an XCD and stream the same
+    // eighth of the targets through its L2), doubled while the grid is short of 4 workgroups per CU (one
+    // rank's slab: 32 query tiles at config #3 / 8 GPUs) and every chunk keeps >= 2 column tiles
+    const long long qtiles = ceil_div(Nq, in_dtype == DVC_BF16 ? 128 : 64) * B;
+    long long nch = 8;
+    while (qtiles * nch < 1024 && nch * 4 <= ncol_tiles && nch < 64) nch *= 2;
+    const int nchunk = (int)std::min<long long>(nch, ncol_tiles);
     if (in_dtype == DVC_BF16) {
         if (store_dtype != DVC_BF16 && store_dtype != DVC_F32) return fail(DVC_ERR_INVALID, "build: bad store dtype");
         const size_t lds = (size_t)128 * Cp * 2 + std::max<size_t>((size_t)128 * Cp * 2, 32768);
@@ -536,10 +556,10 @@ int dvc_corr_lookup_proj(const void *corr, const float *coords, const void *pack
     hipStream_t s = (hipStream_t)stream;
 #define DVC_PROJ_LAUNCH(T)                                                                   \
     switch (radius) {                                                                        \
-    case 1: k_lookup_tile<T, 1, true, 0, true><<<blocks, threads, 0, s>>>(A); break;        \
-    case 2: k_lookup_tile<T, 2, true, 0, true><<<blocks, threads, 0, s>>>(A); break;        \
-    case 3: k_lookup_tile<T, 3, true, 0, true><<<blocks, threads, 0, s>>>(A); break;        \
-    default: k_lookup_tile<T, 4, true, 0, true><<<blocks, threads, 0, s>>>(A); break;       \
+    case 1: k_lookup_tile<T, 1, true, 0, true, 0><<<blocks, threads, 0, s>>>(A); break;        \
+    case 2: k_lookup_tile<T, 2, true, 0, true, 0><<<blocks, threads, 0, s>>>(A); break;        \
+    case 3: k_lookup_tile<T, 3, true, 0, true, 0><<<blocks, threads, 0, s>>>(A); break;        \
+    default: k_lookup_tile<T, 4, true, 0, true, 0><<<blocks, threads, 0, s>>>(A); break;       \
     }
     if (store_dtype == DVC_BF16) { DVC_PROJ_LAUNCH(bf16_t) }
     else { DVC_PROJ_LAUNCH(float) }

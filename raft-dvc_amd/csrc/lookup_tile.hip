@@ -87,16 +87,18 @@ template <int n> struct ZRun {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 // convc1 fusion (PROJ): the motion encoder's first layer, relu(conv1x1(corr, W) + b)
 // with 96 output channels (reference src/core/update.py:219-222, 246), applied to the
 // lookup's L*(2r+1)^3 channels without writing them to HBM.
 //   * the NWAVES lookup waves (producers) write each output row a (their (2r+1) x 3
-//     values per query) as bf16 into a [64 query][NWAVES x 32 k] LDS tile X instead of
+//     values per query) as fp16 into a [64 query][NWAVES x 32 k] LDS tile X instead of
 //     storing them; within a wave's 32-k slice, k = 2 (uu NP + i) + {0, 1} holds the
 //     pair (column uu, v = 2i, 2i + 1) and k = 2 NU NP + uu the tail v = n - 1.
 //   * one extra wave (consumer) multiplies X by the row's 96 x (NWAVES x 32) weight
-//     block on v_mfma_f32_16x16x32_bf16 (A = weights, 16 output channels; B = X, 16
+//     block on v_mfma_f32_16x16x32_f16 (A = weights, 16 output channels; B = X, 16
 //     queries), accumulating D[96][64] over every row of every level in 96 VGPRs, and
 //     stores relu(D + b) once per tile.  The weights are pre-permuted into that k order
 //     and the MFMA A-operand lane layout (dvc_proj_pack), so any sampler convention is
@@ -108,7 +110,9 @@ struct ProjCfg {
 };
 
 // ABL (diagnostics only, never the product path): 1 = skip output stores, 2 = skip loads.
-template <typename T, int R, bool NT, int ABL, bool PROJ>
+// ACH > 0: row split -- the workgroup computes output rows [ACH * blockIdx.z, + ACH) of its level only
+// (ACH + 1 window planes), for launches whose (tile, level) pairs alone cannot fill the chip.
+template <typename T, int R, bool NT, int ABL, bool PROJ, int ACH>
 __global__ __launch_bounds__(64 * ((2 * R + 3) / 3 + (PROJ ? 1 : 0)), 2) void k_lookup_tile(LookupArgs A) {
     using C = TileCfg<T, R>;
     constexpr int n = C::n, NW = C::NW, ES = C::ES, CE = C::CE, NP = n / 2;
@@ -141,7 +145,7 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3 + (PROJ ? 1 : 0)), 2) void k_
             for (int ot = 0; ot < OT; ++ot)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) acc[ot][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-            const bf16x8 *wp = reinterpret_cast<const bf16x8 *>(A.proj_w) + lane;
+            const f16x8 *wp = reinterpret_cast<const f16x8 *>(A.proj_w) + lane;
             for (int li = 0; li < A.nl; ++li) {
                 const int l = A.l0 + (rev ? A.nl - 1 - li : li);
                 if (A.zero[l] || A.generic[l]) continue;   // (the producers skip the same levels)
@@ -150,9 +154,9 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3 + (PROJ ? 1 : 0)), 2) void k_
                 __syncthreads();
                 __syncthreads();   // planes 0 and 1 staged
                 for (int a = 0; a < n; ++a) {
-                    // this row's weight block, [wave slice ks][16-channel tile ot][lane] x 8 bf16
-                    const bf16x8 *wr = wp + (long long)(l * n + a) * NWV * OT * 64;
-                    bf16x8 wa[NWV][OT];
+                    // this row's weight block, [wave slice ks][16-channel tile ot][lane] x 8 fp16
+                    const f16x8 *wr = wp + (long long)(l * n + a) * NWV * OT * 64;
+                    f16x8 wa[NWV][OT];
 #pragma unroll
                     for (int ks = 0; ks < NWV; ++ks)
 #pragma unroll
@@ -161,15 +165,15 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3 + (PROJ ? 1 : 0)), 2) void k_
                     __syncthreads();   // row a complete in X
 #pragma unroll
                     for (int ks = 0; ks < NWV; ++ks) {
-                        bf16x8 xb[4];
+                        f16x8 xb[4];
 #pragma unroll
                         for (int j = 0; j < 4; ++j)
-                            xb[j] = *reinterpret_cast<const bf16x8 *>(xs + (16 * j + m16) * XROW + ks * 64 + h4 * 16);
+                            xb[j] = *reinterpret_cast<const f16x8 *>(xs + (16 * j + m16) * XROW + ks * 64 + h4 * 16);
 #pragma unroll
                         for (int ot = 0; ot < OT; ++ot)
 #pragma unroll
                             for (int j = 0; j < 4; ++j)
-                                acc[ot][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[ks][ot], xb[j], acc[ot][j], 0,
+                                acc[ot][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[ks][ot], xb[j], acc[ot][j], 0,
                                                                                      0, 0);
                     }
                 }
@@ -226,12 +230,15 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3 + (PROJ ? 1 : 0)), 2) void k_
                                                    NT ? 2 : 0);
     };
 
-    auto level = [&](int l, auto nu_c) {
+    static_assert(!PROJ || ACH == 0, "the convc1 consumer accumulates every row of the tile");
+    // output rows [a0, a0 + NA) of level l; planes a0 .. a0 + NA of the window
+    auto level = [&](int l, auto nu_c, auto na_c, int a0) {
         constexpr int NU = decltype(nu_c)::value;
+        constexpr int NA = decltype(na_c)::value;
         float *obase = A.out + ((long long)b * A.Ltot + l) * n3 * Nq;   // wave-uniform
         if (A.zero[l]) {
             if constexpr (PROJ) return;   // zero outputs add nothing to convc1
-            for (int a = 0; a < n; ++a)
+            for (int a = a0; a < a0 + NA; ++a)
 #pragma unroll
                 for (int uu = 0; uu < NU; ++uu) {
                     const __amdgpu_buffer_rsrc_t rs = out_rsrc(obase, a, u0 + uu);
@@ -354,21 +361,24 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3 + (PROJ ? 1 : 0)), 2) void k_
             z.t = __builtin_fmaf(r[n], wv1[n - 1], r[n - 1] * wv0[n - 1]);
         };
 
-        // staged planes: plane p + 2 is loaded into st[p & 1] two rows before it is written
+        // staged planes (relative index p = plane - a0): plane p + 2 is loaded into st[p & 1]
+        // two rows before it is written
+        constexpr int NPL = NA + 1;   // window planes this workgroup reads
         u32x4 st[2][C::MAXCH];
         ZRun<n> zp[NU + 1];       // z-lerped columns of the lower plane of the current row
-        load_plane(0, st[0]);
-        load_plane(1, st[1]);
-        write_plane(0, 0, st[0]);
-        load_plane(2, st[0]);
-        __syncthreads();          // plane 0 in slot 0
+        load_plane(a0, st[0]);
+        load_plane(a0 + 1, st[1]);
+        write_plane(0, a0, st[0]);
+        if (2 < NPL) load_plane(a0 + 2, st[0]);
+        __syncthreads();          // plane a0 in slot 0
 #pragma unroll
         for (int k = 0; k <= NU; ++k) lerp_col(0, k, zp[k]);
-        write_plane(1, 1, st[1]);
-        __syncthreads();          // plane 1 in slot 1
+        write_plane(1, a0 + 1, st[1]);
+        __syncthreads();          // plane a0 + 1 in slot 1
 #pragma unroll
-        for (int a = 0; a < n; ++a) {
-            if (a + 3 < NW) load_plane(a + 3, st[(a + 1) & 1]);   // in flight for two rows
+        for (int ia = 0; ia < NA; ++ia) {
+            const int a = a0 + ia;
+            if (ia + 3 < NPL) load_plane(a + 3, st[(ia + 1) & 1]);   // in flight for two rows
             float wy0, wy1;
             axis_weights(ax.ph, ax.kh, a - R, ax.hs, ax.hs, wy0, wy1);
             wy0 = (unsigned)(ih + a) < (unsigned)Hl ? wy0 : 0.0f;
@@ -376,12 +386,12 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3 + (PROJ ? 1 : 0)), 2) void k_
             // column by column: once window column k of plane a+1 is lerped, output
             // column k-1 is complete and plane a's column k-1 retires
             ZRun<n> zprev;
-            unsigned xr[NU * NP];   // PROJ: this row's value pairs as bf16x2
+            unsigned xr[NU * NP];   // PROJ: this row's value pairs as f16x2
             float xt[NU];           // PROJ: tails (v = n - 1)
 #pragma unroll
             for (int k = 0; k <= NU; ++k) {
                 ZRun<n> zcur;
-                lerp_col((a + 1) & 1, k, zcur);
+                lerp_col((ia + 1) & 1, k, zcur);
                 if (k >= 1) {
                     const int uu = k - 1;
                     const float p00 = wx0[uu] * wy0, p10 = wx1[uu] * wy0;
@@ -395,7 +405,7 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3 + (PROJ ? 1 : 0)), 2) void k_
                         acc = __builtin_elementwise_fma(P01, zprev.p[i], acc);
                         acc = __builtin_elementwise_fma(P11, zcur.p[i], acc);
                         if constexpr (PROJ) {
-                            xr[uu * NP + i] = __builtin_bit_cast(unsigned, __builtin_convertvector(acc, bf16x2));
+                            xr[uu * NP + i] = __builtin_bit_cast(unsigned, __builtin_convertvector(acc, f16x2));
                         } else {
                             store(rs, 2 * i, acc[0]);
                             store(rs, 2 * i + 1, acc[1]);
@@ -421,7 +431,7 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3 + (PROJ ? 1 : 0)), 2) void k_
 #pragma unroll
                 for (int p = 0; 2 * p < NU; ++p) {
                     const f32x2 t2 = {xt[2 * p], 2 * p + 1 < NU ? xt[2 * p + 1 < NU ? 2 * p + 1 : 0] : 0.0f};
-                    xw[T0 + p] = __builtin_bit_cast(unsigned, __builtin_convertvector(t2, bf16x2));
+                    xw[T0 + p] = __builtin_bit_cast(unsigned, __builtin_convertvector(t2, f16x2));
                 }
                 __syncthreads();   // the consumer has read the previous row of X
                 u32x4 *dst = reinterpret_cast<u32x4 *>(xs + lane * XROW + wave * (ProjCfg::KW * 2));
@@ -429,7 +439,7 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3 + (PROJ ? 1 : 0)), 2) void k_
                 for (int j = 0; j < ProjCfg::KW / 8; ++j)
                     dst[j] = u32x4{xw[4 * j], xw[4 * j + 1], xw[4 * j + 2], xw[4 * j + 3]};
             }
-            if (a + 2 < NW) write_plane(a & 1, a + 2, st[a & 1]);   // plane a+2 into the slot of plane a (read in row a-1)
+            if (ia + 2 < NPL) write_plane(ia & 1, a + 2, st[ia & 1]);   // plane a+2 into the slot of plane a (read in row a-1)
             __syncthreads();
         }
     };
@@ -438,31 +448,40 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3 + (PROJ ? 1 : 0)), 2) void k_
     // gather-heavy fine levels with the store-heavy coarse ones
     const int li0 = A.split_levels ? (int)blockIdx.y : 0;
     const int li1 = A.split_levels ? li0 + 1 : A.nl;
+    constexpr int NCH_A = ACH > 0 ? (n + ACH - 1) / ACH : 1;       // row chunks
+    constexpr int NA_FULL = ACH > 0 ? ACH : n;
+    constexpr int NA_TAIL = ACH > 0 ? n - ACH * (NCH_A - 1) : n;    // rows of the last chunk
+    const int a0 = ACH > 0 ? (int)blockIdx.z * ACH : 0;
+    auto rows = [&](int l, auto nu_c) {
+        if (NA_TAIL == NA_FULL || a0 + NA_FULL <= n) level(l, nu_c, std::integral_constant<int, NA_FULL>{}, a0);
+        else level(l, nu_c, std::integral_constant<int, NA_TAIL>{}, a0);
+    };
     for (int li = li0; li < li1; ++li) {
         const int l = A.l0 + (rev ? A.nl - 1 - li : li);
         if (A.generic[l] && !A.zero[l]) continue;   // legacy level with W != D: k_lookup_generic
-        if (NU_LAST == C::COLS || wave < C::NWAVES - 1) level(l, std::integral_constant<int, C::COLS>{});
-        else level(l, std::integral_constant<int, NU_LAST>{});
+        if (NU_LAST == C::COLS || wave < C::NWAVES - 1) rows(l, std::integral_constant<int, C::COLS>{});
+        else rows(l, std::integral_constant<int, NU_LAST>{});
     }
 }
 
-#define DVC_TILE_INST(T, R)                                                   \
-    template __global__ void k_lookup_tile<T, R, false, 0, false>(LookupArgs); \
-    template __global__ void k_lookup_tile<T, R, true, 0, false>(LookupArgs);
+#define DVC_TILE_INST(T, R)                                                      \
+    template __global__ void k_lookup_tile<T, R, false, 0, false, 0>(LookupArgs); \
+    template __global__ void k_lookup_tile<T, R, true, 0, false, 0>(LookupArgs);  \
+    template __global__ void k_lookup_tile<T, R, true, 0, false, 3>(LookupArgs);
 DVC_TILE_INST(float, 1) DVC_TILE_INST(float, 2) DVC_TILE_INST(float, 3)
 DVC_TILE_INST(float, 4) DVC_TILE_INST(float, 5) DVC_TILE_INST(float, 6)
 DVC_TILE_INST(bf16_t, 1) DVC_TILE_INST(bf16_t, 2) DVC_TILE_INST(bf16_t, 3)
 DVC_TILE_INST(bf16_t, 4) DVC_TILE_INST(bf16_t, 5) DVC_TILE_INST(bf16_t, 6)
-template __global__ void k_lookup_tile<bf16_t, 4, true, 1, false>(LookupArgs);
-template __global__ void k_lookup_tile<bf16_t, 4, true, 2, false>(LookupArgs);
-template __global__ void k_lookup_tile<bf16_t, 4, true, 3, false>(LookupArgs);
+template __global__ void k_lookup_tile<bf16_t, 4, true, 1, false, 0>(LookupArgs);
+template __global__ void k_lookup_tile<bf16_t, 4, true, 2, false, 0>(LookupArgs);
+template __global__ void k_lookup_tile<bf16_t, 4, true, 3, false, 0>(LookupArgs);
 // convc1-fused instances (radii whose (2r+1) x 3 row values fit one 32-k slice)
-#define DVC_TILE_PROJ(T, R) template __global__ void k_lookup_tile<T, R, true, 0, true>(LookupArgs);
+#define DVC_TILE_PROJ(T, R) template __global__ void k_lookup_tile<T, R, true, 0, true, 0>(LookupArgs);
 DVC_TILE_PROJ(float, 1) DVC_TILE_PROJ(float, 2) DVC_TILE_PROJ(float, 3) DVC_TILE_PROJ(float, 4)
 DVC_TILE_PROJ(bf16_t, 1) DVC_TILE_PROJ(bf16_t, 2) DVC_TILE_PROJ(bf16_t, 3) DVC_TILE_PROJ(bf16_t, 4)
 
 // Weight re-layout for the PROJ instances: W (96, L (2r+1)^3) fp32, the reference's
-// convc1.weight viewed (96, L*(2r+1)^3) (update.py:222) -> bf16 in the consumer's
+// convc1.weight viewed (96, L*(2r+1)^3) (update.py:222) -> fp16 in the consumer's
 // MFMA A-operand order [l][a][wave][ot][lane][8].  Lane (m16, h4) of tile ot holds
 // channel o = 16 ot + m16 at the slice positions k = 8 h4 .. 8 h4 + 7 (k order above);
 // positions past the wave's values are 0.  Reference channel of (l, a, u, v):
@@ -496,7 +515,7 @@ __global__ void k_proj_pack(const float *__restrict__ w, bf16_t *__restrict__ ou
         const long long ch = (long long)l * n * n * n + (long long)a * n * n + (legacy ? u + v * n : u * n + v);
         val = w[(long long)o * L * n * n * n + ch];
     }
-    out[idx] = f32_to_bf16(val);
+    out[idx] = __builtin_bit_cast(bf16_t, (_Float16)val);   // fp16 bits
 }
 
 }  // namespace dvc

@@ -192,16 +192,16 @@ class CorrBlock(_Block):
         """F.relu(convc1(self(coords))) -> (B, 96, H, W, D) fp32 with convc1 fused into the lookup.
 
         The motion encoder's first layer (update.py:219-222, 246: Conv3d(L*(2r+1)^3, 96, 1) + ReLU)
-        runs on bf16 MFMA inside the lookup kernel of a bf16 block, so the L*(2r+1)^3-channel tensor
-        never reaches HBM (dvc_corr_lookup_proj; tolerance 1e-2 max-normalised, bf16 operands, fp32
-        accumulation).  An fp32 block (tolerance 1e-5), gradients, or radii/conventions the fused
-        kernel does not cover take the composition F.relu(F.conv3d(self(coords), weight, bias)) on
-        the GPU."""
+        runs on fp16 MFMA (fp32 accumulation; the reference's AMP convc1 is fp16 too) inside the
+        lookup kernel of a bf16 block, so the L*(2r+1)^3-channel tensor never reaches HBM
+        (dvc_corr_lookup_proj; tolerance 1e-2 max-normalised).  An fp32 block (tolerance 1e-5),
+        gradients, or radii/conventions the fused kernel does not cover take the composition
+        F.relu(F.conv3d(self(coords), weight, bias)) on the GPU."""
         self._check_coords(coords)
         B, _, H, W, D = self.shape
         w = weight.reshape(weight.shape[0], -1)
-        # fp32 blocks keep the reference's fp32 convc1 (update.py:246): the fused kernel's bf16 MFMA
-        # operands would cost ~5e-3 relative error, so they take the exact composition below
+        # fp32 blocks keep the reference's fp32 convc1 (update.py:246): the fused kernel's fp16 MFMA
+        # operands would cost ~1e-3 relative error, so they take the exact composition below
         fused_ok = (self.precision == "bf16"
                     and not (torch.is_grad_enabled() and (weight.requires_grad or bias.requires_grad or
                                                           self._grad_fmaps is not None))

@@ -10,7 +10,7 @@ straight to libdvccorr.so (no CPU fallback).  Shapes follow include/dvccorr.h:
     lookup(corr, coords (B, 3, Nq) f32, ...)           -> (B, L*(2r+1)^3, Nq)  f32
     lookup_fused(q, t, coords, ...)                    -> (B, L*(2r+1)^3, Nq)  f32
     sample3d(vol (B, C, Hv, Wv, Dv), pts (B, Nq, 3))   -> (B, C, Nq)           f32
-    proj_pack(convc1 weight (96, L*(2r+1)^3) f32, ...) -> packed bf16 weights
+    proj_pack(convc1 weight (96, L*(2r+1)^3) f32, ...) -> packed fp16 weights
     lookup_proj(corr, coords, packed_w, bias, ...)     -> (B, 96, Nq)          f32
     coords_grid(B, H, W, D, device)                    -> (B, 3, H, W, D)      f32
     upflow(flow (B, C, h, w, d), (H, W, D))            -> (B, C, H, W, D)      f32
@@ -126,7 +126,7 @@ def lookup(corr: torch.Tensor, coords: torch.Tensor, H: int, W: int, D: int, num
 
 
 def proj_pack(weight: torch.Tensor, num_levels: int, radius: int, legacy: bool) -> torch.Tensor:
-    """convc1.weight (96, L*(2r+1)^3[, 1, 1, 1]) -> the fused kernel's packed bf16 operand (dvc_proj_pack)."""
+    """convc1.weight (96, L*(2r+1)^3[, 1, 1, 1]) -> the fused kernel's packed fp16 operand (dvc_proj_pack)."""
     _need_cuda(weight)
     w = _f32c(weight.detach().reshape(weight.shape[0], -1))
     nbytes = lib().dvc_proj_packed_bytes(num_levels, radius)
@@ -135,7 +135,7 @@ def proj_pack(weight: torch.Tensor, num_levels: int, radius: int, legacy: bool) 
     if w.shape[1] != num_levels * (2 * radius + 1) ** 3:
         raise ValueError(f"convc1 weight has {w.shape[1]} input channels; the lookup has "
                          f"{num_levels * (2 * radius + 1) ** 3}")
-    out = torch.empty((nbytes // 2,), dtype=torch.bfloat16, device=w.device)
+    out = torch.empty((nbytes // 2,), dtype=torch.float16, device=w.device)
     check(lib().dvc_proj_pack(_ptr(w), _ptr(out), w.shape[0], num_levels, radius,
                               DVC_LEGACY if legacy else DVC_FIXED, _stream(w)), "proj_pack")
     return out

@@ -51,11 +51,11 @@ def _rank(group) -> int:
     return dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
 
 
-def gather_slabs(slab: torch.Tensor, H: int, group=None, dim: int = 2) -> torch.Tensor:
-    """All-gather H-slabs (split along `dim`) into the full tensor.  One collective."""
+def all_gather_slab(slab: torch.Tensor, H: int, group=None, dim: int = 2, buf: Optional[torch.Tensor] = None):
+    """The collective half of gather_slabs: every rank's slab (zero-padded to ceil(H / world) along `dim`)
+    into buf[world, ...].  One collective, chosen from the group's backend -- identical on every rank, so
+    the ranks' collective sequences cannot diverge, and a failing collective raises on every rank."""
     world = _world(group)
-    if world == 1:
-        return slab
     maxh = -(-H // world)
     pad = maxh - slab.shape[dim]
     if pad:
@@ -63,18 +63,32 @@ def gather_slabs(slab: torch.Tensor, H: int, group=None, dim: int = 2) -> torch.
         shape[dim] = pad
         slab = torch.cat([slab, slab.new_zeros(shape)], dim=dim)
     slab = slab.contiguous()
-    buf = slab.new_empty((world,) + tuple(slab.shape))
-    # one collective, chosen from the group's backend (identical on every rank, so the ranks'
-    # collective sequences cannot diverge); a failing collective raises on every rank
-    if dist.get_backend(group) == "nccl":      # RCCL: one fused all-gather into the contiguous buffer
+    if buf is None:
+        buf = slab.new_empty((world,) + tuple(slab.shape))
+    if world == 1:
+        buf[0].copy_(slab)
+    elif dist.get_backend(group) == "nccl":    # RCCL: one all-gather into the contiguous buffer
         dist.all_gather_into_tensor(buf, slab, group=group)
     else:                                      # gloo (CPU tests): list form
         dist.all_gather(list(buf.unbind(0)), slab, group=group)
+    return buf
+
+
+def assemble_slabs(buf: torch.Tensor, H: int, dim: int = 2) -> torch.Tensor:
+    """The local half of gather_slabs: buf[world, ...] (padded slabs) -> the full tensor along `dim`."""
+    world = buf.shape[0]
     parts = []
     for r in range(world):
         h0, h1 = slab_bounds(H, world, r)
         parts.append(buf[r].narrow(dim, 0, h1 - h0))
     return torch.cat(parts, dim=dim)
+
+
+def gather_slabs(slab: torch.Tensor, H: int, group=None, dim: int = 2) -> torch.Tensor:
+    """All-gather H-slabs (split along `dim`) into the full tensor.  One collective."""
+    if _world(group) == 1:
+        return slab
+    return assemble_slabs(all_gather_slab(slab, H, group, dim), H, dim)
 
 
 class HipRows:

@@ -1,9 +1,10 @@
 """GPU parity of the convc1-fused lookup (dvc_corr_lookup_proj, CorrBlock.lookup_convc1).
 
 Reference: CorrBlock.__call__ (src/core/corr.py:169-208) followed by MotionEncoder's
-F.relu(self.convc1(corr)) (src/core/update.py:219-222, 246).  The fused kernel feeds the
-lookup values and the weights to bf16 MFMA with fp32 accumulation, so the tolerance is the
-bf16 one of SURVEY.md 8(c): max|out - ref| / max|ref| <= 1e-2, against
+F.relu(self.convc1(corr)) (src/core/update.py:219-222, 246).  On a bf16 block the fused kernel
+feeds the lookup values and the weights to fp16 MFMA with fp32 accumulation (as the reference's
+AMP convc1 runs in fp16), so the tolerance is the bf16 one of SURVEY.md 8(c): max|out - ref| /
+max|ref| <= 1e-2; an fp32 block keeps fp32 arithmetic and the fp32 tolerance 1e-5.  Against
   * the reference's own outputs (tests/golden/proj_*.npz, gen_proj_golden.py),
   * the CPU oracle (f64 lookup + motion_convc1) on ragged / non-cubic / zero-level cases,
   * the unfused GPU composition relu(conv3d(lookup)) at the bench size (32^3, C=128, L=4, r=4).
@@ -24,6 +25,8 @@ from oracle import oracle as orc
 pytestmark = pytest.mark.gpu
 
 PROJ_TOL = 1e-2
+FP32_TOL = 1e-5
+FUSED_VS_UNFUSED_TOL = 2e-3
 DEV = torch.device("cuda:0")
 PROJ_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "proj_*.npz")))
 
@@ -55,7 +58,7 @@ def test_golden_reference(case, precision):
     out = blk.lookup_convc1(tc, tw, tb)
     torch.cuda.synchronize()
     assert out.shape == g["out"].shape and out.dtype == torch.float32
-    assert orc.rel_err(out.cpu().numpy(), g["out"]) < PROJ_TOL
+    assert orc.rel_err(out.cpu().numpy(), g["out"]) < (PROJ_TOL if precision == "bf16" else FP32_TOL)
 
 
 @pytest.mark.parametrize("shape,C,L,r,legacy", [
@@ -79,7 +82,7 @@ def test_against_oracle(shape, C, L, r, legacy):
     for precision in ("fp32", "bf16"):
         blk = dvccorr.CorrBlock(t1, t2, L, r, legacy_wd_swap=legacy, precision=precision)
         out = blk.lookup_convc1(tc, tw, tb).cpu().numpy()
-        assert orc.rel_err(out, ref) < PROJ_TOL, precision
+        assert orc.rel_err(out, ref) < (PROJ_TOL if precision == "bf16" else FP32_TOL), precision
 
 
 def test_nonfinite_coords_give_relu_bias():
@@ -116,7 +119,7 @@ def test_bench_size_against_unfused_and_deterministic():
     out2 = blk.lookup_convc1(coords, w, b)
     torch.cuda.synchronize()
     err = float((out - ref).abs().max() / ref.abs().max())
-    assert err < PROJ_TOL, err
+    assert err < FUSED_VS_UNFUSED_TOL, err     # same pyramid: only the fp16 operand rounding differs
     assert torch.equal(out, out2)
 
 
