@@ -73,6 +73,8 @@ def parse(argv=None):
     ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
                     help="N>1: strong = one pair's query voxels sharded by H slabs (default); weak = one volume "
                          "pair per rank (global batch N)")
+    ap.add_argument("--no-overlap", dest="overlap", action="store_false", default=True,
+                    help="N>1 strong: do not overlap the next step's fmap2 all-gather with this step's compute")
     ap.add_argument("--graph", dest="graph", action="store_true", default=True,
                     help="replay each rank's post-collective step as a HIP graph (default)")
     ap.add_argument("--no-graph", dest="graph", action="store_false")
@@ -173,12 +175,17 @@ def cpu_baseline(args, f1, f2, coords_list):
 class Runner:
     """One rank's correlation step: [all-gather of the fmap2 slabs] + pack/build + `iters` lookups.
 
-    The collective runs eagerly on the current stream; everything after it is optionally captured once
-    as a HIP graph (torch.cuda.CUDAGraph over the stream-ordered, allocation-free C ABI) and replayed,
-    which removes the host launch cost of the 15 launches per step when the per-rank work is small."""
+    The collective is issued eagerly; everything after it is optionally captured once as a HIP graph
+    (torch.cuda.CUDAGraph over the stream-ordered, allocation-free C ABI) and replayed, which removes the
+    host launch cost of the 15 launches per step when the per-rank work is small.
+
+    overlap=True (sharded runs): the fmap2 all-gather of step k+1 is issued asynchronously (RCCL's own
+    stream) while step k computes, into the other half of a double-buffered receive buffer -- consecutive
+    forwards pipelined the way a serving loop would run them.  Every step still gathers, builds and looks
+    up in full; only the collective's latency is hidden behind the previous step's lookups."""
 
     def __init__(self, f1_slab, f2_slab, coords_slabs, H, args, group, world, gather_output=False,
-                 graph=True, proj=None):
+                 graph=True, proj=None, overlap=False):
         from dvccorr.sharded import LOCAL
         self.args, self.group, self.H = args, group, H
         self.world = 1 if group == LOCAL else world
@@ -189,23 +196,30 @@ class Runner:
         self.coords = [c.reshape(B, 3, -1).contiguous() for c in coords_slabs]
         self.slab_shape = tuple(f1_slab.shape)
         self.proj = proj
-        self.buf = None
+        self.bufs = [None, None]
+        self.overlap = overlap and self.world > 1 and not self.gather_output
         if self.world > 1:
             from dvccorr.sharded import all_gather_slab
-            self.buf = all_gather_slab(self.f2_slab, H, group)      # allocates the static receive buffer
+            # the static receive buffer(s) (two when the next step's gather overlaps this step's compute)
+            self.bufs = [all_gather_slab(self.f2_slab, H, group) for _ in range(2 if self.overlap else 1)]
         self.use_graph = graph and not self.gather_output
-        self.graph = None
+        self.graphs = [None, None]
         self.outs = None
+        self.k = 0            # step counter (selects the receive buffer)
+        self.pending = None   # async work handle of the next step's gather
 
-    def collective(self):
+    def collective(self, slot=0, async_op=False):
         if self.world > 1:
             from dvccorr.sharded import all_gather_slab
-            all_gather_slab(self.f2_slab, self.H, self.group, buf=self.buf)
+            if async_op:
+                return all_gather_slab(self.f2_slab, self.H, self.group, buf=self.bufs[slot], async_op=True)
+            all_gather_slab(self.f2_slab, self.H, self.group, buf=self.bufs[slot])
+        return None
 
-    def compute(self, ev=None, stream=None):
+    def compute(self, ev=None, stream=None, slot=0):
         from dvccorr.sharded import HipRows, assemble_slabs, gather_slabs
         a = self.args
-        f2 = assemble_slabs(self.buf, self.H) if self.world > 1 else self.f2_slab
+        f2 = assemble_slabs(self.bufs[slot], self.H) if self.world > 1 else self.f2_slab
         if ev is not None:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record(stream)
@@ -236,31 +250,52 @@ class Runner:
             outs.append(o)
         return outs
 
-    def capture(self):
+    def capture(self, slot):
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
-            self.compute()                         # warm-up outside the capture (library load, attributes)
+            self.compute(slot=slot)                # warm-up outside the capture (library load, attributes)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.outs = self.compute()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.outs = self.compute(slot=slot)
+        self.graphs[slot] = g
+
+    def _run(self, slot):
+        if self.use_graph:
+            if self.graphs[slot] is None:
+                self.capture(slot)
+            self.graphs[slot].replay()
+        else:
+            self.outs = self.compute(slot=slot)
 
     def step(self):
-        self.collective()
-        if self.use_graph:
-            if self.graph is None:
-                self.capture()
-            self.graph.replay()
-        else:
-            self.outs = self.compute()
+        if not self.overlap:
+            self.collective()
+            self._run(0)
+            return
+        slot = self.k & 1
+        if self.pending is None:                   # first step: nothing in flight yet
+            self.pending = self.collective(slot, async_op=True)
+        self.pending.wait()                        # this step's fmap2 is in bufs[slot]
+        # the next step's gather goes into the other buffer, which the previous step's compute (already
+        # enqueued before this point) has finished reading by the time RCCL's stream starts it
+        self.pending = self.collective(slot ^ 1, async_op=True)
+        self._run(slot)
+        self.k += 1
+
+    def drain(self):
+        if self.pending is not None:
+            self.pending.wait()
+            self.pending = None
 
     def release(self):
-        self.graph = None
+        self.drain()
+        self.graphs = [None, None]
         self.outs = None
-        self.buf = None
+        self.bufs = [None, None]
 
 
 def timed(runner, steps, warmup, dist, dev, participate=True):
@@ -274,11 +309,13 @@ def timed(runner, steps, warmup, dist, dev, participate=True):
         if participate:
             for _ in range(warmup):
                 runner.step()
+            runner.drain()
         barrier()
         t0 = time.perf_counter()
         if participate:
             for _ in range(steps):
                 runner.step()
+            runner.drain()
         barrier()
         elapsed = time.perf_counter() - t0
     if dist:
@@ -360,7 +397,7 @@ def main():
                 ((torch.rand(96, generator=g) * 2 - 1) / K ** 0.5).to(dev))
 
     runner = Runner(f1_slab, f2_slab, coords_slab, S, args, group, world, gather_output=args.gather_output,
-                    graph=args.graph, proj=proj)
+                    graph=args.graph, proj=proj, overlap=args.overlap)
     elapsed = timed(runner, args.steps, args.warmup, dist, dev)
     runner.release()
     ms_per_step = elapsed * 1e3 / args.steps
@@ -459,7 +496,10 @@ def main():
                                    f"input, 1/{args.encoder} encoder), L={L}, r={R}, {args.impl}, {args.precision} build / fp32 lookup",
                        "global_batch": B if strong else B * world, "query_voxels": nq_total, "levels": L,
                        "radius": R, "parallelism": par + (", output all-gather" if args.gather_output else ""),
-                       "step_replay": "hip graph after the collective" if runner.use_graph else "eager"},
+                       "step_replay": "hip graph after the collective" if runner.use_graph else "eager",
+                       "collective": ("next step's fmap2 all-gather overlapped with this step's compute"
+                                      if runner.overlap else "fmap2 all-gather before the step's compute"
+                                      if runner.world > 1 else None)},
             "roofline": roof,
             "build": build_info,
             "lookup_avg_ms": round(lk_avg, 4),
@@ -518,6 +558,14 @@ def scaling_detail(args, f1, f2, coords_list, ms_strong, world, rank, dev, dist,
     torch.cuda.empty_cache()
     out["cfg3_t1_ms"] = round(t1, 4)
     out["cfg3_strong_resident"] = {"ms_per_step": round(ms_strong, 4), "E": round(t1 / (world * ms_strong), 4)}
+    if args.overlap:   # the same layout with the collective on the critical path
+        h0, h1 = slab_bounds(S, world, rank)
+        rs = Runner(f1[:, :, h0:h1].contiguous().to(dev), f2[:, :, h0:h1].contiguous().to(dev),
+                    [c[:, :, h0:h1].contiguous().to(dev) for c in coords_list], S, args, group, world,
+                    graph=args.graph, proj=proj, overlap=False)
+        ts = timed(rs, steps, warm, dist, dev) * 1e3 / steps
+        rs.release()
+        out["cfg3_strong_resident_serial_collective"] = {"ms_per_step": round(ts, 4), "E": round(t1 / (world * ts), 4)}
     h0, h1 = slab_bounds(S, world, rank)
     f1s, f2s = f1[:, :, h0:h1].contiguous().to(dev), f2[:, :, h0:h1].contiguous().to(dev)
     cs = [c[:, :, h0:h1].contiguous().to(dev) for c in coords_list]
@@ -555,7 +603,8 @@ def cfg4_strong(args, world, rank, dev, dist, group):
     torch.cuda.empty_cache()
     h0, h1 = slab_bounds(S, world, rank)
     rn = Runner(f1[:, :, h0:h1].contiguous(), f2[:, :, h0:h1].contiguous(),
-                [c[:, :, h0:h1].contiguous() for c in coords], S, a4, group, world, graph=args.graph)
+                [c[:, :, h0:h1].contiguous() for c in coords], S, a4, group, world, graph=args.graph,
+                overlap=args.overlap)
     tn = timed(rn, steps, 1, dist, dev) * 1e3 / steps
     rn.release()
     del rn

@@ -92,7 +92,8 @@ typedef struct {
  * reference constructor raises: pooling an axis of size < 2. */
 int dvc_layout_init(int H, int W, int D, int num_levels, int C, dvc_layout *out);
 
-/* Bytes of float32 workspace dvc_pack_targets needs (pooled fmap2 levels 1..L-1). */
+/* Bytes of float32 workspace dvc_pack_targets needs (pooled fmap2 levels 1..L-1; 0 for
+ * num_levels <= 4, whose levels are pooled in LDS by one single-pass kernel). */
 size_t dvc_pack_workspace_bytes(int B, int C, int H, int W, int D, int num_levels);
 
 /* fmap1 query slab (B, C, Nq) float32 -> packed queries [B][Nq][c_pad] (dtype). */

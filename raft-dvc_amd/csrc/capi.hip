@@ -18,6 +18,13 @@ namespace dvc {
 __global__ void k_pool_fmap(const float *, float *, long long, int, int, int, int, int, int);
 template <typename T>
 __global__ void k_pack_rows(const float *, T *, int, int, long long, long long, int, int, long long, long long);
+struct PyrGeo {
+    int L, C, Cp, H[4], W[4], D[4], Dp[4];
+    long long off[4];
+    long long row_stride;
+    int ncx, ncy, ncz;
+};
+template <typename T> __global__ void k_pack_pyramid(const float *, T *, PyrGeo);
 template <int NCH, bool STORE_F32, int ABL>
 __global__ void k_build_bf16(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long, long long, long long,
                              long long, int, float);
@@ -67,6 +74,7 @@ static thread_local int g_build_variant = 1;      // 1 = two-barrier bf16-store 
 static thread_local int g_fused_variant = 2;
 static thread_local int g_upflow_rows = 8;        // output rows per k_upflow work item
 static thread_local int g_upflow_wgs = 1024;      // k_upflow grid (workgroups striding over the items)
+static thread_local int g_pack_variant = 1;       // 1 = single-pass k_pack_pyramid where L <= 4, 0 = per-level launches
 static thread_local int g_fused_ablate = 0;       // diagnostics only: 1 = skip output stores, 2 = skip window dots (cube kernel)
 
 static int fail(int code, const char *fmt, ...) {
@@ -151,7 +159,7 @@ static void launch_tile_nt(const LookupArgs &A0, hipStream_t s) {
     const long long tiles = (long long)A.B * A.nqb;
     A.split_levels = tiles < kSplitTiles && A.nl > 1;
     const int n = 2 * A.r + 1;
-    const bool split_rows = NT && tiles * (A.split_levels ? A.nl : 1) < kSplitRows && n > 3;
+    const bool split_rows = NT && A.split_levels && tiles * A.nl < kSplitRows && n > 3;
     const dim3 blocks((unsigned)tiles, A.split_levels ? (unsigned)A.nl : 1u, split_rows ? (unsigned)((n + 2) / 3) : 1u);
     const unsigned threads = 64u * (unsigned)((2 * A.r + 3) / 3);
     if constexpr (std::is_same<T, bf16_t>::value && NT) {
@@ -221,6 +229,11 @@ int dvc_set_tuning(const char *key, int value) {
     }
     if (!strcmp(key, "build_stpol")) {
         g_build_stpol = value != 0;
+        return DVC_OK;
+    }
+    if (!strcmp(key, "pack_variant")) {
+        if (value < 0 || value > 1) return fail(DVC_ERR_INVALID, "set_tuning: pack_variant %d", value);
+        g_pack_variant = value;
         return DVC_OK;
     }
     if (!strcmp(key, "build_variant")) {
@@ -297,6 +310,7 @@ size_t dvc_pack_workspace_bytes(int B, int C, int H, int W, int D, int num_level
     dvc_layout lay;
     if (dvc_layout_init(H, W, D, num_levels, C, &lay)) return 0;
     size_t s = 0;
+    if (num_levels <= 4 && g_pack_variant == 1) return 0;   // k_pack_pyramid pools in LDS
     for (int l = 1; l < num_levels; ++l) s += (size_t)B * C * lay.H[l] * lay.W[l] * lay.D[l] * sizeof(float);
     return s;
 }
@@ -322,7 +336,8 @@ int dvc_pack_targets(const float *fmap2, void *packed, float *workspace, int B, 
     dvc_layout lay;
     int rc = dvc_layout_init(H, W, D, num_levels, C, &lay);
     if (rc) return rc;
-    if (!fmap2 || !packed || (num_levels > 1 && !workspace)) return fail(DVC_ERR_INVALID, "pack_targets: null pointer");
+    if (!fmap2 || !packed || (dvc_pack_workspace_bytes(B, C, H, W, D, num_levels) > 0 && !workspace))
+        return fail(DVC_ERR_INVALID, "pack_targets: null pointer");
     if (B < 1) return fail(DVC_ERR_INVALID, "pack_targets: B=%d", B);
     if (dtype != DVC_BF16 && dtype != DVC_F32) return fail(DVC_ERR_INVALID, "pack_targets: bad dtype %d", dtype);
     hipStream_t s = (hipStream_t)stream;
@@ -330,6 +345,19 @@ int dvc_pack_targets(const float *fmap2, void *packed, float *workspace, int B, 
     const size_t esz = dtype == DVC_BF16 ? 2 : 4;
     if (hipMemsetAsync(packed, 0, (size_t)B * lay.row_stride * Cp * esz, s) != hipSuccess)
         return fail(DVC_ERR_RUNTIME, "pack_targets: memset failed");
+    if (num_levels <= 4 && g_pack_variant == 1) {   // one pass: every level of an 8^3 cell pooled in LDS (k_pack_pyramid)
+        PyrGeo g;
+        memset(&g, 0, sizeof(g));
+        g.L = num_levels; g.C = C; g.Cp = Cp; g.row_stride = lay.row_stride;
+        for (int l = 0; l < num_levels; ++l) {
+            g.H[l] = lay.H[l]; g.W[l] = lay.W[l]; g.D[l] = lay.D[l]; g.Dp[l] = lay.Dp[l]; g.off[l] = lay.offset[l];
+        }
+        g.ncy = (H + 7) / 8; g.ncx = (W + 7) / 8; g.ncz = (D + 7) / 8;
+        dim3 grid((unsigned)(g.ncy * g.ncx * g.ncz), (unsigned)ceil_div(Cp, 16), (unsigned)B);
+        if (dtype == DVC_BF16) k_pack_pyramid<bf16_t><<<grid, 256, 0, s>>>(fmap2, (bf16_t *)packed, g);
+        else k_pack_pyramid<float><<<grid, 256, 0, s>>>(fmap2, (float *)packed, g);
+        return check_launch("pack_targets");
+    }
     const float *src = fmap2;
     float *ws = workspace;
     for (int l = 0; l < num_levels; ++l) {

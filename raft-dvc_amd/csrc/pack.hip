@@ -34,6 +34,20 @@ __global__ __launch_bounds__(256) void k_pool_fmap(const float *__restrict__ src
     }
 }
 
+// 16 consecutive channels of one packed row as 16-byte stores (Cp is a multiple of 32, rows 16-byte aligned).
+__device__ __forceinline__ void store16(float *d, const float (&v)[16]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        *reinterpret_cast<float4 *>(d + 4 * k) = float4{v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]};
+}
+__device__ __forceinline__ void store16(bf16_t *d, const float (&v)[16]) {
+    unsigned w[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w[k] = (unsigned)f32_to_bf16(v[2 * k]) | ((unsigned)f32_to_bf16(v[2 * k + 1]) << 16);
+    *reinterpret_cast<u32x4 *>(d) = u32x4{w[0], w[1], w[2], w[3]};
+    *reinterpret_cast<u32x4 *>(d + 8) = u32x4{w[4], w[5], w[6], w[7]};
+}
+
 // One block: 64 destination rows x 64 channels of one batch element.
 // Destination row j (0 <= j < nrows) maps to source position:
 //   padded (Dp > 0): j = (y*Wl + x)*Dp + z  -> (y*Wl + x)*Dl + z if z < Dl else none
@@ -71,15 +85,138 @@ __global__ __launch_bounds__(256) void k_pack_rows(const float *__restrict__ src
         }
     }
     __syncthreads();
-    // store: thread -> row j0 + (t >> 2), 16 channels starting at c0 + 16*(t & 3)
+    // store: thread -> row j0 + (t >> 2), 16 channels starting at c0 + 16*(t & 3), as 16-byte stores
     const long long j = j0 + (t >> 2);
     if (j >= nrows) return;
     const int cs = 16 * (t & 3);
     if (c0 + cs >= Cp) return;
     T *d = dst + ((long long)b * dst_batch_rows + dst_row0 + j) * Cp + c0 + cs;
+    float v[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) StoreT<T>::store(d + k, tile[cs + k][t >> 2]);
+    for (int k = 0; k < 16; ++k) v[k] = tile[cs + k][t >> 2];
+    store16(d, v);
 }
+
+// ---------------------------------------------------------------------------------------------------
+// k_pack_pyramid: fmap2 (B, C, H, W, D) float32 -> every packed target level in ONE pass (L <= 4).
+// One workgroup = one 8x8x8 cell of level-0 voxels (the cell grid is the ceil of the volume) x 16
+// channels of one batch element: the cell is loaded once into LDS, pooled level by level in LDS with
+// k_pool_fmap's arithmetic (2x2x2 mean in (dy, dx, dz) order, then / 8: bit-identical to the
+// multi-launch path), and every level's rows of the cell leave as 16-byte stores of 8 channels.
+// A level-l voxel exists iff its index is inside level l's (floor-pooled) extent; then all of its
+// children exist.  Padding rows (z >= D_l, row tail) are the caller's memset.
+constexpr int kPyrE = 8, kPyrCG = 16, kPyrLd = kPyrCG + 1;   // cell edge, channels per group, LDS row
+
+struct PyrGeo {
+    int L, C, Cp, H[4], W[4], D[4], Dp[4];
+    long long off[4];
+    long long row_stride;
+    int ncx, ncy, ncz;   // cells per axis (level 0, ceil)
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_pack_pyramid(const float *__restrict__ src, T *__restrict__ dst, PyrGeo g) {
+    __shared__ float lv0[kPyrE * kPyrE * kPyrE][kPyrLd];   // 34 KB
+    __shared__ float lv1[64][kPyrLd];
+    __shared__ float lv2[8][kPyrLd];
+    __shared__ float lv3[1][kPyrLd];
+    const int t = threadIdx.x;
+    const int cg = blockIdx.y, b = blockIdx.z;
+    int cell = blockIdx.x;
+    const int cz = cell % g.ncz; cell /= g.ncz;
+    const int cx = cell % g.ncx;
+    const int cy = cell / g.ncx;
+    const int y0 = cy * kPyrE, x0 = cx * kPyrE, z0 = cz * kPyrE;
+    const long long npos = (long long)g.H[0] * g.W[0] * g.D[0];
+    const float *sb = src + (long long)b * g.C * npos;
+    // load: 4-voxel z-runs; idx -> (channel k, run v4 = (dy, dx, dz / 4)), every load issued before the
+    // LDS writes (16-byte loads when D % 4 == 0: the runs are then 16-byte aligned)
+    constexpr int NLD = kPyrCG * 128 / 256;
+    float4 vals[NLD];
+    const bool vec = (g.D[0] & 3) == 0;
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+        const int idx = t + 256 * i;
+        const int v = (idx & 127) * 4, k = idx >> 7;
+        const int dz = v & 7, dx = (v >> 3) & 7, dy = v >> 6;
+        const int c = cg * kPyrCG + k, y = y0 + dy, x = x0 + dx, z = z0 + dz;
+        const bool in = c < g.C && y < g.H[0] && x < g.W[0];
+        const float *p = sb + (long long)c * npos + ((long long)y * g.W[0] + x) * g.D[0] + z;
+        float4 r = float4{0.f, 0.f, 0.f, 0.f};
+        if (in && vec && z + 3 < g.D[0]) {
+            r = *reinterpret_cast<const float4 *>(p);
+        } else if (in) {
+            r.x = z < g.D[0] ? p[0] : 0.f;
+            r.y = z + 1 < g.D[0] ? p[1] : 0.f;
+            r.z = z + 2 < g.D[0] ? p[2] : 0.f;
+            r.w = z + 3 < g.D[0] ? p[3] : 0.f;
+        }
+        vals[i] = r;
+    }
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+        const int idx = t + 256 * i;
+        const int v = (idx & 127) * 4, k = idx >> 7;
+        lv0[v][k] = vals[i].x;
+        lv0[v + 1][k] = vals[i].y;
+        lv0[v + 2][k] = vals[i].z;
+        lv0[v + 3][k] = vals[i].w;
+    }
+    __syncthreads();
+    // pooled levels (k_pool_fmap's summation order)
+    auto pool = [&](const float (*s)[kPyrLd], float (*d)[kPyrLd], int e) {   // e = destination cell edge
+        const int n = e * e * e;
+        for (int idx = t; idx < n * kPyrCG; idx += 256) {
+            const int v = idx / kPyrCG, k = idx - v * kPyrCG;
+            const int z = v % e, x = (v / e) % e, y = v / (e * e);
+            const int es = 2 * e;
+            float acc = 0.0f;
+#pragma unroll
+            for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < 2; ++dx)
+#pragma unroll
+                    for (int dz = 0; dz < 2; ++dz)
+                        acc += s[((2 * y + dy) * es + (2 * x + dx)) * es + (2 * z + dz)][k];
+            d[v][k] = acc / 8.0f;
+        }
+    };
+    if (g.L > 1) { pool(lv0, lv1, 4); __syncthreads(); }
+    if (g.L > 2) { pool(lv1, lv2, 2); __syncthreads(); }
+    if (g.L > 3) { pool(lv2, lv3, 1); __syncthreads(); }
+    // stores: (voxel, 8-channel chunk) per thread; 2 chunks cover the group's 16 channels
+    T *db = dst + (long long)b * g.row_stride * g.Cp;
+    constexpr int NCK = kPyrCG / 8;
+    for (int l = 0; l < g.L; ++l) {
+        const int e = kPyrE >> l;
+        const float (*s)[kPyrLd] = l == 0 ? lv0 : l == 1 ? lv1 : l == 2 ? lv2 : lv3;
+        const int ly0 = cy * e, lx0 = cx * e, lz0 = cz * e;
+        for (int idx = t; idx < e * e * e * NCK; idx += 256) {
+            const int v = idx / NCK, ch = (idx % NCK) * 8;
+            const int z = v % e, x = (v / e) % e, y = v / (e * e);
+            const int Y = ly0 + y, X = lx0 + x, Z = lz0 + z;
+            const int c = cg * kPyrCG + ch;
+            if (Y >= g.H[l] || X >= g.W[l] || Z >= g.D[l] || c >= g.Cp) continue;
+            T *d = db + (g.off[l] + ((long long)Y * g.W[l] + X) * g.Dp[l] + Z) * g.Cp + c;
+            float w[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) w[k] = s[v][ch + k];
+            if constexpr (sizeof(T) == 4) {
+                *reinterpret_cast<float4 *>(d) = float4{w[0], w[1], w[2], w[3]};
+                *reinterpret_cast<float4 *>(d + 4) = float4{w[4], w[5], w[6], w[7]};
+            } else {
+                unsigned u[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    u[k] = (unsigned)f32_to_bf16(w[2 * k]) | ((unsigned)f32_to_bf16(w[2 * k + 1]) << 16);
+                *reinterpret_cast<u32x4 *>(d) = u32x4{u[0], u[1], u[2], u[3]};
+            }
+        }
+    }
+}
+
+template __global__ void k_pack_pyramid<float>(const float *, float *, PyrGeo);
+template __global__ void k_pack_pyramid<bf16_t>(const float *, bf16_t *, PyrGeo);
 
 template __global__ void k_pack_rows<float>(const float *, float *, int, int, long long, long long, int, int,
                                             long long, long long);

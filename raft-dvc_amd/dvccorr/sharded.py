@@ -51,10 +51,13 @@ def _rank(group) -> int:
     return dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
 
 
-def all_gather_slab(slab: torch.Tensor, H: int, group=None, dim: int = 2, buf: Optional[torch.Tensor] = None):
+def all_gather_slab(slab: torch.Tensor, H: int, group=None, dim: int = 2, buf: Optional[torch.Tensor] = None,
+                    async_op: bool = False):
     """The collective half of gather_slabs: every rank's slab (zero-padded to ceil(H / world) along `dim`)
     into buf[world, ...].  One collective, chosen from the group's backend -- identical on every rank, so
-    the ranks' collective sequences cannot diverge, and a failing collective raises on every rank."""
+    the ranks' collective sequences cannot diverge, and a failing collective raises on every rank.
+    async_op=True returns the work handle (wait() orders the current stream after the gather) instead of
+    the buffer."""
     world = _world(group)
     maxh = -(-H // world)
     pad = maxh - slab.shape[dim]
@@ -67,11 +70,21 @@ def all_gather_slab(slab: torch.Tensor, H: int, group=None, dim: int = 2, buf: O
         buf = slab.new_empty((world,) + tuple(slab.shape))
     if world == 1:
         buf[0].copy_(slab)
+        work = None
     elif dist.get_backend(group) == "nccl":    # RCCL: one all-gather into the contiguous buffer
-        dist.all_gather_into_tensor(buf, slab, group=group)
+        work = dist.all_gather_into_tensor(buf, slab, group=group, async_op=async_op)
     else:                                      # gloo (CPU tests): list form
-        dist.all_gather(list(buf.unbind(0)), slab, group=group)
+        work = dist.all_gather(list(buf.unbind(0)), slab, group=group, async_op=async_op)
+    if async_op:
+        return work if work is not None else _Done()
     return buf
+
+
+class _Done:
+    """Work handle of a collective that completed synchronously (world size 1)."""
+
+    def wait(self):
+        return True
 
 
 def assemble_slabs(buf: torch.Tensor, H: int, dim: int = 2) -> torch.Tensor:

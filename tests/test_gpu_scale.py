@@ -273,3 +273,25 @@ def test_fp32_block_convc1_is_exact():
                           ref)
     assert e32 <= FP32_TOL, e32
     assert e16 <= BF16_TOL, e16
+
+
+@pytest.mark.parametrize("shape,C,L", [((9, 7, 8), 16, 3), ((16, 16, 16), 128, 4), ((33, 20, 17), 40, 4),
+                                       ((8, 8, 2), 64, 2), ((5, 6, 7), 32, 1), ((32, 32, 32), 128, 4),
+                                       ((24, 18, 40), 256, 4)])
+def test_single_pass_pack_matches_per_level(shape, C, L):
+    """k_pack_pyramid (fmap2 -> every packed target level in one pass, pooled in LDS) writes exactly the
+    bytes of the per-level pool + pack launches (same (dy, dx, dz) summation order), both dtypes."""
+    from dvccorr import _lib, ops
+    H, W, D = shape
+    g = torch.Generator(device="cpu").manual_seed(H + W + D + C + L)
+    f2 = torch.randn(2, C, H, W, D, generator=g).to(DEV)
+    for prec in ("bf16", "fp32"):
+        dt = ops.dtype_code(prec)
+        new = ops.pack_targets(f2, L, dt)
+        try:
+            _lib.set_tuning("pack_variant", 0)
+            old = ops.pack_targets(f2, L, dt)
+        finally:
+            _lib.set_tuning("pack_variant", 1)
+        torch.cuda.synchronize()
+        assert torch.equal(new, old), (shape, C, L, prec)
