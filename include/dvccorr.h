@@ -53,11 +53,11 @@ extern "C" {
 
 #define DVC_MAX_LEVELS 8
 #define DVC_ABI_VERSION 1
-/* The corr pyramid buffer passed to dvc_corr_lookup must be readable, and
- * hold finite values (e.g. zeros), for DVC_CORR_GUARD_BYTES before its first
- * row and after its last row: the lookup loads each window run from a clamped
- * address without branching and cancels out-of-range elements with zero
- * weights, so it may touch up to 2r+2 elements outside a row. */
+/* The corr pyramid buffer must be allocated with DVC_CORR_GUARD_BYTES of extra
+ * space before its first row and after its last row.  dvc_corr_build zeroes
+ * them; dvc_corr_lookup's walk kernels load each window run from a clamped
+ * address without branching and cancel out-of-range elements with zero
+ * weights, so they may touch up to 2r+2 elements outside a row. */
 #define DVC_CORR_GUARD_BYTES 256
 
 typedef enum {

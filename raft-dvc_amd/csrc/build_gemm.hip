@@ -66,6 +66,18 @@ template <int PF> struct PfTouch {
 
 __device__ __forceinline__ int swz_mask(int nch) { return (nch >= 16 ? 16 : nch) - 1; }
 
+// The DVC_CORR_GUARD_BYTES before and after the pyramid buffer (B = gridDim.z rows of Nq x row_stride
+// elements) are zeroed by the first workgroup: the lookup walks read them with zero weights.
+__device__ __forceinline__ void zero_guards(void *corr, long long Nq, long long row_stride, int esz) {
+    if (blockIdx.x != 0 || blockIdx.z != 0 || threadIdx.x >= 2 * DVC_CORR_GUARD_BYTES / 16) return;
+    unsigned char *base = reinterpret_cast<unsigned char *>(corr);
+    const int t = threadIdx.x;
+    const long long total = (long long)gridDim.z * Nq * row_stride * esz;
+    unsigned char *p = t < DVC_CORR_GUARD_BYTES / 16 ? base - DVC_CORR_GUARD_BYTES + 16 * t
+                                                    : base + total + 16 * (t - DVC_CORR_GUARD_BYTES / 16);
+    *reinterpret_cast<u32x4 *>(p) = u32x4{0u, 0u, 0u, 0u};
+}
+
 // ABL (diagnostics only, never the product path): 1 = skip the global stores, 2 = skip the MFMAs.
 template <int NCH, bool STORE_F32, int ABL>
 __global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict__ Q, const bf16_t *__restrict__ T,
@@ -74,6 +86,7 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict_
                                                        long long col_begin, long long col_end, int nchunk,
                                                        float scale) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    zero_guards(corr, Nq, row_stride, STORE_F32 ? 4 : 2);
     constexpr int nch = NCH;                  // 16-byte chunks per row (Cp / 8)
     constexpr int msk = (NCH >= 16 ? 16 : NCH) - 1;
     constexpr int PF = kBP * NCH / 256;       // prefetch chunks per thread for one target tile
@@ -281,6 +294,7 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16_2b(const bf16_t *__restri
                                                           long long col_begin, long long col_end, int nchunk,
                                                           float scale, int stpol) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    zero_guards(corr, Nq, row_stride, 2);
     constexpr int nch = NCH;
     constexpr int msk = (NCH >= 16 ? 16 : NCH) - 1;
     constexpr int PF = kBP * NCH / 256;
@@ -455,6 +469,7 @@ __global__ __launch_bounds__(256, 1) void k_build_f32(const float *__restrict__ 
     // features (C = 160..256) re-stage both tiles per chunk; the accumulation is still
     // one k-ordered fmaf chain per output, so the result does not depend on KC.
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    zero_guards(corr, Nq, row_stride, 4);
     const int KC = Cp < 128 ? Cp : 128;
     const bool resident = Cp <= 128;
     u32x2 *sQ = reinterpret_cast<u32x2 *>(smem);

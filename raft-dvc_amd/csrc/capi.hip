@@ -25,6 +25,7 @@ struct PyrGeo {
     int ncx, ncy, ncz;
 };
 template <typename T> __global__ void k_pack_pyramid(const float *, T *, PyrGeo);
+template <typename T> __global__ void k_pack_queries(const float *, T *, int, int, long long);
 template <int NCH, bool STORE_F32, int ABL>
 __global__ void k_build_bf16(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long, long long, long long,
                              long long, int, float);
@@ -321,11 +322,11 @@ int dvc_pack_queries(const float *fmap1, void *packed, int B, int C, int64_t Nq,
                                                (long long)Nq);
     const int Cp = (int)round_up(C, 32);
     hipStream_t s = (hipStream_t)stream;
-    dim3 grid((unsigned)ceil_div(Nq, 64), (unsigned)ceil_div(Cp, 64), (unsigned)B);
+    dim3 grid((unsigned)ceil_div(Nq, 64), (unsigned)ceil_div(Cp, 32), (unsigned)B);
     if (dtype == DVC_BF16)
-        k_pack_rows<bf16_t><<<grid, 256, 0, s>>>(fmap1, (bf16_t *)packed, C, Cp, (long long)C * Nq, Nq, 0, 0, 0, Nq);
+        k_pack_queries<bf16_t><<<grid, 256, 0, s>>>(fmap1, (bf16_t *)packed, C, Cp, Nq);
     else if (dtype == DVC_F32)
-        k_pack_rows<float><<<grid, 256, 0, s>>>(fmap1, (float *)packed, C, Cp, (long long)C * Nq, Nq, 0, 0, 0, Nq);
+        k_pack_queries<float><<<grid, 256, 0, s>>>(fmap1, (float *)packed, C, Cp, Nq);
     else
         return fail(DVC_ERR_INVALID, "pack_queries: bad dtype %d", dtype);
     return check_launch("pack_queries");
@@ -343,9 +344,8 @@ int dvc_pack_targets(const float *fmap2, void *packed, float *workspace, int B, 
     hipStream_t s = (hipStream_t)stream;
     const int Cp = lay.c_pad;
     const size_t esz = dtype == DVC_BF16 ? 2 : 4;
-    if (hipMemsetAsync(packed, 0, (size_t)B * lay.row_stride * Cp * esz, s) != hipSuccess)
-        return fail(DVC_ERR_RUNTIME, "pack_targets: memset failed");
-    if (num_levels <= 4 && g_pack_variant == 1) {   // one pass: every level of an 8^3 cell pooled in LDS (k_pack_pyramid)
+    if (num_levels <= 4 && g_pack_variant == 1) {   // one pass: every level of an 8^3 cell pooled in LDS (k_pack_pyramid,
+                                                     // which also zeroes the z-padding and tail rows)
         PyrGeo g;
         memset(&g, 0, sizeof(g));
         g.L = num_levels; g.C = C; g.Cp = Cp; g.row_stride = lay.row_stride;
@@ -358,6 +358,8 @@ int dvc_pack_targets(const float *fmap2, void *packed, float *workspace, int B, 
         else k_pack_pyramid<float><<<grid, 256, 0, s>>>(fmap2, (float *)packed, g);
         return check_launch("pack_targets");
     }
+    if (hipMemsetAsync(packed, 0, (size_t)B * lay.row_stride * Cp * esz, s) != hipSuccess)
+        return fail(DVC_ERR_RUNTIME, "pack_targets: memset failed");
     const float *src = fmap2;
     float *ws = workspace;
     for (int l = 0; l < num_levels; ++l) {

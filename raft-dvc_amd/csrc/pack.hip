@@ -212,8 +212,96 @@ __global__ __launch_bounds__(256) void k_pack_pyramid(const float *__restrict__ 
                 *reinterpret_cast<u32x4 *>(d) = u32x4{u[0], u[1], u[2], u[3]};
             }
         }
+        // z padding rows [D_l, Dp_l) of this cell's (Y, X) columns: zeroed by the cell holding z = D_l - 1
+        const int npad = g.Dp[l] - g.D[l];
+        if (npad > 0 && lz0 <= g.D[l] - 1 && g.D[l] - 1 < lz0 + e) {
+            for (int idx = t; idx < e * e * npad * NCK; idx += 256) {
+                const int ck = idx % NCK, r = idx / NCK;
+                const int zp = r % npad, yx = r / npad;
+                const int Y = ly0 + yx / e, X = lx0 + yx % e;
+                const int c = cg * kPyrCG + ck * 8;
+                if (Y >= g.H[l] || X >= g.W[l] || c >= g.Cp) continue;
+                T *d = db + (g.off[l] + ((long long)Y * g.W[l] + X) * g.Dp[l] + g.D[l] + zp) * g.Cp + c;
+                if constexpr (sizeof(T) == 4) {
+                    *reinterpret_cast<float4 *>(d) = float4{0.f, 0.f, 0.f, 0.f};
+                    *reinterpret_cast<float4 *>(d + 4) = float4{0.f, 0.f, 0.f, 0.f};
+                } else {
+                    *reinterpret_cast<u32x4 *>(d) = u32x4{0u, 0u, 0u, 0u};
+                }
+            }
+        }
+    }
+    // rows past the last level, up to row_stride: zeroed by the first cell
+    if (blockIdx.x == 0) {
+        const long long r0 = g.off[g.L - 1] + (long long)g.H[g.L - 1] * g.W[g.L - 1] * g.Dp[g.L - 1];
+        const long long nt = (g.row_stride - r0) * NCK;
+        for (long long idx = t; idx < nt; idx += 256) {
+            const long long r = r0 + idx / NCK;
+            const int c = cg * kPyrCG + (int)(idx % NCK) * 8;
+            if (c >= g.Cp) continue;
+            T *d = db + r * g.Cp + c;
+            if constexpr (sizeof(T) == 4) {
+                *reinterpret_cast<float4 *>(d) = float4{0.f, 0.f, 0.f, 0.f};
+                *reinterpret_cast<float4 *>(d + 4) = float4{0.f, 0.f, 0.f, 0.f};
+            } else {
+                *reinterpret_cast<u32x4 *>(d) = u32x4{0u, 0u, 0u, 0u};
+            }
+        }
     }
 }
+
+// Query rows: (B, C, Nq) float32 -> [B][Nq][Cp] dtype.  One block = 64 rows x 32 channels: 16-byte loads of
+// 4 consecutive positions of one channel (Nq % 4 == 0, else per-element), an LDS transpose, 16-byte stores
+// of 8 channels of one row.  Channels C..Cp-1 are written as zeros.
+template <typename T>
+__global__ __launch_bounds__(256) void k_pack_queries(const float *__restrict__ src, T *__restrict__ dst, int C,
+                                                      int Cp, long long Nq) {
+    __shared__ float tile[32][65];
+    const int b = blockIdx.z, t = threadIdx.x;
+    const long long j0 = (long long)blockIdx.x * 64;
+    const int c0 = blockIdx.y * 32;
+    const float *sb = src + (long long)b * C * Nq;
+    {
+        const int k = t >> 3, p = (t & 7) * 8;   // channel c0 + k, positions j0 + p .. + 7
+        const int c = c0 + k;
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = 0.0f;
+        if (c < C) {
+            const float *row = sb + (long long)c * Nq + j0 + p;
+            if ((Nq & 3) == 0 && j0 + p + 8 <= Nq) {
+                const float4 a = *reinterpret_cast<const float4 *>(row);
+                const float4 bq = *reinterpret_cast<const float4 *>(row + 4);
+                v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = bq.x; v[5] = bq.y; v[6] = bq.z; v[7] = bq.w;
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v[i] = j0 + p + i < Nq ? row[i] : 0.0f;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) tile[k][p + i] = v[i];
+    }
+    __syncthreads();
+    const int r = t >> 2, ck = (t & 3) * 8;      // row j0 + r, channels c0 + ck .. + 7
+    const long long j = j0 + r;
+    if (j >= Nq || c0 + ck >= Cp) return;
+    T *d = dst + ((long long)b * Nq + j) * Cp + c0 + ck;
+    float w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = tile[ck + i][r];
+    if constexpr (sizeof(T) == 4) {
+        *reinterpret_cast<float4 *>(d) = float4{w[0], w[1], w[2], w[3]};
+        *reinterpret_cast<float4 *>(d + 4) = float4{w[4], w[5], w[6], w[7]};
+    } else {
+        unsigned u[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) u[k] = (unsigned)f32_to_bf16(w[2 * k]) | ((unsigned)f32_to_bf16(w[2 * k + 1]) << 16);
+        *reinterpret_cast<u32x4 *>(d) = u32x4{u[0], u[1], u[2], u[3]};
+    }
+}
+
+template __global__ void k_pack_queries<float>(const float *, float *, int, int, long long);
+template __global__ void k_pack_queries<bf16_t>(const float *, bf16_t *, int, int, long long);
 
 template __global__ void k_pack_pyramid<float>(const float *, float *, PyrGeo);
 template __global__ void k_pack_pyramid<bf16_t>(const float *, bf16_t *, PyrGeo);

@@ -64,12 +64,13 @@ def pack_queries(fmap1_slab: torch.Tensor, dtype: int) -> torch.Tensor:
     return out
 
 
-def pack_targets(fmap2: torch.Tensor, num_levels: int, dtype: int) -> torch.Tensor:
+def pack_targets(fmap2: torch.Tensor, num_levels: int, dtype: int, out: torch.Tensor = None) -> torch.Tensor:
     _need_cuda(fmap2)
     f = _f32c(fmap2)
     B, C, H, W, D = f.shape
     lay = layout(H, W, D, num_levels, C)
-    out = torch.empty((B, lay.row_stride, lay.c_pad), dtype=_TORCH_DT[dtype], device=f.device)
+    if out is None:
+        out = torch.empty((B, lay.row_stride, lay.c_pad), dtype=_TORCH_DT[dtype], device=f.device)
     nws = lib().dvc_pack_workspace_bytes(B, C, H, W, D, num_levels)
     ws = torch.empty((max(nws, 4) // 4,), dtype=torch.float32, device=f.device)
     check(lib().dvc_pack_targets(_ptr(f), _ptr(out), _ptr(ws), B, C, H, W, D, num_levels, dtype, _stream(f)),
@@ -81,14 +82,13 @@ GUARD_BYTES = 256   # DVC_CORR_GUARD_BYTES
 
 
 def alloc_corr(B: int, Nq: int, row_stride: int, store_dtype: int, device, zero: bool = False) -> torch.Tensor:
-    """(B, Nq, row_stride) corr buffer with zeroed DVC_CORR_GUARD_BYTES guards on both sides."""
+    """(B, Nq, row_stride) corr buffer with DVC_CORR_GUARD_BYTES of guard space on both sides (dvc_corr_build
+    zeroes the guards; zero=True zeroes the whole buffer, for the pooled build whose build call covers only
+    level 0's columns)."""
     dt = _TORCH_DT[store_dtype]
     g = GUARD_BYTES // torch.tensor([], dtype=dt).element_size()
     n = B * Nq * row_stride
     buf = (torch.zeros if zero else torch.empty)((n + 2 * g,), dtype=dt, device=device)
-    if not zero:
-        buf[:g].zero_()
-        buf[g + n:].zero_()
     return buf[g:g + n].view(B, Nq, row_stride)
 
 

@@ -285,9 +285,12 @@ def test_single_pass_pack_matches_per_level(shape, C, L):
     H, W, D = shape
     g = torch.Generator(device="cpu").manual_seed(H + W + D + C + L)
     f2 = torch.randn(2, C, H, W, D, generator=g).to(DEV)
+    lay = ops.layout(H, W, D, L, C)
     for prec in ("bf16", "fp32"):
         dt = ops.dtype_code(prec)
-        new = ops.pack_targets(f2, L, dt)
+        # every row (voxels, z padding, the tail up to row_stride) must be written: start from NaN
+        new = torch.full((2, lay.row_stride, lay.c_pad), float("nan"), dtype=ops._TORCH_DT[dt], device=DEV)
+        ops.pack_targets(f2, L, dt, out=new)
         try:
             _lib.set_tuning("pack_variant", 0)
             old = ops.pack_targets(f2, L, dt)
