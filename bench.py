@@ -471,6 +471,8 @@ def main():
                   "TFLOP/s": round(bd_flops / (bd_avg * 1e-3) / 1e12, 1) if bd_avg and bd_flops else None}
 
     tail = flow_tail(args, coords_slab, S, B, dev, stream, _lib, dvccorr)
+    bwd = backward_timing(args, f1_slab, f2_slab, coords_slab, dims, dev, stream) \
+        if world == 1 and not shard_diag and args.convc1 is None else None
 
     detail = None
     if dist and strong and not args.no_extras:
@@ -504,6 +506,7 @@ def main():
             "build": build_info,
             "lookup_avg_ms": round(lk_avg, 4),
             "flow_step": tail,
+            "backward": bwd,
             "cpu_baseline": cpu,
         }
         if detail is not None:
@@ -511,6 +514,45 @@ def main():
         print(json.dumps(line), flush=True)
     if dist:
         torch.distributed.destroy_process_group()
+
+
+def backward_timing(args, f1, f2, coords, dims, dev, stream):
+    """The training path's backward (dvc_corr_backward: d fmap1, d fmap2 of one lookup; autograd through
+    corr.py:141-208), HIP-event timed outside the timed region on the bench's inputs and a random output
+    gradient.  Algorithmic bytes: read grad_out (fp32) + coords + the packed query/target rows, write
+    d fmap1 + d fmap2 (fp32); FLOPs: 2 x 2 C per window dot (d fmap1 and d fmap2), (2r+2)^3 window dots
+    per query and level."""
+    from dvccorr import ops
+    with torch.no_grad():
+        B, C = f1.shape[:2]
+        S = args.size
+        L, R = args.levels, args.radius
+        Nq = f1[0, 0].numel()
+        dt = ops.dtype_code(args.precision)
+        q = ops.pack_queries(f1.reshape(B, C, -1), dt)
+        t = ops.pack_targets(f2, L, dt)
+        g = torch.Generator(device=dev).manual_seed(99)
+        gout = torch.randn(B, L * (2 * R + 1) ** 3, Nq, device=dev, generator=g)
+        cf = coords[0].reshape(B, 3, -1).contiguous()
+        for _ in range(2):
+            ops.corr_backward(q, t, cf, gout, C, S, S, S, L, R, False, dt)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        n = 5
+        a.record(stream)
+        for _ in range(n):
+            ops.corr_backward(q, t, cf, gout, C, S, S, S, L, R, False, dt)
+        b.record(stream)
+        torch.cuda.synchronize()
+        ms = a.elapsed_time(b) / n
+    esz = 2 if args.precision == "bf16" else 4
+    nbytes = gout.numel() * 4 + cf.numel() * 4 + (q.numel() + t.numel()) * esz + 2 * B * C * Nq * 4
+    flops = 2.0 * 2 * C * (2 * R + 2) ** 3 * L * B * Nq
+    peak = BF16_PEAK_TFS if args.precision == "bf16" else F32_PEAK_TFS
+    return {"kernels": "k_win_grad + k_grad_q + radix sort + k_grad_t + k_unpack_sum (dvc_corr_backward)",
+            "avg_ms": round(ms, 4), "algorithmic_bytes": nbytes, "GB/s": round(nbytes / (ms * 1e-3) / 1e9, 1),
+            "hbm_frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "flops": flops,
+            "TFLOP/s": round(flops / (ms * 1e-3) / 1e12, 2),
+            "mfma_frac": round(flops / (ms * 1e-3) / 1e12 / peak, 4)}
 
 
 def flow_tail(args, coords_slab, S, B, dev, stream, _lib, dvccorr):

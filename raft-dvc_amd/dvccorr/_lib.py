@@ -11,7 +11,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdvccorr.so")
+# DVCCORR_LIB (diagnostics): load another in-tree build of the same ABI, e.g. for A/B kernel timing
+LIB_PATH = os.environ.get("DVCCORR_LIB") or os.path.join(_HERE, "libdvccorr.so")
 
 DVC_OK, DVC_ERR_INVALID, DVC_ERR_UNSUPPORTED, DVC_ERR_LAUNCH, DVC_ERR_RUNTIME = range(5)
 DVC_F32, DVC_BF16 = 0, 1
