@@ -203,7 +203,8 @@ __device__ __forceinline__ void fma_partners(f32x2 (&acc)[64], float (*gs)[64], 
         }
 }
 
-constexpr int kBatch = 4;   // partners staged per LDS round
+constexpr int kBatch = 4;    // partners staged per LDS round (k_grad_q)
+constexpr int kTBatch = 8;   // partners per pipelined group (k_grad_t)
 
 // ---------------------------------------------------------------------------------
 // 2. dQ for one 4x4x4 box of queries (owner lane i = query i), summed over levels.
@@ -322,19 +323,24 @@ __global__ __launch_bounds__(256) void k_cell_starts(const unsigned long long *_
 // target i), streaming the queries whose window origin cell lies in
 // [brick, brick + NW - 1] (per axis, in o' coordinates).
 // ---------------------------------------------------------------------------------
+// nsplit > 1 (coarse levels: a handful of bricks, each reached by most queries): workgroup
+// (brick, split) takes the origin rows row = 4 split + wave (mod 4 nsplit) and writes its partial
+// sums to dTp[split][brick][64][Cp]; k_grad_t_reduce adds the nsplit partials in split order.
 template <typename TT, int R>
 __global__ __launch_bounds__(256) void k_grad_t(const TT *__restrict__ Qp, const unsigned long long *__restrict__ keys,
-                                                const int *__restrict__ starts, float *__restrict__ dT, BwdArgs A,
-                                                int b, int l) {
+                                                const int *__restrict__ starts, float *__restrict__ dT,
+                                                float *__restrict__ dTp, int nsplit, BwdArgs A, int b, int l) {
     constexpr int NW = 2 * R + 2, NW3 = NW * NW * NW;
-    __shared__ __attribute__((aligned(16))) float gs_all[4][kBatch][64];
+    __shared__ __attribute__((aligned(16))) float gs_all[4][kTBatch][64];
     __shared__ __attribute__((aligned(16))) f32x2 red[2][64][64];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float (*gs)[64] = gs_all[w];
     const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
     const int nbz = (Dl + 3) >> 2, nbx = (Wl + 3) >> 2;
-    int t = blockIdx.x;
+    const int split = (int)(blockIdx.x % nsplit);
+    const int brick = (int)(blockIdx.x / nsplit);
+    int t = brick;
     const int bz = t % nbz; t /= nbz;
     const int bx = t % nbx;
     const int by = t / nbx;
@@ -352,36 +358,62 @@ __global__ __launch_bounds__(256) void k_grad_t(const TT *__restrict__ Qp, const
     f32x2 acc[64];
 #pragma unroll
     for (int i = 0; i < 64; ++i) acc[i] = f32x2{0.0f, 0.0f};
-    for (int row = w; row < nrows; row += 4) {
+    // Queries are streamed 64 keys at a time (one coalesced key load per lane, broadcast with
+    // shuffles) in groups of kTBatch partners, the loads of group k+1 in flight while group k's
+    // 64 x kTBatch FMAs run: the loop is bound by its dependent gathers otherwise.
+    for (int row = 4 * split + w; row < nrows; row += 4 * nsplit) {
         const int oy = oy0 + row / nox, ox = ox0 + row % nox;
         const long long cbase = ((long long)oy * CX + ox) * CZ;
         const int s = starts[cbase + oz0], e = starts[cbase + oz1 + 1];
         // window position of this lane's target for a query of origin o' = (oy, ox, ozq)
         const int py = ty - oy + NW - 1, px = tx - ox + NW - 1;
         const bool yxok = tval && (unsigned)py < (unsigned)NW && (unsigned)px < (unsigned)NW;
-        for (int idx = s; idx < e; idx += kBatch) {
-            float g[kBatch];
-            f32x2 qv[kBatch];
+        const int pyx = (py * NW + px) * NW;
+        for (int base = s; base < e; base += 64) {
+            const int nk = min(64, e - base);
+            const unsigned long long key = lane < nk ? keys[base + lane] : 0ull;
+            const int qq_l = (int)(unsigned)(key & 0xffffffffu);
+            const int oz_l = (int)((long long)(key >> 32) - cbase);
+            auto fetch = [&](int k0, float (&g)[kTBatch], f32x2 (&qv)[kTBatch]) {
 #pragma unroll
-            for (int k = 0; k < kBatch; ++k) {
-                const bool in = idx + k < e;
-                const unsigned long long key = keys[in ? idx + k : s];
-                const long long qq = (long long)(unsigned)(key & 0xffffffffu);
-                const int ozq = (int)((long long)(key >> 32) - cbase);
-                const int pz = tz - ozq + NW - 1;
-                const bool ok = in && yxok && (unsigned)pz < (unsigned)NW;
-                g[k] = ok ? gl[qq * NW3 + (py * NW + px) * NW + pz] : 0.0f;
-                qv[k] = (in && cok) ? load2<TT>(qb + qq * A.Cp) : f32x2{0.0f, 0.0f};
+                for (int k = 0; k < kTBatch; ++k) {
+                    const int idx = k0 + k;
+                    const bool in = idx < nk;
+                    const int qq = __shfl(qq_l, in ? idx : 0);
+                    const int pz = tz - __shfl(oz_l, in ? idx : 0) + NW - 1;
+                    const bool ok = in && yxok && (unsigned)pz < (unsigned)NW;
+                    g[k] = ok ? gl[(long long)qq * NW3 + pyx + pz] : 0.0f;
+                    qv[k] = (in && cok) ? load2<TT>(qb + (long long)qq * A.Cp) : f32x2{0.0f, 0.0f};
+                }
+            };
+            auto consume = [&](const float (&g)[kTBatch], const f32x2 (&qv)[kTBatch]) {
+#pragma unroll
+                for (int k = 0; k < kTBatch; ++k) gs[k][lane] = g[k];
+                __builtin_amdgcn_wave_barrier();
+                fma_partners<kTBatch>(acc, gs, qv);
+                __builtin_amdgcn_wave_barrier();
+            };
+            float ga[kTBatch], gb[kTBatch];
+            f32x2 qa[kTBatch], qb2[kTBatch];
+            fetch(0, ga, qa);
+            for (int k0 = 0; k0 < nk; k0 += 2 * kTBatch) {
+                if (k0 + kTBatch < nk) fetch(k0 + kTBatch, gb, qb2);
+                consume(ga, qa);
+                if (k0 + kTBatch < nk) {
+                    if (k0 + 2 * kTBatch < nk) fetch(k0 + 2 * kTBatch, ga, qa);
+                    consume(gb, qb2);
+                }
             }
-#pragma unroll
-            for (int k = 0; k < kBatch; ++k) gs[k][lane] = g[k];
-            __builtin_amdgcn_wave_barrier();
-            fma_partners<kBatch>(acc, gs, qv);
-            __builtin_amdgcn_wave_barrier();
         }
     }
     reduce4(acc, red, w, lane);
     if (w == 0 && cok) {
+        if (nsplit > 1) {
+            float *pp = dTp + ((long long)split * gridDim.x / nsplit + brick) * 64 * A.Cp + c0;
+#pragma unroll
+            for (int i = 0; i < 64; ++i) *reinterpret_cast<f32x2 *>(pp + (long long)i * A.Cp) = acc[i];
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < 64; ++i) {
             const int y = by * 4 + (i >> 4), x = bx * 4 + ((i >> 2) & 3), z = bz * 4 + (i & 3);
@@ -391,6 +423,28 @@ __global__ __launch_bounds__(256) void k_grad_t(const TT *__restrict__ Qp, const
             }
         }
     }
+}
+
+// dT rows of level l <- scale * sum over the nsplit partials (split order: deterministic).  One thread per
+// (brick target, channel pair).
+__global__ __launch_bounds__(256) void k_grad_t_reduce(const float *__restrict__ dTp, float *__restrict__ dT,
+                                                       int nsplit, int nbricks, BwdArgs A, int b, int l) {
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    const int cp2 = A.Cp / 2;
+    if (idx >= (long long)nbricks * 64 * cp2) return;
+    const int c0 = 2 * (int)(idx % cp2);
+    const int i = (int)((idx / cp2) % 64);
+    const int brick = (int)(idx / (cp2 * 64LL));
+    const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
+    const int nbz = (Dl + 3) >> 2, nbx = (Wl + 3) >> 2;
+    const int bz = brick % nbz, bx = (brick / nbz) % nbx, by = brick / (nbz * nbx);
+    const int y = by * 4 + (i >> 4), x = bx * 4 + ((i >> 2) & 3), z = bz * 4 + (i & 3);
+    if (y >= Hl || x >= Wl || z >= Dl) return;
+    f32x2 acc = {0.0f, 0.0f};
+    for (int sp = 0; sp < nsplit; ++sp)
+        acc += *reinterpret_cast<const f32x2 *>(dTp + (((long long)sp * nbricks + brick) * 64 + i) * A.Cp + c0);
+    const long long row = (long long)b * A.row_stride + A.off[l] + ((long long)y * Wl + x) * Dpl + z;
+    *reinterpret_cast<f32x2 *>(dT + row * A.Cp + c0) = acc * f32x2{A.scale, A.scale};
 }
 
 // ---------------------------------------------------------------------------------
@@ -447,8 +501,18 @@ __global__ __launch_bounds__(256) void k_unpack_sum(UnpackArgs U) {
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct BwdPlan {
-    size_t gwin, dq, dt, keys, starts, temp, total;
+    size_t gwin, dq, dt, keys, starts, temp, part, total;
 };
+
+// k_grad_t split factor of level l: enough (brick, split) workgroups for ~2 per CU, at most one origin
+// row per wave and split
+static int grad_t_splits(const dvc_layout &lay, int l, int NW) {
+    const long long bricks = (long long)((lay.H[l] + 3) / 4) * ((lay.W[l] + 3) / 4) * ((lay.D[l] + 3) / 4);
+    const long long rows = (long long)(std::min(lay.H[l], 4) + NW - 1) * (std::min(lay.W[l], 4) + NW - 1);
+    long long sp = (512 + bricks - 1) / bricks;
+    sp = std::min(sp, std::max(1LL, rows / 4));
+    return (int)std::max(1LL, std::min(sp, 256LL));
+}
 
 static long long max_cells(const dvc_layout &lay, int NW) {
     long long m = 0;
@@ -469,7 +533,14 @@ static void bwd_plan(int B, long long Nq, const dvc_layout &lay, int radius, Bwd
     (void)rocprim::radix_sort_keys(nullptr, tb, (unsigned long long *)nullptr, (unsigned long long *)nullptr,
                                    (size_t)Nq, 0u, 64u, (hipStream_t)0);
     P.temp = al256(tb);
-    P.total = P.gwin + P.dq + P.dt + 2 * P.keys + P.starts + P.temp;
+    size_t part = 0;
+    for (int l = 0; l < lay.num_levels; ++l) {
+        const int sp = grad_t_splits(lay, l, NW);
+        const long long bricks = (long long)((lay.H[l] + 3) / 4) * ((lay.W[l] + 3) / 4) * ((lay.D[l] + 3) / 4);
+        if (sp > 1) part = std::max<size_t>(part, (size_t)sp * (size_t)bricks * 64 * (size_t)lay.c_pad * sizeof(float));
+    }
+    P.part = al256(std::max<size_t>(part, 256));
+    P.total = P.gwin + P.dq + P.dt + 2 * P.keys + P.starts + P.temp + P.part;
 }
 
 size_t backward_workspace_bytes(int B, long long Nq, const dvc_layout &lay, int radius) {
@@ -488,6 +559,7 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     unsigned long long *kout = (unsigned long long *)(ws + P.gwin + P.dq + P.dt + P.keys);
     int *starts = (int *)(ws + P.gwin + P.dq + P.dt + 2 * P.keys);
     void *temp = ws + P.gwin + P.dq + P.dt + 2 * P.keys + P.starts;
+    float *dtp = (float *)(ws + P.gwin + P.dq + P.dt + 2 * P.keys + P.starts + P.temp);
     A.gwin = (float *)ws;
     auto launched = [&](const char *what) {
         hipError_t e = hipGetLastError();
@@ -519,8 +591,14 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
             k_cell_starts<<<(unsigned)((A.Nq + 1 + 255) / 256), 256, 0, s>>>(kout, A.Nq, ncell, starts);
             if (!launched("cell_starts")) return DVC_ERR_LAUNCH;
             const long long bricks = (long long)((A.H[l] + 3) / 4) * ((A.W[l] + 3) / 4) * ((A.D[l] + 3) / 4);
-            k_grad_t<TT, R><<<(unsigned)bricks, 256, 0, s>>>(Q, kout, starts, dt, A, b, l);
+            const int sp = grad_t_splits(lay, l, NW);
+            k_grad_t<TT, R><<<(unsigned)(bricks * sp), 256, 0, s>>>(Q, kout, starts, dt, dtp, sp, A, b, l);
             if (!launched("grad_t")) return DVC_ERR_LAUNCH;
+            if (sp > 1) {
+                const long long nt = bricks * 64 * (A.Cp / 2);
+                k_grad_t_reduce<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(dtp, dt, sp, (int)bricks, A, b, l);
+                if (!launched("grad_t_reduce")) return DVC_ERR_LAUNCH;
+            }
         }
     // dfmap1 (B, C, Nq) <- dQ
     UnpackArgs U{};
