@@ -138,8 +138,9 @@ int dvc_corr_lookup_fused(const void *packed_q, const void *packed_t, const floa
  *   grad_fmap2 (B, C, H, W, D) float32       overwritten (these Nq queries' contribution)
  * packed_q / packed_t are the forward's packed operands (dtype).  No atomics: every
  * sum runs in a fixed order, so results are bitwise reproducible.  Supported:
- * radius 1..6, c_pad <= 128, Nq a multiple of W*D, and for the legacy convention
- * W == D at every non-zero level (DVC_ERR_UNSUPPORTED otherwise). */
+ * radius 1..6, c_pad <= 128, Nq a multiple of W*D (DVC_ERR_UNSUPPORTED otherwise);
+ * both conventions on every level shape (legacy levels with W != D use a stretched
+ * window box).  The workspace size covers either convention. */
 size_t dvc_corr_backward_workspace_bytes(int B, int64_t Nq, int C, int H, int W, int D, int num_levels, int radius);
 int dvc_corr_backward(const void *packed_q, const void *packed_t, const float *coords, const float *grad_out,
                       float *grad_fmap1, float *grad_fmap2, void *workspace, int B, int64_t Nq, int C, int H, int W,

@@ -22,9 +22,16 @@
 //   k_unpack_sum  dfmap1 (B, C, Nq) <- dQ, and dfmap2 (B, C, H, W, D) <- sum_l 8^-l dT_l
 //                 (the adjoint of the floor-mode 2x2x2 avg_pool3d pyramid).
 // Every sum runs in a fixed order, so the result is bitwise reproducible.
+//
+// Legacy levels with W != D (grid channels [2,0,1] normalised by one axis' size and
+// unnormalised by the other's, corr.py:49-50 + grid_sample): the samples along W step by
+// (W-1)/(D-1) and along D by the inverse, so a query's footprint is an nwh x nwu x nwv box
+// (host-sized per level, win_dims) anchored at the floor of its first sample per axis;
+// k_win_grad_generic fills it and the other kernels read the per-level box sizes.
 #include <stdio.h>
 
 #include <algorithm>
+#include <cmath>
 
 #include <rocprim/device/device_radix_sort.hpp>
 
@@ -38,13 +45,19 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 struct BwdArgs {
     const float *coords;   // (B, 3, Nq)
     const float *gout;     // (B, L*n^3, Nq)
-    float *gwin;           // [B][L][Nq][NW^3]
+    float *gwin;           // level l at goff[l]: [B][Nq][nwh * nwu * nwv]
     long long Nq, row_stride;
     int B, L, legacy, Hq, Wq, Dq, Cp;
     int H[DVC_MAX_LEVELS], W[DVC_MAX_LEVELS], D[DVC_MAX_LEVELS], Dp[DVC_MAX_LEVELS], zero[DVC_MAX_LEVELS];
-    long long off[DVC_MAX_LEVELS];
+    int generic[DVC_MAX_LEVELS];                                  // legacy level with W != D
+    int nwh[DVC_MAX_LEVELS], nwu[DVC_MAX_LEVELS], nwv[DVC_MAX_LEVELS];   // window box per level (2r+2 each if not generic)
+    long long off[DVC_MAX_LEVELS], goff[DVC_MAX_LEVELS];
     float scale;
 };
+
+__device__ __forceinline__ long long bw_nw3(const BwdArgs &A, int l) {
+    return (long long)A.nwh[l] * A.nwu[l] * A.nwv[l];
+}
 
 __device__ __forceinline__ int bw_wave_min(int v) {
 #pragma unroll
@@ -61,6 +74,24 @@ __device__ __forceinline__ int bw_wave_max(int v) {
 __device__ __forceinline__ void bw_axes(const BwdArgs &A, int l, float cy, float cx, float cz, WinAxes &ax) {
     const float sc = (float)(1 << l);
     window_axes(cy / sc, cx / sc, cz / sc, A.H[l], A.W[l], A.D[l], A.legacy, ax);
+}
+
+// window origin (first cell) per axis: floor(p) - R, or for a generic level the floor of the first sample
+__device__ __forceinline__ int bw_floor_sample(float p, int R, float sn, float su) {
+    const float x = roundtrip(p + (float)(-R), sn, su);
+    return (int)floorf(fminf(fmaxf(x, -1e8f), 1e8f));
+}
+__device__ __forceinline__ void bw_origin(const BwdArgs &A, int l, int R, const WinAxes &ax, int &oh, int &ou,
+                                          int &ov) {
+    if (A.generic[l]) {
+        oh = bw_floor_sample(ax.ph, R, ax.hs, ax.hs);
+        ou = bw_floor_sample(ax.pu, R, ax.un, ax.uu);
+        ov = bw_floor_sample(ax.pv, R, ax.vn, ax.vu);
+    } else {
+        oh = (int)ax.kh - R;
+        ou = (int)ax.ku - R;
+        ov = (int)ax.kv - R;
+    }
 }
 
 template <typename TT> __device__ __forceinline__ f32x2 load2(const TT *p);
@@ -87,8 +118,8 @@ __global__ __launch_bounds__(256) void k_win_grad(BwdArgs A) {
     const int bl = (int)(item / nqb);
     const int l = bl % A.L, b = bl / A.L;
     const long long q = (item - (long long)bl * nqb) * 64 + lane;
-    if (q >= A.Nq) return;
-    float *gw = A.gwin + ((long long)bl * A.Nq + q) * NW3;
+    if (q >= A.Nq || A.generic[l]) return;   // generic levels: k_win_grad_generic
+    float *gw = A.gwin + A.goff[l] + ((long long)b * A.Nq + q) * NW3;
     if (A.zero[l]) {   // a size-1 level samples zeros (corr.py:41-44): no gradient reaches it
         for (int i = 0; i < NW3; i += 2) *reinterpret_cast<f32x2 *>(gw + i) = f32x2{0.0f, 0.0f};
         return;
@@ -162,6 +193,81 @@ __global__ __launch_bounds__(256) void k_win_grad(BwdArgs A) {
     }
 }
 
+// Generic (legacy W != D) levels: lane = query; the window box is zeroed, then every output's
+// (up to) 8 in-range corners are added in output order with grid_sample's weights
+// (tri_sample in common.h).  The box is private to the lane: no atomics, fixed order.
+template <int R>
+__global__ __launch_bounds__(256) void k_win_grad_generic(BwdArgs A) {
+    constexpr int n = 2 * R + 1;
+    const int lane = threadIdx.x & 63;
+    const long long nqb = (A.Nq + 63) / 64;
+    const long long item = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (item >= (long long)A.B * A.L * nqb) return;
+    const int bl = (int)(item / nqb);
+    const int l = bl % A.L, b = bl / A.L;
+    const long long q = (item - (long long)bl * nqb) * 64 + lane;
+    if (q >= A.Nq || !A.generic[l]) return;
+    const int nh = A.nwh[l], nu = A.nwu[l], nv = A.nwv[l];
+    const long long nw3 = bw_nw3(A, l);
+    float *gw = A.gwin + A.goff[l] + ((long long)b * A.Nq + q) * nw3;
+    for (long long i = 0; i < nw3; ++i) gw[i] = 0.0f;
+    if (A.zero[l]) return;
+    const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l];
+    float cy, cx, cz;
+    load_coords(A.coords, b, A.Nq, q, cy, cx, cz);
+    WinAxes ax;
+    bw_axes(A, l, cy, cx, cz, ax);
+    int oh, ou, ov;
+    bw_origin(A, l, R, ax, oh, ou, ov);
+    // per axis and offset t: window index of the low corner and the two corner weights (0 when the corner
+    // lies outside the level, where grid_sample's zero padding gives it no gradient)
+    auto corner = [&](float p, int t, float sn, float su, int o, int S, int nw, int &j, float &w0, float &w1) {
+#pragma clang fp contract(off)
+        const float x = roundtrip(p + (float)(t - R), sn, su);
+        j = 0; w0 = 0.0f; w1 = 0.0f;
+        if (!(fabsf(x) < 1e7f)) return;   // tri_sample: NaN / huge index samples nothing
+        const float fx = floorf(x);
+        const int k = (int)fx;
+        if (k - o < 0 || k - o + 1 >= nw) return;   // outside the box: only far outside the level
+        j = k - o;
+        w1 = (unsigned)(k + 1) < (unsigned)S ? x - fx : 0.0f;
+        w0 = (unsigned)k < (unsigned)S ? (fx + 1.0f) - x : 0.0f;
+    };
+    int ju[n], jv[n];
+    float wu0[n], wu1[n], wv0[n], wv1[n];
+#pragma unroll
+    for (int t = 0; t < n; ++t) {
+        corner(ax.pu, t, ax.un, ax.uu, ou, Wl, nu, ju[t], wu0[t], wu1[t]);
+        corner(ax.pv, t, ax.vn, ax.vu, ov, Dl, nv, jv[t], wv0[t], wv1[t]);
+    }
+    const long long chu = A.legacy ? 1 : n, chv = A.legacy ? n : 1;
+    const float *g = A.gout + (long long)bl * n * n * n * A.Nq + q;
+    for (int a = 0; a < n; ++a) {
+        int jh;
+        float wh0, wh1;
+        corner(ax.ph, a, ax.hs, ax.hs, oh, Hl, nh, jh, wh0, wh1);
+        if (wh0 == 0.0f && wh1 == 0.0f) continue;
+        const float *ga = g + (long long)a * n * n * A.Nq;
+#pragma unroll
+        for (int tu = 0; tu < n; ++tu) {
+            if (wu0[tu] == 0.0f && wu1[tu] == 0.0f) continue;
+#pragma unroll
+            for (int tv = 0; tv < n; ++tv) {
+                const float gv = ga[(tu * chu + tv * chv) * A.Nq];
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    const float w = ((c & 1 ? wu1[tu] : wu0[tu]) * (c & 2 ? wh1 : wh0)) * (c & 4 ? wv1[tv] : wv0[tv]);
+                    if (w != 0.0f) {
+                        float *d = gw + ((long long)(jh + ((c >> 1) & 1)) * nu + ju[tu] + (c & 1)) * nv + jv[tv] +
+                                   ((c >> 2) & 1);
+                        *d = __builtin_fmaf(w, gv, *d);
+                    }
+                }
+            }
+        }
+    }
+}
+
 // Cross-wave sum of the four waves' 64 x (2 channels) partials: waves 2, 3 -> LDS ->
 // waves 0, 1; wave 1 -> LDS -> wave 0.  Fixed order (deterministic).  Every wave of the
 // block must call it.
@@ -211,7 +317,6 @@ constexpr int kTBatch = 8;   // partners per pipelined group (k_grad_t)
 // ---------------------------------------------------------------------------------
 template <typename TT, int R>
 __global__ __launch_bounds__(256) void k_grad_q(const TT *__restrict__ Tt, float *__restrict__ dQ, BwdArgs A) {
-    constexpr int NW = 2 * R + 2, NW3 = NW * NW * NW;
     __shared__ __attribute__((aligned(16))) float gs_all[4][kBatch][64];
     __shared__ __attribute__((aligned(16))) f32x2 red[2][64][64];
     const int lane = threadIdx.x & 63;
@@ -237,23 +342,25 @@ __global__ __launch_bounds__(256) void k_grad_q(const TT *__restrict__ Tt, float
     for (int l = 0; l < A.L; ++l) {
         if (A.zero[l]) continue;
         const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
+        const int nh = A.nwh[l], nu = A.nwu[l], nv = A.nwv[l];
         WinAxes ax;
         bw_axes(A, l, cy, cx, cz, ax);
-        const int ih = (int)ax.kh - R, iu = (int)ax.ku - R, iv = (int)ax.kv - R;
+        int ih, iu, iv;
+        bw_origin(A, l, R, ax, ih, iu, iv);
         const bool live = active && !ax.dead;
-        const int ys = max(bw_wave_min(live ? ih : BIG), 0), ye = min(bw_wave_max(live ? ih : -BIG) + NW - 1, Hl - 1);
-        const int xs = max(bw_wave_min(live ? iu : BIG), 0), xe = min(bw_wave_max(live ? iu : -BIG) + NW - 1, Wl - 1);
+        const int ys = max(bw_wave_min(live ? ih : BIG), 0), ye = min(bw_wave_max(live ? ih : -BIG) + nh - 1, Hl - 1);
+        const int xs = max(bw_wave_min(live ? iu : BIG), 0), xe = min(bw_wave_max(live ? iu : -BIG) + nu - 1, Wl - 1);
         const int nx = xe - xs + 1;
         const int nrows = (ye >= ys && nx > 0) ? (ye - ys + 1) * nx : 0;
-        const float *gq = A.gwin + (((long long)b * A.L + l) * A.Nq + q) * NW3;
+        const float *gq = A.gwin + A.goff[l] + ((long long)b * A.Nq + q) * bw_nw3(A, l);
         for (int row = w; row < nrows; row += 4) {
             const int y = ys + row / nx, x = xs + row % nx;
             const int wy = y - ih, wx = x - iu;
-            const bool rok = live && (unsigned)wy < (unsigned)NW && (unsigned)wx < (unsigned)NW;
+            const bool rok = live && (unsigned)wy < (unsigned)nh && (unsigned)wx < (unsigned)nu;
             if (__ballot(rok) == 0) continue;
             const int zlo = max(bw_wave_min(rok ? iv : BIG), 0);
-            const int zhi = min(bw_wave_max(rok ? iv : -BIG) + NW - 1, Dl - 1);
-            const float *grow = gq + (wy * NW + wx) * NW;
+            const int zhi = min(bw_wave_max(rok ? iv : -BIG) + nv - 1, Dl - 1);
+            const float *grow = gq + (wy * nu + wx) * nv;
             const TT *trow = Tt + ((long long)b * A.row_stride + A.off[l] + ((long long)y * Wl + x) * Dpl) * A.Cp + c0;
             for (int z = zlo; z <= zhi; z += kBatch) {
                 float g[kBatch];
@@ -262,7 +369,7 @@ __global__ __launch_bounds__(256) void k_grad_q(const TT *__restrict__ Tt, float
                 for (int k = 0; k < kBatch; ++k) {
                     const int zz = z + k;
                     const int wz = zz - iv;
-                    g[k] = (rok && zz <= zhi && (unsigned)wz < (unsigned)NW) ? grow[wz] : 0.0f;
+                    g[k] = (rok && zz <= zhi && (unsigned)wz < (unsigned)nv) ? grow[wz] : 0.0f;
                     tv[k] = (cok && zz <= zhi) ? load2<TT>(trow + (long long)zz * A.Cp) : f32x2{0.0f, 0.0f};
                 }
 #pragma unroll
@@ -288,20 +395,21 @@ __global__ __launch_bounds__(256) void k_grad_q(const TT *__restrict__ Tt, float
 }
 
 // ---------------------------------------------------------------------------------
-// 3. queries of (b, l) keyed by window-origin cell: o' = origin + NW - 1 per axis, in
-// [0, S_l + NW - 2] exactly when the window meets the level; others sort last.
+// 3. queries of (b, l) keyed by window-origin cell: o' = origin + nw - 1 per axis, in
+// [0, S_l + nw - 2] exactly when the window meets the level; others sort last.
 // ---------------------------------------------------------------------------------
 template <int R>
 __global__ __launch_bounds__(256) void k_bw_keys(BwdArgs A, int b, int l, unsigned long long *__restrict__ keys) {
-    constexpr int NW = 2 * R + 2;
     const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
     if (q >= A.Nq) return;
     float cy, cx, cz;
     load_coords(A.coords, b, A.Nq, q, cy, cx, cz);
     WinAxes ax;
     bw_axes(A, l, cy, cx, cz, ax);
-    const int oy = (int)ax.kh - R + NW - 1, ox = (int)ax.ku - R + NW - 1, oz = (int)ax.kv - R + NW - 1;
-    const int CY = A.H[l] + NW - 1, CX = A.W[l] + NW - 1, CZ = A.D[l] + NW - 1;
+    int ih, iu, iv;
+    bw_origin(A, l, R, ax, ih, iu, iv);
+    const int oy = ih + A.nwh[l] - 1, ox = iu + A.nwu[l] - 1, oz = iv + A.nwv[l] - 1;
+    const int CY = A.H[l] + A.nwh[l] - 1, CX = A.W[l] + A.nwu[l] - 1, CZ = A.D[l] + A.nwv[l] - 1;
     const long long ncell = (long long)CY * CX * CZ;
     const bool in = !ax.dead && (unsigned)oy < (unsigned)CY && (unsigned)ox < (unsigned)CX && (unsigned)oz < (unsigned)CZ;
     const long long cell = in ? ((long long)oy * CX + ox) * CZ + oz : ncell;
@@ -321,7 +429,7 @@ __global__ __launch_bounds__(256) void k_cell_starts(const unsigned long long *_
 // ---------------------------------------------------------------------------------
 // 4. dT_l for one 4x4x4 brick of level-l targets of batch element b (owner lane i =
 // target i), streaming the queries whose window origin cell lies in
-// [brick, brick + NW - 1] (per axis, in o' coordinates).
+// [brick, brick + nw - 1] (per axis, in o' coordinates).
 // ---------------------------------------------------------------------------------
 // nsplit > 1 (coarse levels: a handful of bricks, each reached by most queries): workgroup
 // (brick, split) takes the origin rows row = 4 split + wave (mod 4 nsplit) and writes its partial
@@ -330,13 +438,14 @@ template <typename TT, int R>
 __global__ __launch_bounds__(256) void k_grad_t(const TT *__restrict__ Qp, const unsigned long long *__restrict__ keys,
                                                 const int *__restrict__ starts, float *__restrict__ dT,
                                                 float *__restrict__ dTp, int nsplit, BwdArgs A, int b, int l) {
-    constexpr int NW = 2 * R + 2, NW3 = NW * NW * NW;
     __shared__ __attribute__((aligned(16))) float gs_all[4][kTBatch][64];
     __shared__ __attribute__((aligned(16))) f32x2 red[2][64][64];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float (*gs)[64] = gs_all[w];
     const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
+    const int nh = A.nwh[l], nu = A.nwu[l], nv = A.nwv[l];
+    const long long nw3 = bw_nw3(A, l);
     const int nbz = (Dl + 3) >> 2, nbx = (Wl + 3) >> 2;
     const int split = (int)(blockIdx.x % nsplit);
     const int brick = (int)(blockIdx.x / nsplit);
@@ -346,14 +455,14 @@ __global__ __launch_bounds__(256) void k_grad_t(const TT *__restrict__ Qp, const
     const int by = t / nbx;
     const int ty = by * 4 + (lane >> 4), tx = bx * 4 + ((lane >> 2) & 3), tz = bz * 4 + (lane & 3);
     const bool tval = ty < Hl && tx < Wl && tz < Dl;
-    const int CX = Wl + NW - 1, CZ = Dl + NW - 1;
-    const int oy0 = by * 4, oy1 = min(by * 4 + 3, Hl - 1) + NW - 1;
-    const int ox0 = bx * 4, ox1 = min(bx * 4 + 3, Wl - 1) + NW - 1;
-    const int oz0 = bz * 4, oz1 = min(bz * 4 + 3, Dl - 1) + NW - 1;
+    const int CX = Wl + nu - 1, CZ = Dl + nv - 1;
+    const int oy0 = by * 4, oy1 = min(by * 4 + 3, Hl - 1) + nh - 1;
+    const int ox0 = bx * 4, ox1 = min(bx * 4 + 3, Wl - 1) + nu - 1;
+    const int oz0 = bz * 4, oz1 = min(bz * 4 + 3, Dl - 1) + nv - 1;
     const int nox = ox1 - ox0 + 1, nrows = (oy1 - oy0 + 1) * nox;
     const int c0 = 2 * lane;
     const bool cok = c0 < A.Cp;
-    const float *gl = A.gwin + ((long long)b * A.L + l) * A.Nq * NW3;
+    const float *gl = A.gwin + A.goff[l] + (long long)b * A.Nq * nw3;
     const TT *qb = Qp + (long long)b * A.Nq * A.Cp + c0;
     f32x2 acc[64];
 #pragma unroll
@@ -366,9 +475,9 @@ __global__ __launch_bounds__(256) void k_grad_t(const TT *__restrict__ Qp, const
         const long long cbase = ((long long)oy * CX + ox) * CZ;
         const int s = starts[cbase + oz0], e = starts[cbase + oz1 + 1];
         // window position of this lane's target for a query of origin o' = (oy, ox, ozq)
-        const int py = ty - oy + NW - 1, px = tx - ox + NW - 1;
-        const bool yxok = tval && (unsigned)py < (unsigned)NW && (unsigned)px < (unsigned)NW;
-        const int pyx = (py * NW + px) * NW;
+        const int py = ty - oy + nh - 1, px = tx - ox + nu - 1;
+        const bool yxok = tval && (unsigned)py < (unsigned)nh && (unsigned)px < (unsigned)nu;
+        const int pyx = (py * nu + px) * nv;
         for (int base = s; base < e; base += 64) {
             const int nk = min(64, e - base);
             const unsigned long long key = lane < nk ? keys[base + lane] : 0ull;
@@ -380,9 +489,9 @@ __global__ __launch_bounds__(256) void k_grad_t(const TT *__restrict__ Qp, const
                     const int idx = k0 + k;
                     const bool in = idx < nk;
                     const int qq = __shfl(qq_l, in ? idx : 0);
-                    const int pz = tz - __shfl(oz_l, in ? idx : 0) + NW - 1;
-                    const bool ok = in && yxok && (unsigned)pz < (unsigned)NW;
-                    g[k] = ok ? gl[(long long)qq * NW3 + pyx + pz] : 0.0f;
+                    const int pz = tz - __shfl(oz_l, in ? idx : 0) + nv - 1;
+                    const bool ok = in && yxok && (unsigned)pz < (unsigned)nv;
+                    g[k] = ok ? gl[(long long)qq * nw3 + pyx + pz] : 0.0f;
                     qv[k] = (in && cok) ? load2<TT>(qb + (long long)qq * A.Cp) : f32x2{0.0f, 0.0f};
                 }
             };
@@ -502,57 +611,78 @@ static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct BwdPlan {
     size_t gwin, dq, dt, keys, starts, temp, part, total;
+    int nw[DVC_MAX_LEVELS][3];   // window box (h, u, v) per level
+    long long goff[DVC_MAX_LEVELS];
 };
+
+// Window box of level l: 2r+2 per axis, or for a legacy level with W != D the span of 2r+1 samples
+// spaced (S_u - 1) / (S_n - 1) apart (ceil(2r * ratio) + 1 cells, + 1 for the upper corner, + 1 for
+// float rounding of the first and last sample)
+static void win_dims(const dvc_layout &lay, int l, int radius, bool legacy, int nw[3]) {
+    const int NW = 2 * radius + 2;
+    nw[0] = nw[1] = nw[2] = NW;
+    if (!(legacy && !lay.zero_level[l] && lay.W[l] != lay.D[l])) return;
+    auto span = [&](int su, int sn) {
+        const double ratio = (double)(su - 1) / (double)(sn - 1);
+        return (int)std::ceil(2.0 * radius * ratio - 1e-9) + 3;
+    };
+    nw[0] = 2 * radius + 3;
+    nw[1] = span(lay.W[l], lay.D[l]);   // U: memory W axis, normalised by D (legacy)
+    nw[2] = span(lay.D[l], lay.W[l]);   // V: memory D axis, normalised by W
+}
 
 // k_grad_t split factor of level l: enough (brick, split) workgroups for ~2 per CU, at most one origin
 // row per wave and split
-static int grad_t_splits(const dvc_layout &lay, int l, int NW) {
+static int grad_t_splits(const dvc_layout &lay, int l, const int nw[3]) {
     const long long bricks = (long long)((lay.H[l] + 3) / 4) * ((lay.W[l] + 3) / 4) * ((lay.D[l] + 3) / 4);
-    const long long rows = (long long)(std::min(lay.H[l], 4) + NW - 1) * (std::min(lay.W[l], 4) + NW - 1);
+    const long long rows = (long long)(std::min(lay.H[l], 4) + nw[0] - 1) * (std::min(lay.W[l], 4) + nw[1] - 1);
     long long sp = (512 + bricks - 1) / bricks;
     sp = std::min(sp, std::max(1LL, rows / 4));
     return (int)std::max(1LL, std::min(sp, 256LL));
 }
 
-static long long max_cells(const dvc_layout &lay, int NW) {
-    long long m = 0;
-    for (int l = 0; l < lay.num_levels; ++l)
-        m = std::max(m, (long long)(lay.H[l] + NW - 1) * (lay.W[l] + NW - 1) * (lay.D[l] + NW - 1));
-    return m;
+static long long level_cells(const dvc_layout &lay, int l, const int nw[3]) {
+    return (long long)(lay.H[l] + nw[0] - 1) * (lay.W[l] + nw[1] - 1) * (lay.D[l] + nw[2] - 1);
 }
 
-static void bwd_plan(int B, long long Nq, const dvc_layout &lay, int radius, BwdPlan &P) {
-    const int NW = 2 * radius + 2;
-    const long long NW3 = (long long)NW * NW * NW;
-    P.gwin = al256((size_t)B * lay.num_levels * Nq * NW3 * sizeof(float));
+static void bwd_plan(int B, long long Nq, const dvc_layout &lay, int radius, bool legacy, BwdPlan &P) {
+    size_t gw = 0;
+    long long cells = 0;
+    size_t part = 0;
+    for (int l = 0; l < lay.num_levels; ++l) {
+        win_dims(lay, l, radius, legacy, P.nw[l]);
+        gw = al256(gw);   // k_win_grad stores 8-byte pairs
+        P.goff[l] = (long long)(gw / sizeof(float));
+        gw += (size_t)B * Nq * P.nw[l][0] * P.nw[l][1] * P.nw[l][2] * sizeof(float);
+        cells = std::max(cells, level_cells(lay, l, P.nw[l]));
+        const int sp = grad_t_splits(lay, l, P.nw[l]);
+        const long long bricks = (long long)((lay.H[l] + 3) / 4) * ((lay.W[l] + 3) / 4) * ((lay.D[l] + 3) / 4);
+        if (sp > 1) part = std::max<size_t>(part, (size_t)sp * (size_t)bricks * 64 * (size_t)lay.c_pad * sizeof(float));
+    }
+    P.gwin = al256(gw);
     P.dq = al256((size_t)B * Nq * lay.c_pad * sizeof(float));
     P.dt = al256((size_t)B * lay.row_stride * lay.c_pad * sizeof(float));
     P.keys = al256((size_t)Nq * sizeof(unsigned long long));
-    P.starts = al256((size_t)(max_cells(lay, NW) + 1) * sizeof(int));
+    P.starts = al256((size_t)(cells + 1) * sizeof(int));
     size_t tb = 0;
     (void)rocprim::radix_sort_keys(nullptr, tb, (unsigned long long *)nullptr, (unsigned long long *)nullptr,
                                    (size_t)Nq, 0u, 64u, (hipStream_t)0);
     P.temp = al256(tb);
-    size_t part = 0;
-    for (int l = 0; l < lay.num_levels; ++l) {
-        const int sp = grad_t_splits(lay, l, NW);
-        const long long bricks = (long long)((lay.H[l] + 3) / 4) * ((lay.W[l] + 3) / 4) * ((lay.D[l] + 3) / 4);
-        if (sp > 1) part = std::max<size_t>(part, (size_t)sp * (size_t)bricks * 64 * (size_t)lay.c_pad * sizeof(float));
-    }
     P.part = al256(std::max<size_t>(part, 256));
     P.total = P.gwin + P.dq + P.dt + 2 * P.keys + P.starts + P.temp + P.part;
 }
 
+// workspace for either convention (the legacy plan is larger only when a level has W != D)
 size_t backward_workspace_bytes(int B, long long Nq, const dvc_layout &lay, int radius) {
-    BwdPlan P;
-    bwd_plan(B, Nq, lay, radius, P);
-    return P.total;
+    BwdPlan P, Q;
+    bwd_plan(B, Nq, lay, radius, false, P);
+    bwd_plan(B, Nq, lay, radius, true, Q);
+    return std::max(P.total, Q.total);
 }
 
 template <typename TT, int R>
 static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &lay, const BwdPlan &P,
                       unsigned char *ws, float *g1, float *g2, int C, hipStream_t s, char *err, size_t errlen) {
-    constexpr int NW = 2 * R + 2;
     float *dq = (float *)(ws + P.gwin);
     float *dt = (float *)(ws + P.gwin + P.dq);
     unsigned long long *kin = (unsigned long long *)(ws + P.gwin + P.dq + P.dt);
@@ -572,13 +702,19 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     const long long nqb = (A.Nq + 63) / 64;
     k_win_grad<R><<<(unsigned)((A.B * A.L * nqb + 3) / 4), 256, 0, s>>>(A);
     if (!launched("win_grad")) return DVC_ERR_LAUNCH;
+    bool any_generic = false;
+    for (int l = 0; l < A.L; ++l) any_generic |= A.generic[l] != 0;
+    if (any_generic) {
+        k_win_grad_generic<R><<<(unsigned)((A.B * A.L * nqb + 3) / 4), 256, 0, s>>>(A);
+        if (!launched("win_grad_generic")) return DVC_ERR_LAUNCH;
+    }
     const long long boxes = (long long)A.B * ((A.Hq + 3) / 4) * ((A.Wq + 3) / 4) * ((A.Dq + 3) / 4);
     k_grad_q<TT, R><<<(unsigned)boxes, 256, 0, s>>>(Tt, dq, A);
     if (!launched("grad_q")) return DVC_ERR_LAUNCH;
     for (int b = 0; b < A.B; ++b)
         for (int l = 0; l < A.L; ++l) {
             if (A.zero[l]) continue;
-            const long long ncell = (long long)(A.H[l] + NW - 1) * (A.W[l] + NW - 1) * (A.D[l] + NW - 1);
+            const long long ncell = level_cells(lay, l, P.nw[l]);
             unsigned bits = 1;
             while ((1LL << bits) <= ncell) ++bits;
             k_bw_keys<R><<<(unsigned)((A.Nq + 255) / 256), 256, 0, s>>>(A, b, l, kin);
@@ -591,7 +727,7 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
             k_cell_starts<<<(unsigned)((A.Nq + 1 + 255) / 256), 256, 0, s>>>(kout, A.Nq, ncell, starts);
             if (!launched("cell_starts")) return DVC_ERR_LAUNCH;
             const long long bricks = (long long)((A.H[l] + 3) / 4) * ((A.W[l] + 3) / 4) * ((A.D[l] + 3) / 4);
-            const int sp = grad_t_splits(lay, l, NW);
+            const int sp = grad_t_splits(lay, l, P.nw[l]);
             k_grad_t<TT, R><<<(unsigned)(bricks * sp), 256, 0, s>>>(Q, kout, starts, dt, dtp, sp, A, b, l);
             if (!launched("grad_t")) return DVC_ERR_LAUNCH;
             if (sp > 1) {
@@ -644,16 +780,13 @@ int corr_backward(const void *packed_q, const void *packed_t, const float *coord
         return DVC_ERR_UNSUPPORTED;
     }
     const bool legacy = convention == DVC_LEGACY;
+    BwdPlan P;
+    bwd_plan(B, Nq, lay, radius, legacy, P);
     for (int l = 0; l < lay.num_levels; ++l)
-        if (legacy && !lay.zero_level[l] && lay.W[l] != lay.D[l]) {
-            snprintf(err, errlen, "corr_backward: legacy convention with W != D at level %d is not supported", l);
+        if (level_cells(lay, l, P.nw[l]) >= (1LL << 31) - 1 || Nq >= (1LL << 31) - 1) {
+            snprintf(err, errlen, "corr_backward: volume too large for 32-bit keys");
             return DVC_ERR_UNSUPPORTED;
         }
-    const int NW = 2 * radius + 2;
-    if (max_cells(lay, NW) >= (1LL << 31) - 1 || Nq >= (1LL << 31) - 1) {
-        snprintf(err, errlen, "corr_backward: volume too large for 32-bit keys");
-        return DVC_ERR_UNSUPPORTED;
-    }
     BwdArgs A{};
     A.coords = coords; A.gout = grad_out; A.Nq = Nq; A.row_stride = lay.row_stride;
     A.B = B; A.L = lay.num_levels; A.legacy = legacy; A.Wq = lay.W[0]; A.Dq = lay.D[0];
@@ -661,9 +794,11 @@ int corr_backward(const void *packed_q, const void *packed_t, const float *coord
     for (int l = 0; l < DVC_MAX_LEVELS; ++l) {
         A.H[l] = lay.H[l]; A.W[l] = lay.W[l]; A.D[l] = lay.D[l]; A.Dp[l] = lay.Dp[l];
         A.zero[l] = lay.zero_level[l]; A.off[l] = lay.offset[l];
+        if (l < lay.num_levels) {
+            A.generic[l] = legacy && !lay.zero_level[l] && lay.W[l] != lay.D[l];
+            A.nwh[l] = P.nw[l][0]; A.nwu[l] = P.nw[l][1]; A.nwv[l] = P.nw[l][2]; A.goff[l] = P.goff[l];
+        }
     }
-    BwdPlan P;
-    bwd_plan(B, Nq, lay, radius, P);
     unsigned char *ws = (unsigned char *)workspace;
 #define DVC_BWD_CASE(RR)                                                                                           \
     case RR:                                                                                                       \

@@ -128,8 +128,10 @@ def test_backward_validation_without_gpu():
     assert rc == _lib.DVC_ERR_UNSUPPORTED
     with pytest.raises(NotImplementedError, match="radius"):
         _lib.check(rc)
-    rc = L.dvc_corr_backward(p, p, p, p, p, p, p, 1, 512, 16, 8, 8, 4, 2, 4, 1, 0, None)
-    assert rc == _lib.DVC_ERR_UNSUPPORTED     # legacy convention with W != D
+    # legacy convention with W != D is supported: level 0 of (8, 8, 4) at r = 4 has an 11 x 22 x 7 window box
+    # (2r+3, ceil(8 * 7/3) + 3, ceil(8 * 3/7) + 3), and the workspace covers either convention
+    nws_wd = L.dvc_corr_backward_workspace_bytes(1, 256, 16, 8, 8, 4, 2, 4)
+    assert nws_wd >= 256 * (11 * 22 * 7) * 4
     # workspace: window gradients (B*L*Nq*(2r+2)^3 f32) + dQ + dT + keys + cell starts + sort scratch
     nws = L.dvc_corr_backward_workspace_bytes(1, 32768, 128, 32, 32, 32, 4, 4)
     assert nws >= 4 * 32768 * 1000 * 4 and nws < 4 * 32768 * 1000 * 4 + 64 * 2 ** 20

@@ -145,11 +145,23 @@ def test_grad_reproducible_and_accumulates():
     assert orc.rel_err((p2 + q2).cpu().numpy(), a2.cpu().numpy()) < 1e-6
 
 
-def test_grad_unsupported_raises():
-    """Legacy convention with W != D (non-unit sample spacing): forward works, backward says so."""
-    import dvccorr
-    t1 = torch.randn(1, 16, 8, 8, 4, device=DEV, requires_grad=True)
-    t2 = torch.randn(1, 16, 8, 8, 4, device=DEV, requires_grad=True)
-    out = dvccorr.CorrBlock(t1, t2, 2, 2, legacy_wd_swap=True)(dvccorr.coords_grid_3d(1, 8, 8, 4, DEV))
-    with pytest.raises(NotImplementedError, match="legacy"):
-        out.sum().backward()
+@pytest.mark.parametrize("shape,C,L,r", [((8, 8, 4), 16, 2, 2), ((6, 16, 4), 8, 2, 4), ((7, 5, 17), 16, 3, 1),
+                                         ((12, 9, 11), 32, 2, 6)])
+def test_grad_legacy_w_ne_d(shape, C, L, r):
+    """Legacy convention on levels with W != D (grid x/z normalised by one axis' size and unnormalised by the
+    other's, corr.py:49-50): per-level window boxes of the stretched sample footprint (k_win_grad_generic),
+    against autograd through the CPU restatement; ratios above and below 1, flows leaving the volume."""
+    H, W, D = shape
+    seed = 5000 + H * 100 + W * 10 + D + r
+    f1 = prng.normal(seed, (1, C, H, W, D))
+    f2 = prng.normal(seed + 1, (1, C, H, W, D))
+    coords = prng.flow_coords(seed + 2, 1, H, W, D, r + 2.0)
+    G = prng.normal(seed + 3, (1, L * (2 * r + 1) ** 3, H, W, D))
+    ref1, ref2 = oracle_grads(f1, f2, coords, G, L, r, True)
+    for kind in ("gemm", "fused"):
+        d1, d2 = _gpu_grads(kind, f1, f2, coords, G, L, r, True)
+        e1, e2 = orc.rel_err(d1, ref1), orc.rel_err(d2, ref2)
+        assert e1 <= GRAD_TOL and e2 <= GRAD_TOL, (shape, r, kind, e1, e2)
+    a1, a2 = _gpu_grads("gemm", f1, f2, coords, G, L, r, True)
+    b1, b2 = _gpu_grads("gemm", f1, f2, coords, G, L, r, True)
+    assert np.array_equal(a1, b1) and np.array_equal(a2, b2)
