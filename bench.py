@@ -446,6 +446,9 @@ def main():
             kname = {"fused": "k_lookup_tile<PROJ> (dvc_corr_lookup_proj, convc1 fused)",
                      "unfused": "k_lookup_tile (dvc_corr_lookup) + torch conv/relu (timed together)"}.get(
                          args.convc1, "k_lookup_tile (dvc_corr_lookup)")
+        elif args.convc1 == "fused" and args.precision == "bf16" and 1 <= R <= 4:
+            kname = ("k_otf_keys + radix sort + k_fused_proj + k_rows_to_channels "
+                     "(dvc_corr_lookup_fused_proj, convc1 fused, timed together)")
         elif args.precision == "bf16" and 1 <= R <= 4:
             kname = "k_fused_box (dvc_corr_lookup_fused)"
         else:
@@ -458,6 +461,8 @@ def main():
             # the reference OTF dot count 2 C (2r+1)^3 L per voxel-query, against the dtype's MFMA peak
             fl = 2.0 * C * (2 * R + 1) ** 3 * L * nq_local
             peak = BF16_PEAK_TFS if args.precision == "bf16" else F32_PEAK_TFS
+            if args.convc1 == "fused":   # + convc1: 2 x 96 x L (2r+1)^3 per voxel-query
+                fl += 2.0 * 96 * (2 * R + 1) ** 3 * L * nq_local
             roof["mfma"] = {"achieved": round(fl / (lk_avg * 1e-3) / 1e12, 1), "peak": peak, "unit": "TFLOP/s",
                             "frac": round(fl / (lk_avg * 1e-3) / 1e12 / peak, 4), "flops_per_launch": fl}
     else:

@@ -25,6 +25,8 @@
  *   dvc_sample3d           -- bilinear_sampler_3d                             src/core/corr.py:17-68
  *   dvc_proj_pack,         -- CorrBlock.__call__ followed by the motion       src/core/corr.py:169-208 +
  *   dvc_corr_lookup_proj      encoder's F.relu(self.convc1(corr))            src/core/update.py:219-222, 246
+ *   dvc_corr_lookup_fused_proj -- CorrBlockOnTheFly.__call__ + the same       src/core/corr_otf.py:96-237 +
+ *                             convc1                                         src/core/update.py:219-222, 246
  *   dvc_coords_grid        -- coords_grid_3d                                 src/core/corr.py:71-99
  *   dvc_upflow             -- upflow_3d(flow, target_shape)                  src/core/corr.py:211-253
  *   dvc_flow_step          -- coords1 + delta_flow; upflow_3d(coords1 - coords0)  src/core/raft_dvc.py:482-485
@@ -165,6 +167,20 @@ int dvc_proj_pack(const float *weight, void *packed, int cout, int num_levels, i
 int dvc_corr_lookup_proj(const void *corr, const float *coords, const void *packed_w, const float *bias, float *out,
                          int B, int64_t Nq, int H, int W, int D, int num_levels, int radius, int convention,
                          int store_dtype, void *stream);
+
+/* The same composition on the on-the-fly path (CorrBlockOnTheFly.__call__ followed by
+ * F.relu(self.convc1(corr)), src/core/corr_otf.py:96-237 + src/core/update.py:246):
+ * packed_q / packed_t as for dvc_corr_lookup_fused (bf16), packed_w from dvc_proj_pack,
+ * out (B, 96, Nq) float32.  Queries are processed in order of their level-0 window
+ * origin (a radix sort per call), so each workgroup's union of windows is small; the
+ * per-query 96-channel rows are transposed to (B, 96, Nq) at the end.  Workspace:
+ * dvc_lookup_fused_proj_workspace_bytes (sort keys + the [B][Nq][96] rows).
+ * Supported: bf16, radius 1..4, C_pad in {32, 64, 128}, and for the legacy convention
+ * W == D at every non-zero level (DVC_ERR_UNSUPPORTED otherwise). */
+size_t dvc_lookup_fused_proj_workspace_bytes(int B, int64_t Nq);
+int dvc_corr_lookup_fused_proj(const void *packed_q, const void *packed_t, const float *coords, const void *packed_w,
+                               const float *bias, float *out, void *workspace, int B, int64_t Nq, int C, int H, int W,
+                               int D, int num_levels, int radius, int convention, int dtype, void *stream);
 
 /* bilinear_sampler_3d: vol (B, C, Hv, Wv, Dv), pts (B, Nq, 3) in (h, w, d) -> out (B, C, Nq). */
 int dvc_sample3d(const float *vol, const float *pts, float *out, int B, int C, int Hv, int Wv, int Dv, int64_t Nq,

@@ -45,6 +45,11 @@ int fused_lookup(const void *packed_q, const void *packed_t, const float *coords
                  long long Nq, int C, const dvc_layout &lay, int radius, int convention, int dtype, int variant,
                  hipStream_t s, char *err, size_t errlen);
 size_t fused_workspace_bytes(int B, long long Nq, int L, int radius);
+int fused_lookup_proj(const void *packed_q, const void *packed_t, const float *coords, const void *packed_w,
+                      const float *bias, float *out, void *workspace, int B, long long Nq, int C,
+                      const dvc_layout &lay, int radius, int convention, int dtype, int ablate, hipStream_t s,
+                      char *err, size_t errlen);
+size_t fused_proj_workspace_bytes(int B, long long Nq);
 int corr_backward(const void *packed_q, const void *packed_t, const float *coords, const float *grad_out,
                   float *grad_fmap1, float *grad_fmap2, void *workspace, int B, long long Nq, int C,
                   const dvc_layout &lay, int radius, int convention, int dtype, hipStream_t s, char *err,
@@ -719,3 +724,24 @@ int dvc_flow_step(const float *coords1, const float *delta_flow, float *coords1_
 }
 
 }  // extern "C"
+
+size_t dvc_lookup_fused_proj_workspace_bytes(int B, int64_t Nq) {
+    if (B < 1 || Nq < 1) return 0;
+    return fused_proj_workspace_bytes(B, Nq);
+}
+
+int dvc_corr_lookup_fused_proj(const void *packed_q, const void *packed_t, const float *coords, const void *packed_w,
+                               const float *bias, float *out, void *workspace, int B, int64_t Nq, int C, int H, int W,
+                               int D, int num_levels, int radius, int convention, int dtype, void *stream) {
+    dvc_layout lay;
+    int rc = dvc_layout_init(H, W, D, num_levels, C, &lay);
+    if (rc) return rc;
+    if (!packed_q || !packed_t || !coords || !packed_w || !bias || !out)
+        return fail(DVC_ERR_INVALID, "lookup_fused_proj: null pointer");
+    if (B < 1 || Nq < 1) return fail(DVC_ERR_INVALID, "lookup_fused_proj: B=%d Nq=%lld", B, (long long)Nq);
+    if (convention != DVC_FIXED && convention != DVC_LEGACY)
+        return fail(DVC_ERR_INVALID, "lookup_fused_proj: bad convention %d", convention);
+    if (dtype != DVC_BF16 && dtype != DVC_F32) return fail(DVC_ERR_INVALID, "lookup_fused_proj: bad dtype %d", dtype);
+    return fused_lookup_proj(packed_q, packed_t, coords, packed_w, bias, out, workspace, B, Nq, C, lay, radius,
+                             convention, dtype, g_fused_ablate, (hipStream_t)stream, g_err, sizeof(g_err));
+}

@@ -34,14 +34,11 @@
 // (tests/test_gpu_parity.py::test_fused_tile_matches_materialised).
 #include "common.h"
 #include "lookup_common.h"
+#include "fused_common.h"
 
 #include <type_traits>
 
 namespace dvc {
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 template <int R, int NWAVES> struct BoxCfg {
     static constexpr int n = 2 * R + 1;
@@ -52,29 +49,6 @@ template <int R, int NWAVES> struct BoxCfg {
     static constexpr int TRASH = GUARD + 64 * WQ;                 // per-lane scratch slots
     static constexpr int LDS = (TRASH + 64 * 4 + GUARD + 15) & ~15;
     static constexpr int COLS = NWAVES >= 8 ? 2 : 3;              // output columns per wave (phase 2)
-};
-
-__device__ __forceinline__ int buni(int v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ long long buni64(long long v) {
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
-    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((unsigned long long)v >> 32));
-    return (long long)(((unsigned long long)hi << 32) | lo);
-}
-template <typename T> __device__ __forceinline__ T *buniptr(T *p) { return (T *)buni64((long long)p); }
-__device__ __forceinline__ int bwave_min(int v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = min(v, __shfl_xor(v, o));
-    return buni(v);
-}
-__device__ __forceinline__ int bwave_max(int v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));
-    return buni(v);
-}
-
-template <int n> struct BRun {
-    f32x2 p[n / 2];
-    float t;
 };
 
 template <int R, int KS, int NWAVES, int TY, int TX, int TZ>

@@ -25,7 +25,8 @@ EXPORTED = (
     "dvc_corr_pool", "dvc_corr_lookup", "dvc_lookup_fused_workspace_bytes", "dvc_corr_lookup_fused",
     "dvc_sample3d", "dvc_set_tuning", "dvc_last_error", "dvc_version", "dvc_abi_version",
     "dvc_corr_backward_workspace_bytes", "dvc_corr_backward", "dvc_proj_packed_bytes", "dvc_proj_pack",
-    "dvc_corr_lookup_proj", "dvc_coords_grid", "dvc_upflow", "dvc_flow_step",
+    "dvc_corr_lookup_proj", "dvc_lookup_fused_proj_workspace_bytes", "dvc_corr_lookup_fused_proj",
+    "dvc_coords_grid", "dvc_upflow", "dvc_flow_step",
 )
 PROJ_COUT = 96          # DVC_PROJ_COUT (convc1 output channels, update.py:222)
 PROJ_MAX_RADIUS = 4     # DVC_PROJ_MAX_RADIUS
@@ -85,6 +86,9 @@ def lib() -> ctypes.CDLL:
         "dvc_proj_packed_bytes": (sz, [i32, i32]),
         "dvc_proj_pack": (i32, [vp, vp, i32, i32, i32, i32, vp]),
         "dvc_corr_lookup_proj": (i32, [vp, vp, vp, vp, vp, i32, i64, i32, i32, i32, i32, i32, i32, i32, vp]),
+        "dvc_lookup_fused_proj_workspace_bytes": (sz, [i32, i64]),
+        "dvc_corr_lookup_fused_proj": (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i64, i32, i32, i32, i32, i32, i32, i32,
+                                             i32, vp]),
         "dvc_coords_grid": (i32, [vp, i32, i32, i32, i32, vp]),
         "dvc_upflow": (i32, [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
         "dvc_flow_step": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp]),

@@ -110,6 +110,21 @@ class _Block:
         if coords.ndim != 5 or tuple(coords.shape) != (B, 3, H, W, D):
             raise ValueError(f"coords must be (B, 3, H, W, D) = {(B, 3, H, W, D)}; got {tuple(coords.shape)}")
 
+    def _convc1_fusable(self, weight: torch.Tensor, bias: torch.Tensor, w: torch.Tensor) -> bool:
+        """The fused convc1 kernels cover a bf16 block without gradients, radius 1..4, 96 output channels and
+        no legacy level with W != D; fp32 blocks keep the reference's fp32 convc1 (update.py:246), since the
+        kernels' fp16 MFMA operands would cost ~1e-3 relative error."""
+        return (self.precision == "bf16"
+                and not (torch.is_grad_enabled() and (weight.requires_grad or bias.requires_grad or
+                                                      self._grad_fmaps is not None))
+                and 1 <= self.radius <= ops._lib.PROJ_MAX_RADIUS and w.shape[0] == ops._lib.PROJ_COUT
+                and not (self.legacy_wd_swap and any(lw != ld and min(lh, lw, ld) > 1
+                                                     for lh, lw, ld in self._lay.levels())))
+
+    def _convc1_composition(self, coords: torch.Tensor, w: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+        out = self(coords)
+        return torch.relu(torch.nn.functional.conv3d(out, w.reshape(w.shape[0], -1, 1, 1, 1), bias))
+
     def __call__(self, coords: torch.Tensor) -> torch.Tensor:
         self._check_coords(coords)
         B, C, H, W, D = self.shape
@@ -200,17 +215,8 @@ class CorrBlock(_Block):
         self._check_coords(coords)
         B, _, H, W, D = self.shape
         w = weight.reshape(weight.shape[0], -1)
-        # fp32 blocks keep the reference's fp32 convc1 (update.py:246): the fused kernel's fp16 MFMA
-        # operands would cost ~1e-3 relative error, so they take the exact composition below
-        fused_ok = (self.precision == "bf16"
-                    and not (torch.is_grad_enabled() and (weight.requires_grad or bias.requires_grad or
-                                                          self._grad_fmaps is not None))
-                    and 1 <= self.radius <= ops._lib.PROJ_MAX_RADIUS and w.shape[0] == ops._lib.PROJ_COUT
-                    and not (self.legacy_wd_swap and any(lw != ld and min(lh, lw, ld) > 1
-                                                         for lh, lw, ld in self._lay.levels())))
-        if not fused_ok:
-            out = self(coords)
-            return torch.relu(torch.nn.functional.conv3d(out, w.reshape(w.shape[0], -1, 1, 1, 1), bias))
+        if not self._convc1_fusable(weight, bias, w):
+            return self._convc1_composition(coords, w, bias)
         packed = ops.proj_pack_cached(weight, self.num_levels, self.radius, self.legacy_wd_swap)
         out = ops.lookup_proj(self._corr, coords.reshape(B, 3, H * W * D), packed, bias, H, W, D,
                               self.num_levels, self.radius, self.legacy_wd_swap, self._dt)
@@ -245,6 +251,22 @@ class CorrBlockFused(_Block):
         _, C, H, W, D = self.shape
         return library.lookup_fused(self._q, self._t, coords_flat, C, H, W, D, self.num_levels, self.radius,
                                     self.legacy_wd_swap, self._dt)
+
+    def lookup_convc1(self, coords: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+        """F.relu(convc1(self(coords))) -> (B, 96, H, W, D) fp32 with convc1 fused into the on-the-fly lookup
+        (dvc_corr_lookup_fused_proj): the L*(2r+1)^3 channels never reach HBM, and the queries are grouped by
+        window position so each workgroup's window union is small.  Same numerics and fallbacks as
+        CorrBlock.lookup_convc1 (fp16 convc1 operands, tolerance 1e-2; fp32 blocks, gradients, radii > 4,
+        legacy W != D levels and C_pad outside {32, 64, 128} take relu(conv3d(self(coords))))."""
+        self._check_coords(coords)
+        B, C, H, W, D = self.shape
+        w = weight.reshape(weight.shape[0], -1)
+        if not (self._convc1_fusable(weight, bias, w) and self._lay.c_pad in (32, 64, 128)):
+            return self._convc1_composition(coords, w, bias)
+        packed = ops.proj_pack_cached(weight, self.num_levels, self.radius, self.legacy_wd_swap)
+        out = library.lookup_fused_proj(self._q, self._t, coords.reshape(B, 3, H * W * D), packed, bias, C, H, W,
+                                        D, self.num_levels, self.radius, self.legacy_wd_swap, self._dt)
+        return out.view(B, -1, H, W, D)
 
 
 class CorrBlockOnTheFly(CorrBlockFused):

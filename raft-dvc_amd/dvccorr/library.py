@@ -6,6 +6,8 @@ the PyTorch dispatcher as named operators with shape functions:
     dvccorr::build(q, t, ...)                    -> corr pyramid (B, Nq, row_stride)   corr.py:141-167
     dvccorr::lookup(corr, coords, ...)           -> (B, L*(2r+1)^3, Nq) f32            corr.py:169-208
     dvccorr::lookup_fused(q, t, coords, ...)     -> (B, L*(2r+1)^3, Nq) f32            corr_otf.py:96-237
+    dvccorr::lookup_fused_proj(q, t, coords, w, b, ...) -> (B, 96, Nq) f32 = relu(convc1(lookup_fused))
+                                                                                       + update.py:246
     dvccorr::corr_backward(q, t, coords, g, ...) -> (d fmap1 (B, C, Nq), d fmap2)      autograd of corr.py:141-208
     dvccorr::lookup_ad(fmap1, fmap2, corr?, q, t, coords, ...)
         the lookup as a differentiable op: fmap1 / fmap2 are its gradient carriers
@@ -78,6 +80,19 @@ def _(packed_q, packed_t, coords, C, H, W, D, num_levels, radius, legacy, dtype)
     return packed_q.new_empty((B, num_levels * _n3(radius), Nq), dtype=_F32)
 
 
+@torch.library.custom_op("dvccorr::lookup_fused_proj", mutates_args=())
+def lookup_fused_proj(packed_q: Tensor, packed_t: Tensor, coords: Tensor, packed_w: Tensor, bias: Tensor, C: int,
+                      H: int, W: int, D: int, num_levels: int, radius: int, legacy: bool, dtype: int) -> Tensor:
+    return ops.lookup_fused_proj(packed_q, packed_t, coords, packed_w, bias, C, H, W, D, num_levels, radius, legacy,
+                                 dtype)
+
+
+@lookup_fused_proj.register_fake
+def _(packed_q, packed_t, coords, packed_w, bias, C, H, W, D, num_levels, radius, legacy, dtype):
+    B, Nq, _ = packed_q.shape
+    return packed_q.new_empty((B, 96, Nq), dtype=_F32)
+
+
 @torch.library.custom_op("dvccorr::corr_backward", mutates_args=())
 def corr_backward(packed_q: Tensor, packed_t: Tensor, coords: Tensor, grad_out: Tensor, C: int, H: int, W: int,
                   D: int, num_levels: int, radius: int, legacy: bool, dtype: int) -> tuple[Tensor, Tensor]:
@@ -122,4 +137,4 @@ def _lookup_ad_backward(ctx, grad_out):
 
 torch.library.register_autograd("dvccorr::lookup_ad", _lookup_ad_backward, setup_context=_lookup_ad_setup)
 
-__all__ = ["build", "lookup", "lookup_fused", "corr_backward", "lookup_ad"]
+__all__ = ["build", "lookup", "lookup_fused", "lookup_fused_proj", "corr_backward", "lookup_ad"]

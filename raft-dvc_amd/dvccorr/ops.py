@@ -180,6 +180,29 @@ def lookup_proj(corr: torch.Tensor, coords: torch.Tensor, packed_w: torch.Tensor
     return out
 
 
+def lookup_fused_proj(packed_q: torch.Tensor, packed_t: torch.Tensor, coords: torch.Tensor, packed_w: torch.Tensor,
+                      bias: torch.Tensor, C: int, H: int, W: int, D: int, num_levels: int, radius: int, legacy: bool,
+                      dtype: int, out: torch.Tensor = None, workspace: torch.Tensor = None) -> torch.Tensor:
+    """relu(convc1(lookup_fused(coords))) -> (B, 96, Nq) f32 on the on-the-fly path, the lookup never written
+    (dvc_corr_lookup_fused_proj: queries grouped by window origin, convc1 on MFMA)."""
+    _need_cuda(packed_q, packed_t, coords, packed_w, bias)
+    B, Nq, _ = packed_q.shape
+    c = _f32c(coords)
+    b = _f32c(bias)
+    if b.numel() != _lib.PROJ_COUT:
+        raise ValueError(f"convc1 bias must have {_lib.PROJ_COUT} entries; got {b.numel()}")
+    if out is None:
+        out = torch.empty((B, _lib.PROJ_COUT, Nq), dtype=torch.float32, device=packed_q.device)
+    nws = lib().dvc_lookup_fused_proj_workspace_bytes(B, Nq)
+    if workspace is None or workspace.numel() * workspace.element_size() < nws:
+        workspace = torch.empty((max(nws, 256),), dtype=torch.uint8, device=packed_q.device)
+    check(lib().dvc_corr_lookup_fused_proj(_ptr(packed_q), _ptr(packed_t), _ptr(c), _ptr(packed_w), _ptr(b), _ptr(out),
+                                           _ptr(workspace), B, Nq, C, H, W, D, num_levels, radius,
+                                           DVC_LEGACY if legacy else DVC_FIXED, dtype, _stream(packed_q)),
+          "corr_lookup_fused_proj")
+    return out
+
+
 def lookup_fused(packed_q: torch.Tensor, packed_t: torch.Tensor, coords: torch.Tensor, C: int, H: int, W: int,
                  D: int, num_levels: int, radius: int, legacy: bool, dtype: int, out: torch.Tensor = None,
                  workspace: torch.Tensor = None) -> torch.Tensor:
@@ -274,7 +297,7 @@ def flow_step(coords1: torch.Tensor, delta_flow, target_shape):
     return new, up
 
 
-__all__ = ["pack_queries", "pack_targets", "build", "pool", "lookup", "lookup_fused", "corr_backward", "sample3d",
+__all__ = ["pack_queries", "pack_targets", "build", "pool", "lookup", "lookup_fused", "lookup_fused_proj", "corr_backward", "sample3d",
            "proj_pack", "proj_pack_cached", "lookup_proj",
            "coords_grid", "upflow", "flow_step",
            "fused_workspace", "dtype_code", "layout", "_lib"]

@@ -26,6 +26,7 @@ import torch
 import torch.distributed as dist
 
 from . import ops
+from ._lib import layout
 from .corr_block import resolve_precision
 
 
@@ -130,12 +131,29 @@ class HipRows:
                                 workspace=self.ws)
 
     def lookup_convc1(self, coords_flat: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
-        """relu(convc1(lookup)) of this rank's rows, convc1 fused into the lookup (materialised only)."""
+        """relu(convc1(lookup)) of this rank's rows, convc1 fused into the lookup kernel (materialised:
+        dvc_corr_lookup_proj, fused: dvc_corr_lookup_fused_proj) for a bf16 block; an fp32 block, or shapes
+        the fused kernels do not cover, take relu(W . lookup + b) in fp32."""
         C, H, W, D = self.dims
-        if self.impl != "materialised":
-            raise NotImplementedError("convc1 fusion is implemented for the materialised pyramid")
+        w = weight.reshape(weight.shape[0], -1)
+        generic = self.legacy and any(lw != ld and min(lh, lw, ld) > 1
+                                      for lh, lw, ld in layout(H, W, D, self.L, C).levels())
+        fusable = (self.dt == ops.dtype_code("bf16") and 1 <= self.R <= ops._lib.PROJ_MAX_RADIUS
+                   and w.shape[0] == ops._lib.PROJ_COUT and not generic
+                   and (self.impl == "materialised" or layout(H, W, D, self.L, C).c_pad in (32, 64, 128)))
+        if not fusable:
+            out = self.lookup(coords_flat)
+            return torch.relu(torch.matmul(w.float(), out) + bias.float().view(1, -1, 1))
         packed = ops.proj_pack_cached(weight, self.L, self.R, self.legacy)
-        return ops.lookup_proj(self.corr, coords_flat, packed, bias, H, W, D, self.L, self.R, self.legacy, self.dt)
+        if self.impl == "materialised":
+            return ops.lookup_proj(self.corr, coords_flat, packed, bias, H, W, D, self.L, self.R, self.legacy,
+                                   self.dt)
+        if getattr(self, "pws", None) is None:   # sort keys + [B][N][96] rows, reused across lookups
+            B, _, N = coords_flat.shape
+            self.pws = torch.empty((max(ops.lib().dvc_lookup_fused_proj_workspace_bytes(B, N), 256),),
+                                   dtype=torch.uint8, device=coords_flat.device)
+        return ops.lookup_fused_proj(self.q, self.t, coords_flat, packed, bias, C, H, W, D, self.L, self.R,
+                                     self.legacy, self.dt, workspace=self.pws)
 
 
 class ShardedCorrBlock:

@@ -1,0 +1,173 @@
+"""GPU parity of convc1 fused into the ON-THE-FLY lookup (dvc_corr_lookup_fused_proj,
+CorrBlockFused.lookup_convc1, ShardedCorrBlock(impl="fused").lookup_convc1).
+
+Reference: CorrBlockOnTheFly.__call__ (src/core/corr_otf.py:96-237; CorrBlock's values,
+src/core/corr.py:169-208) followed by MotionEncoder's F.relu(self.convc1(corr))
+(src/core/update.py:219-222, 246).  The kernel groups queries by window origin (a radix
+sort per call) and feeds the bf16-pyramid lookup values and the weights to fp16 MFMA with
+fp32 accumulation, like dvc_corr_lookup_proj.  Tolerances (written here):
+max|out - ref| / max|ref| <= 1e-2 against the reference and the f64 oracle; <= 2e-3 against
+the unfused GPU composition relu(conv3d(lookup)) of the same block (only the fp16 operand
+rounding differs); <= 1e-5 against the materialised block's fused convc1 (same dots, same fp16
+rows, accumulated in the same order).
+"""
+from __future__ import annotations
+
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import prng
+from conftest import GOLDEN, load_golden, proj_inputs
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+PROJ_TOL = 1e-2
+FP32_TOL = 1e-5
+FUSED_VS_UNFUSED_TOL = 2e-3
+SAME_DOTS_TOL = 1e-5
+DEV = torch.device("cuda:0")
+PROJ_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "proj_*.npz")))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _no_grad():
+    with torch.no_grad():
+        yield
+
+
+def _gpu(*arrs):
+    return [torch.from_numpy(np.ascontiguousarray(a)).to(DEV) for a in arrs]
+
+
+def _conv_inputs(seed, L, r):
+    K = L * (2 * r + 1) ** 3
+    bound = 1.0 / np.sqrt(K)
+    return prng.uniform(seed, (96, K), -bound, bound), prng.uniform(seed + 1, (96,), -bound, bound)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", PROJ_CASES)
+def test_golden_reference(case, precision):
+    import dvccorr
+    g = load_golden(case + ".npz")
+    f1, f2, coords, w, b, L, r, legacy = proj_inputs(g)
+    t1, t2, tc, tw, tb = _gpu(f1, f2, coords, w, b)
+    blk = dvccorr.CorrBlockFused(t1, t2, L, r, legacy_wd_swap=legacy, precision=precision)
+    out = blk.lookup_convc1(tc, tw, tb)
+    torch.cuda.synchronize()
+    assert out.shape == g["out"].shape and out.dtype == torch.float32
+    assert orc.rel_err(out.cpu().numpy(), g["out"]) < (PROJ_TOL if precision == "bf16" else FP32_TOL)
+
+
+@pytest.mark.parametrize("shape,C,L,r,legacy,B", [
+    ((9, 7, 5), 32, 2, 1, False, 1),      # 315 queries: a partial last chunk
+    ((12, 10, 16), 64, 3, 2, False, 2),   # two batch elements (one sort each)
+    ((16, 16, 16), 32, 4, 3, False, 1),
+    ((8, 8, 8), 16, 4, 4, True, 1),       # level 3 = 1^3: zero level
+    ((10, 12, 12), 32, 2, 4, True, 1),    # legacy with W == D
+    ((11, 9, 13), 128, 3, 4, False, 1),
+])
+def test_against_oracle(shape, C, L, r, legacy, B):
+    import dvccorr
+    H, W, D = shape
+    seed = 1900 + H + 3 * W + 7 * D + r
+    f1 = prng.normal(seed, (B, C, H, W, D))
+    f2 = prng.normal(seed + 1, (B, C, H, W, D))
+    coords = prng.flow_coords(seed + 2, B, H, W, D, 2.5)
+    w, b = _conv_inputs(seed + 3, L, r)
+    ref = orc.motion_convc1(orc.corr_lookup(f1, f2, coords, L, r, legacy), w, b)
+    t1, t2, tc, tw, tb = _gpu(f1, f2, coords, w, b)
+    out = dvccorr.CorrBlockFused(t1, t2, L, r, legacy_wd_swap=legacy, precision="bf16").lookup_convc1(tc, tw, tb)
+    assert orc.rel_err(out.cpu().numpy(), ref) < PROJ_TOL
+    # the materialised block's fused convc1 (k_lookup_tile<PROJ>) sees the same bf16 dots
+    mat = dvccorr.CorrBlock(t1, t2, L, r, legacy_wd_swap=legacy, precision="bf16").lookup_convc1(tc, tw, tb)
+    assert float((out - mat).abs().max() / mat.abs().max()) < SAME_DOTS_TOL
+
+
+def _bench_like(S, C, L, r, max_flow, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    f1 = torch.randn(1, C, S, S, S, generator=g).to(DEV)
+    f2 = torch.randn(1, C, S, S, S, generator=g).to(DEV)
+    base = torch.stack(torch.meshgrid(*[torch.arange(S, dtype=torch.float32)] * 3, indexing="ij"))[None]
+    coords = (base + (torch.rand(1, 3, S, S, S, generator=g) * 2 - 1) * max_flow).to(DEV)
+    return f1, f2, coords
+
+
+@pytest.mark.parametrize("S,L,max_flow", [(32, 4, 2.0), (40, 2, 6.0)])
+def test_against_unfused_and_deterministic(S, L, max_flow):
+    """Bench-like volumes (the #3 shape; a 40^3 L=2 one with +-6-voxel flows, whose windows spread wider
+    than one origin column): fused vs relu(conv3d(lookup_fused)) of the same block; bitwise repeatable."""
+    import dvccorr
+    C, r = 128, 4
+    f1, f2, coords = _bench_like(S, C, L, r, max_flow, 177 + S)
+    w, b = (torch.from_numpy(a).to(DEV) for a in _conv_inputs(178, L, r))
+    blk = dvccorr.CorrBlockFused(f1, f2, L, r, precision="bf16")
+    ref = torch.relu(torch.nn.functional.conv3d(blk(coords), w.view(96, -1, 1, 1, 1), b))
+    out = blk.lookup_convc1(coords, w, b)
+    out2 = blk.lookup_convc1(coords, w, b)
+    torch.cuda.synchronize()
+    err = float((out - ref).abs().max() / ref.abs().max())
+    assert err < FUSED_VS_UNFUSED_TOL, err
+    assert torch.equal(out, out2)
+
+
+def test_outliers_nonfinite_and_far_windows():
+    """NaN coordinates and windows entirely outside the volume sample zeros (relu(b)); a few queries with
+    +-20-voxel flows among +-1-voxel ones stay exact (they sort next to their window neighbours)."""
+    import dvccorr
+    H = W = D = 16
+    C, L, r = 32, 2, 4
+    f1 = prng.normal(61, (1, C, H, W, D))
+    f2 = prng.normal(62, (1, C, H, W, D))
+    coords = prng.flow_coords(63, 1, H, W, D, 1.0)
+    rng = np.random.default_rng(64)
+    idx = rng.integers(0, H, size=(40, 3))
+    for (y, x, z) in idx:
+        coords[0, :, y, x, z] += rng.uniform(-20, 20, size=3).astype(np.float32)
+    coords[0, :, 1, 2, 3] = np.nan
+    coords[0, 0, 4, 4, 4] = 1e30
+    coords[0, :, 5, 5, 5] = -200.0      # window misses every level
+    w, b = _conv_inputs(65, L, r)
+    far = coords.copy()                  # the oracle takes the zero-sampling cases as far windows
+    far[0, :, 1, 2, 3] = -200.0
+    far[0, 0, 4, 4, 4] = -200.0
+    ref = orc.motion_convc1(orc.corr_lookup(f1, f2, far, L, r, False), w, b)
+    t1, t2, tc, tw, tb = _gpu(f1, f2, coords, w, b)
+    out = dvccorr.CorrBlockFused(t1, t2, L, r, precision="bf16").lookup_convc1(tc, tw, tb).cpu().numpy()
+    assert np.isfinite(out).all()
+    relu_b = np.maximum(b, 0).astype(np.float32)
+    for (y, x, z) in ((1, 2, 3), (4, 4, 4), (5, 5, 5)):
+        np.testing.assert_allclose(out[0, :, y, x, z], relu_b, rtol=0, atol=1e-6)
+    assert orc.rel_err(out, ref) < PROJ_TOL
+
+
+def test_sharded_fused_convc1_matches_block():
+    """ShardedCorrBlock(impl="fused").lookup_convc1 on one rank equals CorrBlockFused.lookup_convc1."""
+    import dvccorr
+    from dvccorr.sharded import ShardedCorrBlock
+    S, C, L, r = 24, 64, 3, 4
+    f1, f2, coords = _bench_like(S, C, L, r, 2.0, 91)
+    w, b = (torch.from_numpy(a).to(DEV) for a in _conv_inputs(92, L, r))
+    ref = dvccorr.CorrBlockFused(f1, f2, L, r, precision="bf16").lookup_convc1(coords, w, b)
+    sh = ShardedCorrBlock(f1, f2, S, L, r, precision="bf16", impl="fused")
+    out = sh.lookup_convc1(coords, w, b)
+    assert torch.equal(out, ref)
+
+
+def test_fp32_block_takes_exact_composition():
+    import dvccorr
+    H, W, D = 10, 9, 8
+    C, L, r = 32, 2, 3
+    f1 = prng.normal(71, (1, C, H, W, D))
+    f2 = prng.normal(72, (1, C, H, W, D))
+    coords = prng.flow_coords(73, 1, H, W, D, 2.0)
+    w, b = _conv_inputs(74, L, r)
+    ref = orc.motion_convc1(orc.corr_lookup(f1, f2, coords, L, r, False), w, b)
+    t1, t2, tc, tw, tb = _gpu(f1, f2, coords, w, b)
+    out = dvccorr.CorrBlockFused(t1, t2, L, r, precision="fp32").lookup_convc1(tc, tw, tb)
+    assert orc.rel_err(out.cpu().numpy(), ref) < FP32_TOL

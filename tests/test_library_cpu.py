@@ -36,6 +36,10 @@ def test_ops_registered_with_fake_shapes():
         g = torch.empty(B, L * n3, H * W * D, device="cuda")
         d1, d2 = torch.ops.dvccorr.corr_backward(q, t, c, g, C, H, W, D, L, r, False, 1)
         assert d1.shape == (B, C, H * W * D) and d2.shape == (B, C, H, W, D)
+        wp = torch.empty(1024, dtype=torch.float16, device="cuda")
+        bias = torch.empty(96, device="cuda")
+        out = torch.ops.dvccorr.lookup_fused_proj(q, t, c, wp, bias, C, H, W, D, L, r, False, 1)
+        assert out.shape == (B, 96, H * W * D) and out.dtype == torch.float32
 
 
 def test_lookup_ad_autograd_shapes():

@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Ablation timings of the convc1-fused on-the-fly lookup (dvc_corr_lookup_fused_proj) at config #5
+(128^3 x 128 fmaps, L=2, r=4, coords = identity + U(-2, 2)).  Diagnostics only: the fused_ablate bits
+skip parts of k_fused_proj (1 phase 1, 2 producers, 4 convc1 MFMA, 8 window writes, 16 target loads)."""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "raft-dvc_amd"))
+import dvccorr  # noqa: E402
+from dvccorr import _lib  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--size", type=int, default=128)
+ap.add_argument("--levels", type=int, default=2)
+ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--ablate", default="0,1,2,4,8,16,6,7")
+a = ap.parse_args()
+dev = torch.device("cuda:0")
+S, L = a.size, a.levels
+g = torch.Generator(device="cpu").manual_seed(7)
+f1 = torch.randn(1, 128, S, S, S, generator=g).to(dev)
+f2 = torch.randn(1, 128, S, S, S, generator=g).to(dev)
+c = (dvccorr.coords_grid_3d(1, S, S, S, torch.device("cpu")) + (torch.rand(1, 3, S, S, S, generator=g) * 4 - 2)).to(dev)
+K = L * 729
+w = ((torch.rand(96, K, generator=g) * 2 - 1) / K ** 0.5).to(dev)
+b = ((torch.rand(96, generator=g) * 2 - 1) / K ** 0.5).to(dev)
+res = {}
+with torch.no_grad():
+    blk = dvccorr.CorrBlockFused(f1, f2, L, 4, precision="bf16")
+    for v in [int(x) for x in a.ablate.split(",")]:
+        _lib.set_tuning("fused_ablate", v)
+        blk.lookup_convc1(c, w, b)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.reps):
+            blk.lookup_convc1(c, w, b)
+        e1.record()
+        torch.cuda.synchronize()
+        res[v] = round(e0.elapsed_time(e1) / a.reps, 3)
+        print(f"ablate {v}: {res[v]} ms per lookup_convc1", flush=True)
+    _lib.set_tuning("fused_ablate", 0)
+print(json.dumps({"size": S, "levels": L, "ms": res}))

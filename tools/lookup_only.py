@@ -19,6 +19,7 @@ ap.add_argument("--reps", type=int, default=4)
 ap.add_argument("--variant", type=int, default=0)
 ap.add_argument("--impl", default="materialised")
 ap.add_argument("--tune", default="", help="comma list key=value of dvc_set_tuning knobs")
+ap.add_argument("--convc1", action="store_true", help="lookup_convc1 (convc1 fused) instead of the lookup")
 a = ap.parse_args()
 _lib.set_tuning("lookup_variant", a.variant)
 for kv in filter(None, a.tune.split(",")):
@@ -33,7 +34,10 @@ c = (dvccorr.coords_grid_3d(1, S, S, S, torch.device("cpu")) + (torch.rand(1, 3,
 with torch.no_grad():
     cls = dvccorr.CorrBlock if a.impl == "materialised" else dvccorr.CorrBlockFused
     blk = cls(f1, f2, a.levels, 4, precision=a.precision)
+    K = a.levels * 729
+    w = ((torch.rand(96, K, generator=g) * 2 - 1) / K ** 0.5).to(dev)
+    bias = ((torch.rand(96, generator=g) * 2 - 1) / K ** 0.5).to(dev)
     for _ in range(a.reps):
-        out = blk(c)
+        out = blk.lookup_convc1(c, w, bias) if a.convc1 else blk(c)
 torch.cuda.synchronize()
 print("ok", float(out.abs().sum()))
