@@ -258,7 +258,7 @@ int dvc_set_tuning(const char *key, int value) {
         return DVC_OK;
     }
     if (!strcmp(key, "fused_ablate")) {
-        if (value < 0 || value > 15) return fail(DVC_ERR_INVALID, "set_tuning: fused_ablate %d", value);
+        if (value < 0 || value > 31) return fail(DVC_ERR_INVALID, "set_tuning: fused_ablate %d", value);
         g_fused_ablate = value;
         return DVC_OK;
     }

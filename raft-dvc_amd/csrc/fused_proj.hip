@@ -90,7 +90,9 @@ __global__ __launch_bounds__(256) void k_otf_keys(LookupArgs A, int b, int ncx, 
     keys[q] = ((unsigned long long)cell << 32) | (unsigned long long)(unsigned)q;
 }
 
-template <int R, int KS>
+// ABL (diagnostics only, never the product path; capi "fused_ablate"): 1 no phase 1, 2 no producers,
+// 4 no convc1 MFMA, 8 no window writes, 16 no target loads
+template <int R, int KS, int ABL>
 __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict__ Q, const bf16_t *__restrict__ Tt,
                                                        LookupArgs A, const unsigned long long *__restrict__ keys,
                                                        int b, int Cp, long long t_rows, float scale,
@@ -134,8 +136,6 @@ __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict_
         (void *)(((unsigned long long)tbhi << 32) | tblo), (short)0, t_bytes, 0x00020000);
 
     const int legacy = buni(A.legacy);
-    const int ablate = buni(A.ablate);   // diagnostics only (capi "fused_ablate"): 1 no phase 1, 2 no producers,
-                                         // 4 no convc1 MFMA, 8 no window writes, 16 no target loads
     unsigned sink = 0;
     const f32x2 sc2 = {scale, scale};
     const int trash = C::TRASH + lane * 4;
@@ -182,7 +182,7 @@ __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict_
         __syncthreads();   // the previous level's phase-2 reads are done
 
         // ---------------- phase 1: window dots on MFMA (k_fused_box's loop) ----------------
-        if (ny > 0 && nx > 0 && nz > 0 && !(ablate & 1)) {
+        if (ny > 0 && nx > 0 && nz > 0 && !(ABL & 1)) {
             // MFMA B operands, reloaded per level (L2 hits) so that they are not live in phase 2:
             // block j = slots 16 j .. 16 j + 15, lane i holds the query of slot 16 j + (i & 15),
             // channels 32 ks + 8 (i >> 4) .. + 7 (v_mfma_f32_16x16x32_bf16 B layout)
@@ -216,7 +216,7 @@ __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict_
                 const long long rowbase = offl + ((long long)(ys + pl.by) * Wl + (xs0 + pl.bx)) * Dpl;
                 const int off = z0 + m16 <= ze ? (int)(((rowbase + z0 + m16) * Cp + 8 * h4) * 2) : 0x7fff0000;
                 advance(pl);
-                if (ablate & 16) {
+                if constexpr ((ABL & 16) != 0) {
 #pragma unroll
                     for (int ks = 0; ks < KS; ++ks) dst[ks] = bq[0][ks];
                     return;
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict_
                     const f32x2 hi = f32x2{d[j][2], d[j][3]} * sc2;
                     const unsigned p01 = __builtin_bit_cast(unsigned, __builtin_convertvector(lo, bf16x2));
                     const unsigned p23 = __builtin_bit_cast(unsigned, __builtin_convertvector(hi, bf16x2));
-                    if (ablate & 8) {
+                    if constexpr ((ABL & 8) != 0) {
                         sink ^= p01 ^ p23;
                         continue;
                     }
@@ -288,19 +288,22 @@ __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict_
         __syncthreads();   // every window complete
 
         // ---------------- phase 2: interpolation -> X tile -> convc1 on MFMA ----------------
+        // (the interpolation weights are the producers' only: the others skip their divisions)
         const unsigned char *myw = win + lane * C::WQ;
         float wv0[n], wv1[n];
-#pragma unroll
-        for (int tt = 0; tt < n; ++tt) {
-            axis_weights(ax.pv, ax.kv, tt - R, ax.vn, ax.vu, wv0[tt], wv1[tt]);
-            wv0[tt] = (unsigned)(iv + tt) < (unsigned)Dl ? wv0[tt] : 0.0f;
-            wv1[tt] = (unsigned)(iv + tt + 1) < (unsigned)Dl ? wv1[tt] : 0.0f;
-        }
         f32x2 w0p[NP], w1p[NP];
+        if constexpr (NU > 0) {
 #pragma unroll
-        for (int i = 0; i < NP; ++i) {
-            w0p[i] = f32x2{wv0[2 * i], wv0[2 * i + 1]};
-            w1p[i] = f32x2{wv1[2 * i], wv1[2 * i + 1]};
+            for (int tt = 0; tt < n; ++tt) {
+                axis_weights(ax.pv, ax.kv, tt - R, ax.vn, ax.vu, wv0[tt], wv1[tt]);
+                wv0[tt] = (unsigned)(iv + tt) < (unsigned)Dl ? wv0[tt] : 0.0f;
+                wv1[tt] = (unsigned)(iv + tt + 1) < (unsigned)Dl ? wv1[tt] : 0.0f;
+            }
+#pragma unroll
+            for (int i = 0; i < NP; ++i) {
+                w0p[i] = f32x2{wv0[2 * i], wv0[2 * i + 1]};
+                w1p[i] = f32x2{wv1[2 * i], wv1[2 * i + 1]};
+            }
         }
         float wx0[NU > 0 ? NU : 1], wx1[NU > 0 ? NU : 1];
 #pragma unroll
@@ -338,7 +341,7 @@ __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict_
                 for (int ks = 0; ks < NWV; ++ks) wa[ks] = wr[(ks * OT + ot) * 64];
             }
             unsigned xw[16];   // producer: this wave's 32-k slice of row a as f16 pairs
-            if constexpr (NU > 0) if (!(ablate & 2)) {
+            if constexpr (NU > 0 && !(ABL & 2)) {
                 float wy0, wy1;
                 axis_weights(ax.ph, ax.kh, a - R, ax.hs, ax.hs, wy0, wy1);
                 wy0 = (unsigned)(ih + a) < (unsigned)Hl ? wy0 : 0.0f;
@@ -384,13 +387,13 @@ __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict_
                 }
             }
             __syncthreads();   // the consumers have read row a - 1 of X
-            if constexpr (NU > 0) if (!(ablate & 2)) {
+            if constexpr (NU > 0 && !(ABL & 2)) {
                 u32x4 *dst = reinterpret_cast<u32x4 *>(xs + lane * C::XROW + wave * 64);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) dst[j] = u32x4{xw[4 * j], xw[4 * j + 1], xw[4 * j + 2], xw[4 * j + 3]};
             }
             __syncthreads();   // row a complete in X
-            if (cons && !(ablate & 4)) {
+            if (cons && !(ABL & 4)) {
 #pragma unroll
                 for (int ks = 0; ks < NWV; ++ks) {
                     f16x8 xb[4];
@@ -426,7 +429,7 @@ __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict_
             if (ok) *reinterpret_cast<f32x4 *>(rows_out + ((long long)b * Nq + qrow[j]) * C::COUT + o0) = v;
         }
     }
-    if ((ablate & 8) && sink == 0x9e3779b9u) rows_out[0] = (float)sink;   // keeps the diagnostics' dots live
+    if ((ABL & 8) && sink == 0x9e3779b9u) rows_out[0] = (float)sink;   // keeps the diagnostics' dots live
 }
 
 // [B][Nq][96] -> (B, 96, Nq): 64 queries x 96 channels per block through LDS
@@ -479,10 +482,22 @@ static void launch_fused_proj(const bf16_t *Q, const bf16_t *Tt, const LookupArg
                               int b, int Cp, long long t_rows, float scale, float *rows, hipStream_t s) {
     const long long nchunks = (A.Nq + 63) / 64;
     const unsigned grid = (unsigned)(8 * ((nchunks + 7) / 8));
+    if constexpr (R == 4) {   // diagnostics instances (C_pad 128 only)
+        if (A.ablate && Cp == 128) {
+#define DVC_FPROJ_ABL(V) \
+    case V: k_fused_proj<4, 4, V><<<grid, 512, 0, s>>>(Q, Tt, A, keys, b, Cp, t_rows, scale, rows); return;
+            switch (A.ablate) {
+                DVC_FPROJ_ABL(1) DVC_FPROJ_ABL(2) DVC_FPROJ_ABL(3) DVC_FPROJ_ABL(4) DVC_FPROJ_ABL(6)
+                DVC_FPROJ_ABL(7) DVC_FPROJ_ABL(8) DVC_FPROJ_ABL(16) DVC_FPROJ_ABL(24)
+            default: break;
+            }
+#undef DVC_FPROJ_ABL
+        }
+    }
     switch (Cp / 32) {
-    case 1: k_fused_proj<R, 1><<<grid, 512, 0, s>>>(Q, Tt, A, keys, b, Cp, t_rows, scale, rows); break;
-    case 2: k_fused_proj<R, 2><<<grid, 512, 0, s>>>(Q, Tt, A, keys, b, Cp, t_rows, scale, rows); break;
-    default: k_fused_proj<R, 4><<<grid, 512, 0, s>>>(Q, Tt, A, keys, b, Cp, t_rows, scale, rows); break;
+    case 1: k_fused_proj<R, 1, 0><<<grid, 512, 0, s>>>(Q, Tt, A, keys, b, Cp, t_rows, scale, rows); break;
+    case 2: k_fused_proj<R, 2, 0><<<grid, 512, 0, s>>>(Q, Tt, A, keys, b, Cp, t_rows, scale, rows); break;
+    default: k_fused_proj<R, 4, 0><<<grid, 512, 0, s>>>(Q, Tt, A, keys, b, Cp, t_rows, scale, rows); break;
     }
 }
 

@@ -18,7 +18,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--size", type=int, default=128)
 ap.add_argument("--levels", type=int, default=2)
 ap.add_argument("--reps", type=int, default=3)
-ap.add_argument("--ablate", default="0,1,2,4,8,16,6,7")
+ap.add_argument("--ablate", default="0,1,3,7,2,4,6,8,16,24")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 S, L = a.size, a.levels
