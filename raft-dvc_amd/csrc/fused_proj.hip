@@ -49,16 +49,23 @@ namespace dvc {
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
+// Window rows hold NW + 2 bf16 starting at an EVEN offset from the union's z start (st = iv or iv - 1),
+// so the MFMA epilogue writes value PAIRS (4-byte stores, one predicate per pair) and phase 2 realigns
+// the run by 0 or 16 bits.  Phase 2 keeps window planes 0 and 1 in registers from the start (each
+// plane is read one row ahead), so the X tile of query q lives in q's own dead planes 0-1: 64 windows
+// of (2r+2)^2 x (2r+4) values are the whole LDS (151 KB at r = 4).
 template <int R> struct OtfProjCfg {
     static constexpr int n = 2 * R + 1, NW = 2 * R + 2, NP = n / 2;
-    static constexpr int WROW = NW * 2;                       // bytes of one window z-row (bf16)
-    static constexpr int WQ = NW * NW * WROW + 8;             // bytes per query window (+8: banks)
+    static constexpr int WZ = NW + 2;                         // stored values per window z-row
+    static constexpr int WROW = WZ * 2;                       // bytes of one window z-row (bf16)
+    static constexpr int WQ = ((NW * NW * WROW + 15) & ~15) + 16;   // bytes per query window (16-B
+                                                                    // aligned; 16-B reads of 16 windows
+                                                                    // at r = 4 cover the 64 banks once)
     static constexpr int GUARD = 64;
     static constexpr int TRASH = GUARD + 64 * WQ;             // per-lane scratch slots
-    static constexpr int WIN_BYTES = (TRASH + 64 * 4 + GUARD + 15) & ~15;
+    static constexpr int LDS = (TRASH + 64 * 4 + GUARD + 15) & ~15;
     static constexpr int NWV = (n + 2) / 3;                   // producer waves, 3 output columns each
-    static constexpr int XROW = NWV * 64 + 16;                // bytes per query row of X (+16: banks)
-    static constexpr int LDS = WIN_BYTES + 64 * XROW;
+    static_assert(2 * NW * WROW >= NWV * 64, "X row of a query must fit its window planes 0-1");
     static constexpr int NWAVES = 8;
     static constexpr int CONS0 = 2;                           // consumer waves CONS0 .. CONS0 + 5: one 16-channel tile each
     static constexpr int COUT = 96, OT = COUT / 16;
@@ -100,8 +107,7 @@ __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict_
     using C = OtfProjCfg<R>;
     constexpr int n = C::n, NW = C::NW, NP = C::NP, NWV = C::NWV, OT = C::OT;
     __shared__ __attribute__((aligned(16))) unsigned char smem[C::LDS];
-    unsigned char *win = smem + C::GUARD;       // [64 q][NW wy][NW wx][NW z] bf16
-    unsigned char *xs = smem + C::WIN_BYTES;    // [64 q][XROW] fp16
+    unsigned char *win = smem + C::GUARD;       // [64 q][NW wy][NW wx][WZ z] bf16; X row of q at win + q WQ
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const long long Nq = A.Nq;
@@ -166,17 +172,22 @@ __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict_
         const int ny = ye - ys + 1, nx = xe - xs0 + 1, nz = ze - zs + 1;
         const int nzb = (nz + 15) / 16;
 
-        // per B block j: the window origin of slot 16 j + m16 and its LDS base; a value of target
-        // (y, x, z) lands at wb[j] + (y NW + x) WROW + 2 z
+        // stored z-row of this lane's window starts at st (even offset from zs), so the run starts at
+        // offset iv - st in {0, 1}
+        const int st = iv - ((iv - zs) & 1);
+        // per B block j: the window origin of slot 16 j + m16 and its LDS base; the PAIR of targets
+        // (y, x, z0 + 4 h4 + 2 p + {0, 1}) lands at wb[j] + (y NW + x) WROW + 2 z0 + 4 p when
+        // 0 <= z0 + 4 h4 + 2 p - st <= NW (t = z0 - ov[j] below)
         int oh[4], ou[4], ov[4], wb[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int src = 16 * j + m16;
             const int sh = __shfl(ih, src);
+            const int stj = __shfl(st, src);
             oh[j] = __shfl((int)live, src) ? sh : -BIG;
             ou[j] = __shfl(iu, src);
-            ov[j] = __shfl(iv, src) - 4 * h4;   // lane holds z = z0 + 4 h4 + k
-            wb[j] = C::GUARD + src * C::WQ - (sh * NW + ou[j]) * C::WROW - ov[j] * 2;
+            ov[j] = stj - 4 * h4;
+            wb[j] = C::GUARD + src * C::WQ - (sh * NW + ou[j]) * C::WROW - stj * 2 + 8 * h4;
         }
 
         __syncthreads();   // the previous level's phase-2 reads are done
@@ -252,14 +263,10 @@ __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict_
                     const bool rok = (unsigned)(y - oh[j]) < (unsigned)NW && (unsigned)(x - ou[j]) < (unsigned)NW;
                     const int t0 = z0 - ov[j];
                     const int base = wb[j] + rowu;
-                    const int a0 = rok && (unsigned)(t0 + 0) < (unsigned)NW ? base + 0 : trash;
-                    const int a1 = rok && (unsigned)(t0 + 1) < (unsigned)NW ? base + 2 : trash;
-                    const int a2 = rok && (unsigned)(t0 + 2) < (unsigned)NW ? base + 4 : trash;
-                    const int a3 = rok && (unsigned)(t0 + 3) < (unsigned)NW ? base + 6 : trash;
-                    *reinterpret_cast<unsigned short *>(smem + a0) = (unsigned short)p01;
-                    *reinterpret_cast<unsigned short *>(smem + a1) = (unsigned short)(p01 >> 16);
-                    *reinterpret_cast<unsigned short *>(smem + a2) = (unsigned short)p23;
-                    *reinterpret_cast<unsigned short *>(smem + a3) = (unsigned short)(p23 >> 16);
+                    const int a0 = rok && (unsigned)t0 <= (unsigned)NW ? base : trash;
+                    const int a1 = rok && (unsigned)(t0 + 2) <= (unsigned)NW ? base + 4 : trash;
+                    *reinterpret_cast<unsigned *>(smem + a0) = p01;
+                    *reinterpret_cast<unsigned *>(smem + a1) = p23;
                 }
             };
             bf16x8 a0[KS], a1[KS];
@@ -313,12 +320,21 @@ __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict_
             wx0[uu] = (unsigned)(iu + u) < (unsigned)Wl ? wx0[uu] : 0.0f;
             wx1[uu] = (unsigned)(iu + u + 1) < (unsigned)Wl ? wx1[uu] : 0.0f;
         }
-        auto lerp_col = [&](int wp, int k, BRun<n> &z) {
-            const unsigned *p = reinterpret_cast<const unsigned *>(myw + (wp * NW + u0 + k) * C::WROW);
+        const unsigned rsh = (unsigned)(iv - st) * 16u;   // run offset in the stored row, in bits
+        // window plane wp, columns u0 .. u0 + NU: the raw stored dwords (prefetched one row ahead)
+        auto load_raw = [&](int wp, unsigned (&raw)[NU + 1][NW / 2 + 1]) {
+#pragma unroll
+            for (int k = 0; k <= NU; ++k) {
+                const unsigned *p = reinterpret_cast<const unsigned *>(myw + (wp * NW + u0 + k) * C::WROW);
+#pragma unroll
+                for (int i = 0; i <= NW / 2; ++i) raw[k][i] = p[i];
+            }
+        };
+        auto lerp_col = [&](const unsigned (&dw)[NW / 2 + 1], BRun<n> &z) {
             float r[NW];
 #pragma unroll
             for (int i = 0; i < NW / 2; ++i) {
-                const unsigned w = p[i];
+                const unsigned w = __builtin_amdgcn_alignbit(dw[i + 1], dw[i], rsh);
                 r[2 * i] = __uint_as_float(w << 16);
                 r[2 * i + 1] = __uint_as_float(w & 0xffff0000u);
             }
@@ -329,9 +345,12 @@ __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict_
             z.t = __builtin_fmaf(r[n], wv1[n - 1], r[n - 1] * wv0[n - 1]);
         };
         BRun<n> zp[NU + 1];
+        unsigned raw[NU + 1][NW / 2 + 1];
         if constexpr (NU > 0) {
+            load_raw(0, raw);
 #pragma unroll
-            for (int k = 0; k <= NU; ++k) lerp_col(0, k, zp[k]);
+            for (int k = 0; k <= NU; ++k) lerp_col(raw[k], zp[k]);
+            load_raw(1, raw);
         }
         for (int a = 0; a < n; ++a) {
             f16x8 wa[NWV];
@@ -346,36 +365,34 @@ __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict_
                 axis_weights(ax.ph, ax.kh, a - R, ax.hs, ax.hs, wy0, wy1);
                 wy0 = (unsigned)(ih + a) < (unsigned)Hl ? wy0 : 0.0f;
                 wy1 = (unsigned)(ih + a + 1) < (unsigned)Hl ? wy1 : 0.0f;
-                BRun<n> zprev;
+                // plane a + 1 from the prefetched dwords, then the loads of plane a + 2 for the next row
+                BRun<n> zc[NU + 1];
+#pragma unroll
+                for (int k = 0; k <= NU; ++k) lerp_col(raw[k], zc[k]);
+                if (a + 2 < NW) load_raw(a + 2, raw);
                 unsigned xr[NU * NP];
                 float xt[NU];
 #pragma unroll
-                for (int k = 0; k <= NU; ++k) {
-                    BRun<n> zcur;
-                    lerp_col(a + 1, k, zcur);
-                    if (k >= 1) {
-                        const int uu = k - 1;
-                        const float p00 = wx0[uu] * wy0, p10 = wx1[uu] * wy0;
-                        const float p01 = wx0[uu] * wy1, p11 = wx1[uu] * wy1;
-                        const f32x2 P00 = {p00, p00}, P10 = {p10, p10}, P01 = {p01, p01}, P11 = {p11, p11};
+                for (int uu = 0; uu < NU; ++uu) {
+                    const float p00 = wx0[uu] * wy0, p10 = wx1[uu] * wy0;
+                    const float p01 = wx0[uu] * wy1, p11 = wx1[uu] * wy1;
+                    const f32x2 P00 = {p00, p00}, P10 = {p10, p10}, P01 = {p01, p01}, P11 = {p11, p11};
 #pragma unroll
-                        for (int i = 0; i < NP; ++i) {
-                            f32x2 v = P00 * zp[uu].p[i];
-                            v = __builtin_elementwise_fma(P10, zp[uu + 1].p[i], v);
-                            v = __builtin_elementwise_fma(P01, zprev.p[i], v);
-                            v = __builtin_elementwise_fma(P11, zcur.p[i], v);
-                            xr[uu * NP + i] = __builtin_bit_cast(unsigned, __builtin_convertvector(v, f16x2));
-                        }
-                        float v = p00 * zp[uu].t;
-                        v = __builtin_fmaf(p10, zp[uu + 1].t, v);
-                        v = __builtin_fmaf(p01, zprev.t, v);
-                        v = __builtin_fmaf(p11, zcur.t, v);
-                        xt[uu] = v;
-                        zp[uu] = zprev;
+                    for (int i = 0; i < NP; ++i) {
+                        f32x2 v = P00 * zp[uu].p[i];
+                        v = __builtin_elementwise_fma(P10, zp[uu + 1].p[i], v);
+                        v = __builtin_elementwise_fma(P01, zc[uu].p[i], v);
+                        v = __builtin_elementwise_fma(P11, zc[uu + 1].p[i], v);
+                        xr[uu * NP + i] = __builtin_bit_cast(unsigned, __builtin_convertvector(v, f16x2));
                     }
-                    zprev = zcur;
-                    if (k == NU) zp[k] = zcur;
+                    float v = p00 * zp[uu].t;
+                    v = __builtin_fmaf(p10, zp[uu + 1].t, v);
+                    v = __builtin_fmaf(p01, zc[uu].t, v);
+                    v = __builtin_fmaf(p11, zc[uu + 1].t, v);
+                    xt[uu] = v;
                 }
+#pragma unroll
+                for (int k = 0; k <= NU; ++k) zp[k] = zc[k];
                 // slice order (dvc_proj_pack): pairs (column uu, v = 2i, 2i + 1), then the tails, then zeros
                 constexpr int T0 = NU * NP;
 #pragma unroll
@@ -386,9 +403,9 @@ __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict_
                     xw[T0 + p] = __builtin_bit_cast(unsigned, __builtin_convertvector(t2, f16x2));
                 }
             }
-            __syncthreads();   // the consumers have read row a - 1 of X
+            __syncthreads();   // the consumers have read row a - 1 of X (and, at a = 0, planes 0-1 are in registers)
             if constexpr (NU > 0 && !(ABL & 2)) {
-                u32x4 *dst = reinterpret_cast<u32x4 *>(xs + lane * C::XROW + wave * 64);
+                u32x4 *dst = reinterpret_cast<u32x4 *>(win + lane * C::WQ + wave * 64);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) dst[j] = u32x4{xw[4 * j], xw[4 * j + 1], xw[4 * j + 2], xw[4 * j + 3]};
             }
@@ -399,7 +416,7 @@ __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict_
                     f16x8 xb[4];
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                        xb[j] = *reinterpret_cast<const f16x8 *>(xs + (16 * j + m16) * C::XROW + ks * 64 + h4 * 16);
+                        xb[j] = *reinterpret_cast<const f16x8 *>(win + (16 * j + m16) * C::WQ + ks * 64 + h4 * 16);
 #pragma unroll
                     for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[ks], xb[j], acc[j], 0, 0, 0);
                 }
