@@ -213,7 +213,7 @@ static void launch_fused_tile(const bf16_t *Q, const bf16_t *Tt, const LookupArg
     }
 }
 
-template <int R, int KS, int NWAVES, int TY, int TX, int TZ>
+template <int R, int KS, int NWAVES, int TY, int TX, int TZ, int ABL>
 __global__ void k_fused_box(const bf16_t *, const bf16_t *, LookupArgs, int, long long, int, int, int, float);
 
 template <int R, int NWV, int TY, int TX, int TZ>
@@ -224,10 +224,22 @@ static void launch_fused_box(const bf16_t *Q, const bf16_t *Tt, const LookupArgs
                     ngz = ((Dq + TZ - 1) / TZ + 1) / 2;
     const long long tiles = (long long)A.B * ngy * ngx * ngz * 32;
     const unsigned grid = (unsigned)(8 * ((tiles + 7) / 8));
+    if constexpr (R == 4 && NWV == 8 && TY == 2 && TX == 2 && TZ == 16) {   // diagnostics (fused_ablate)
+        if (A.ablate && Cp == 128) {
+#define DVC_FBOX_ABL(V) \
+    case V: k_fused_box<4, 4, 8, 2, 2, 16, V><<<grid, 512, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); return;
+            switch (A.ablate) {
+                DVC_FBOX_ABL(1) DVC_FBOX_ABL(2) DVC_FBOX_ABL(3) DVC_FBOX_ABL(4) DVC_FBOX_ABL(8) DVC_FBOX_ABL(12)
+                DVC_FBOX_ABL(13)
+            default: break;
+            }
+#undef DVC_FBOX_ABL
+        }
+    }
     switch (Cp / 32) {
-    case 1: k_fused_box<R, 1, NWV, TY, TX, TZ><<<grid, 64 * NWV, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;
-    case 2: k_fused_box<R, 2, NWV, TY, TX, TZ><<<grid, 64 * NWV, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;
-    default: k_fused_box<R, 4, NWV, TY, TX, TZ><<<grid, 64 * NWV, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;
+    case 1: k_fused_box<R, 1, NWV, TY, TX, TZ, 0><<<grid, 64 * NWV, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;
+    case 2: k_fused_box<R, 2, NWV, TY, TX, TZ, 0><<<grid, 64 * NWV, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;
+    default: k_fused_box<R, 4, NWV, TY, TX, TZ, 0><<<grid, 64 * NWV, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;
     }
 }
 

@@ -40,18 +40,22 @@
 
 namespace dvc {
 
+// Window z-rows hold NW + 2 bf16 from an EVEN offset of the union's z start (st = iv or iv - 1): the
+// epilogue stores value pairs (one predicate per pair) and phase 2 realigns the run by 0 or 16 bits.
 template <int R, int NWAVES> struct BoxCfg {
     static constexpr int n = 2 * R + 1;
     static constexpr int NW = 2 * R + 2;
-    static constexpr int WROW = NW * 2;                           // bytes of one window z-row (bf16)
-    static constexpr int WQ = NW * NW * WROW + 8;                 // bytes per query window (+8: banks)
+    static constexpr int WROW = (NW + 2) * 2;                     // bytes of one window z-row (bf16)
+    static constexpr int WQ = ((NW * NW * WROW + 15) & ~15) + 16; // bytes per query window (16-B aligned)
     static constexpr int GUARD = 64;
     static constexpr int TRASH = GUARD + 64 * WQ;                 // per-lane scratch slots
     static constexpr int LDS = (TRASH + 64 * 4 + GUARD + 15) & ~15;
     static constexpr int COLS = NWAVES >= 8 ? 2 : 3;              // output columns per wave (phase 2)
 };
 
-template <int R, int KS, int NWAVES, int TY, int TX, int TZ>
+// ABL (diagnostics only, never the product path; capi "fused_ablate"): 1 no output stores, 2 no window
+// dots, 4 no target loads, 8 no window writes
+template <int R, int KS, int NWAVES, int TY, int TX, int TZ, int ABL>
 __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__restrict__ Q,
                                                               const bf16_t *__restrict__ Tt, LookupArgs A,
                                                               int Cp, long long t_rows, int Hq, int Wq, int Dq,
@@ -131,7 +135,6 @@ __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__re
     const int out_bytes = buni((int)(n * n * Nq * 4));
     const f32x2 sc2 = {scale, scale};
     const int trash = C::TRASH + lane * 4;
-    const int ablate = buni(A.ablate);
     unsigned sink = 0;
     const int u0 = wave * C::COLS;
     __syncthreads();   // LDS cleared
@@ -141,7 +144,7 @@ __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__re
             buniptr(obase + ((long long)a * n * n + (long long)u * chstep_u) * Nq), (short)0, out_bytes, 0x00020000);
     };
     auto store = [&](__amdgpu_buffer_rsrc_t rs, int v, float val) {
-        if (!(ablate & 1)) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val), rs, q4, v * vstep, 2);
+        if constexpr (!(ABL & 1)) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val), rs, q4, v * vstep, 2);
     };
 
     auto level = [&](int l, auto nu_c) {
@@ -174,25 +177,29 @@ __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__re
         const int ny = ye - ys + 1, nx = xe - xs + 1, nz = ze - zs + 1;
         const int nzb = (nz + 15) / 16;
 
+        // the stored z-row of this lane's window starts at st (even offset from zs): run offset iv - st
+        const int st = iv - ((iv - zs) & 1);
         // per B block j: this lane's query is 16 j + m16; its window origin and LDS base.
-        // A value of target (y, x, z) lands at
-        //   win + q * WQ + ((y - ih) * NW + (x - iu)) * WROW + (z - iv) * 2
-        // = wb[j] + (y * NW + x) * WROW + z * 2            (wb[j] folds the query's part)
+        // The pair of targets (y, x, z0 + 4 h4 + 2 p + {0, 1}) lands at
+        //   win + q * WQ + ((y - ih) * NW + (x - iu)) * WROW + (z0 + 4 h4 + 2 p - st) * 2
+        // = wb[j] + (y * NW + x) * WROW + z0 * 2 + 4 p     (wb[j] folds the query's part)
+        // when 0 <= z0 + 4 h4 + 2 p - st <= NW (t0 = z0 - ov[j] below)
         int oh[4], ou[4], ov[4], wb[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int src = 16 * j + m16;
             const int sh = __shfl(ih, src);                 // |ih| < 2^20: finite or "dead" origins
+            const int stj = __shfl(st, src);
             oh[j] = __shfl((int)live, src) ? sh : -BIG;     // dead / inactive queries take no values
             ou[j] = __shfl(iu, src);
-            ov[j] = __shfl(iv, src) - 4 * h4;               // lane holds z = z0 + 4 h4 + k
-            wb[j] = C::GUARD + src * C::WQ - (sh * NW + ou[j]) * C::WROW - ov[j] * 2;
+            ov[j] = stj - 4 * h4;
+            wb[j] = C::GUARD + src * C::WQ - (sh * NW + ou[j]) * C::WROW - stj * 2 + 8 * h4;
         }
 
         __syncthreads();   // previous level's phase-2 reads are done
 
         // ---------------- phase 1: window dots on MFMA ----------------
-        if (ny > 0 && nx > 0 && nz > 0 && !(ablate & 2)) {
+        if (ny > 0 && nx > 0 && nz > 0 && !(ABL & 2)) {
             // this wave's iterations it = wave + NWAVES k over (row, z block), row-major,
             // z block fastest; (by, bx, zb) advance without divisions
             const int total = ny * nx * nzb;
@@ -218,7 +225,7 @@ __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__re
                 const long long rowbase = offl + ((long long)(ys + pl.by) * Wl + (xs + pl.bx)) * Dpl;
                 const int off = z0 + m16 <= ze ? (int)(((rowbase + z0 + m16) * Cp + 8 * h4) * 2) : 0x7fff0000;
                 advance(pl);
-                if (ablate & 4) {   // diagnostics: no target loads
+                if constexpr ((ABL & 4) != 0) {   // diagnostics: no target loads
 #pragma unroll
                     for (int ks = 0; ks < KS; ++ks) dst[ks] = bq[0][ks];
                     return;
@@ -247,21 +254,17 @@ __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__re
                     const f32x2 hi = f32x2{acc[j][2], acc[j][3]} * sc2;
                     const unsigned p01 = __builtin_bit_cast(unsigned, __builtin_convertvector(lo, bf16x2));
                     const unsigned p23 = __builtin_bit_cast(unsigned, __builtin_convertvector(hi, bf16x2));
-                    if (ablate & 8) {   // diagnostics: no window writes (keep the values live)
+                    if constexpr ((ABL & 8) != 0) {   // diagnostics: no window writes (keep the values live)
                         sink ^= p01 ^ p23;
                         continue;
                     }
                     const bool rok = (unsigned)(y - oh[j]) < (unsigned)NW && (unsigned)(x - ou[j]) < (unsigned)NW;
-                    const int t0 = z0 - ov[j];                   // window z of this lane's k = 0 value
+                    const int t0 = z0 - ov[j];                   // stored-row offset of this lane's first pair
                     const int base = wb[j] + rowu;
-                    const int a0 = rok && (unsigned)(t0 + 0) < (unsigned)NW ? base + 0 : trash;
-                    const int a1 = rok && (unsigned)(t0 + 1) < (unsigned)NW ? base + 2 : trash;
-                    const int a2 = rok && (unsigned)(t0 + 2) < (unsigned)NW ? base + 4 : trash;
-                    const int a3 = rok && (unsigned)(t0 + 3) < (unsigned)NW ? base + 6 : trash;
-                    *reinterpret_cast<unsigned short *>(smem + a0) = (unsigned short)p01;
-                    *reinterpret_cast<unsigned short *>(smem + a1) = (unsigned short)(p01 >> 16);
-                    *reinterpret_cast<unsigned short *>(smem + a2) = (unsigned short)p23;
-                    *reinterpret_cast<unsigned short *>(smem + a3) = (unsigned short)(p23 >> 16);
+                    const int a0 = rok && (unsigned)t0 <= (unsigned)NW ? base : trash;
+                    const int a1 = rok && (unsigned)(t0 + 2) <= (unsigned)NW ? base + 4 : trash;
+                    *reinterpret_cast<unsigned *>(smem + a0) = p01;
+                    *reinterpret_cast<unsigned *>(smem + a1) = p23;
                 }
             };
             // two operand sets in flight; the MFMAs of iteration k + 1 are issued before the
@@ -315,12 +318,16 @@ __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__re
             wx0[uu] = (unsigned)(iu + u) < (unsigned)Wl ? wx0[uu] : 0.0f;
             wx1[uu] = (unsigned)(iu + u + 1) < (unsigned)Wl ? wx1[uu] : 0.0f;
         }
+        const unsigned rsh = (unsigned)(iv - st) * 16u;   // run offset in the stored row, in bits
         auto lerp_col = [&](int wp, int k, BRun<n> &z) {
             const unsigned *p = reinterpret_cast<const unsigned *>(myw + (wp * NW + u0 + k) * C::WROW);
+            unsigned dw[NW / 2 + 1];
+#pragma unroll
+            for (int i = 0; i <= NW / 2; ++i) dw[i] = p[i];
             float r[NW];
 #pragma unroll
             for (int i = 0; i < NW / 2; ++i) {
-                const unsigned w = p[i];
+                const unsigned w = __builtin_amdgcn_alignbit(dw[i + 1], dw[i], rsh);
                 r[2 * i] = __uint_as_float(w << 16);
                 r[2 * i + 1] = __uint_as_float(w & 0xffff0000u);
             }
@@ -384,12 +391,12 @@ __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__re
         else if (wave == NWC - 1) level(l, std::integral_constant<int, NU_LAST>{});
         else level(l, std::integral_constant<int, 0>{});
     }
-    if ((ablate & 8) && sink == 0x9e3779b9u) A.out[0] = (float)sink;   // keeps the diagnostics' dots live
+    if ((ABL & 8) && sink == 0x9e3779b9u) A.out[0] = (float)sink;   // keeps the diagnostics' dots live
 }
 
-#define DVC_FBOX_INST1(R, KS, NWV, TY, TX, TZ)                                                                 \
-    template __global__ void k_fused_box<R, KS, NWV, TY, TX, TZ>(const bf16_t *, const bf16_t *, LookupArgs, int, \
-                                                                 long long, int, int, int, float);
+#define DVC_FBOX_INST1(R, KS, NWV, TY, TX, TZ)                                                                    \
+    template __global__ void k_fused_box<R, KS, NWV, TY, TX, TZ, 0>(const bf16_t *, const bf16_t *, LookupArgs, int, \
+                                                                    long long, int, int, int, float);
 #define DVC_FBOX_INST(R, NWV, TY, TX, TZ)                                                                      \
     DVC_FBOX_INST1(R, 1, NWV, TY, TX, TZ) DVC_FBOX_INST1(R, 2, NWV, TY, TX, TZ) DVC_FBOX_INST1(R, 4, NWV, TY, TX, TZ)
 #define DVC_FBOX_ALLR(NWV, TY, TX, TZ)                                                                         \
@@ -398,5 +405,11 @@ __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__re
 DVC_FBOX_ALLR(8, 2, 2, 16)
 DVC_FBOX_ALLR(4, 2, 2, 16)
 DVC_FBOX_ALLR(8, 4, 4, 4)
+
+// diagnostics instances (fused_ablate) of the default configuration
+#define DVC_FBOX_ABL(V) \
+    template __global__ void k_fused_box<4, 4, 8, 2, 2, 16, V>(const bf16_t *, const bf16_t *, LookupArgs, int, \
+                                                               long long, int, int, int, float);
+DVC_FBOX_ABL(1) DVC_FBOX_ABL(2) DVC_FBOX_ABL(3) DVC_FBOX_ABL(4) DVC_FBOX_ABL(8) DVC_FBOX_ABL(12) DVC_FBOX_ABL(13)
 
 }  // namespace dvc
