@@ -142,9 +142,12 @@ static bool tile_ok(const LookupArgs &A, size_t esz) {
 
 // Fewer query tiles than 2 x the 256 CUs (e.g. one rank's 4096-row slab at config #3: 64 tiles) leave most
 // of the chip idle; then each workgroup takes one (tile, level) pair instead of a tile's whole level loop,
-// and if that is still short of 4 workgroups per CU, one (tile, level, 3-row chunk) triple (ACH = 3:
-// each chunk reads 4 of the 2r+2 window planes).
-static constexpr long long kSplitTiles = 512, kSplitRows = 1024;
+// and if that is still short of 2 workgroups per CU, one (tile, level, 5-row chunk) triple (ACH = 5: the
+// two chunks read 6 and 5 of the 2r+2 window planes).  Round 2 A/B (tools/ab_split.py, bitwise-equal
+// outputs): at 64 tiles ACH 5 24.9 us, no row split 26.6, ACH 3 28.0, ACH 2 31.1; at 128 tiles no row
+// split 39.1, ACH 5 41.2, ACH 3 43.6.
+static constexpr long long kSplitTiles = 512, kSplitRows = 512;
+static thread_local int g_split_ach = 5;          // rows per chunk of the row split (0 = no row split; 2, 3, 5)
 
 template <typename T, bool NT, int ACH>
 static void launch_tile_r(const LookupArgs &A, dim3 blocks, unsigned threads, hipStream_t s) {
@@ -165,8 +168,10 @@ static void launch_tile_nt(const LookupArgs &A0, hipStream_t s) {
     const long long tiles = (long long)A.B * A.nqb;
     A.split_levels = tiles < kSplitTiles && A.nl > 1;
     const int n = 2 * A.r + 1;
-    const bool split_rows = NT && A.split_levels && tiles * A.nl < kSplitRows && n > 3;
-    const dim3 blocks((unsigned)tiles, A.split_levels ? (unsigned)A.nl : 1u, split_rows ? (unsigned)((n + 2) / 3) : 1u);
+    const int ach = g_split_ach;
+    const bool split_rows = NT && A.split_levels && tiles * A.nl < kSplitRows && n > ach && ach > 0;
+    const dim3 blocks((unsigned)tiles, A.split_levels ? (unsigned)A.nl : 1u,
+                      split_rows ? (unsigned)((n + ach - 1) / ach) : 1u);
     const unsigned threads = 64u * (unsigned)((2 * A.r + 3) / 3);
     if constexpr (std::is_same<T, bf16_t>::value && NT) {
         if (A.r == 4 && A.ablate >= 1 && A.ablate <= 3) {   // diagnostics only
@@ -178,7 +183,12 @@ static void launch_tile_nt(const LookupArgs &A0, hipStream_t s) {
         }
     }
     if constexpr (NT) {
-        if (split_rows) { launch_tile_r<T, NT, 3>(A, blocks, threads, s); return; }
+        if (split_rows) {
+            if (ach == 2) launch_tile_r<T, NT, 2>(A, blocks, threads, s);
+            else if (ach == 5) launch_tile_r<T, NT, 5>(A, blocks, threads, s);
+            else launch_tile_r<T, NT, 3>(A, blocks, threads, s);
+            return;
+        }
     }
     launch_tile_r<T, NT, 0>(A, blocks, threads, s);
 }
@@ -231,6 +241,12 @@ int dvc_set_tuning(const char *key, int value) {
     if (!strcmp(key, "lookup_ldpol")) {
         if (value < 0 || value > 3) return fail(DVC_ERR_INVALID, "set_tuning: lookup_ldpol %d", value);
         g_lookup_ldpol = value;
+        return DVC_OK;
+    }
+    if (!strcmp(key, "split_ach")) {
+        if (value != 0 && value != 2 && value != 3 && value != 5)
+            return fail(DVC_ERR_INVALID, "set_tuning: split_ach %d (0, 2, 3 or 5)", value);
+        g_split_ach = value;
         return DVC_OK;
     }
     if (!strcmp(key, "build_stpol")) {

@@ -467,7 +467,9 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3 + (PROJ ? 1 : 0)), 2) void k_
 #define DVC_TILE_INST(T, R)                                                      \
     template __global__ void k_lookup_tile<T, R, false, 0, false, 0>(LookupArgs); \
     template __global__ void k_lookup_tile<T, R, true, 0, false, 0>(LookupArgs);  \
-    template __global__ void k_lookup_tile<T, R, true, 0, false, 3>(LookupArgs);
+    template __global__ void k_lookup_tile<T, R, true, 0, false, 2>(LookupArgs);  \
+    template __global__ void k_lookup_tile<T, R, true, 0, false, 3>(LookupArgs);  \
+    template __global__ void k_lookup_tile<T, R, true, 0, false, 5>(LookupArgs);
 DVC_TILE_INST(float, 1) DVC_TILE_INST(float, 2) DVC_TILE_INST(float, 3)
 DVC_TILE_INST(float, 4) DVC_TILE_INST(float, 5) DVC_TILE_INST(float, 6)
 DVC_TILE_INST(bf16_t, 1) DVC_TILE_INST(bf16_t, 2) DVC_TILE_INST(bf16_t, 3)
