@@ -31,6 +31,7 @@
 #include <stdio.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -47,7 +48,7 @@ struct BwdArgs {
     const float *gout;     // (B, L*n^3, Nq)
     float *gwin;           // level l at goff[l]: [B][Nq][nwh * nwu * nwv]
     long long Nq, row_stride;
-    int B, L, legacy, Hq, Wq, Dq, Cp;
+    int B, L, legacy, Hq, Wq, Dq, Cp, R;
     int H[DVC_MAX_LEVELS], W[DVC_MAX_LEVELS], D[DVC_MAX_LEVELS], Dp[DVC_MAX_LEVELS], zero[DVC_MAX_LEVELS];
     int generic[DVC_MAX_LEVELS];                                  // legacy level with W != D
     int nwh[DVC_MAX_LEVELS], nwu[DVC_MAX_LEVELS], nwv[DVC_MAX_LEVELS];   // window box per level (2r+2 each if not generic)
@@ -395,6 +396,176 @@ __global__ __launch_bounds__(256) void k_grad_q(const TT *__restrict__ Tt, float
 }
 
 // ---------------------------------------------------------------------------------
+// 2b. bf16 path of step 2 on the matrix cores.  Per 4x4x4 query box, union row (y, x) and
+// 16-target z batch: dQ[64 queries][Cp] += G[64 queries][16 targets] x T[16 targets][Cp] on
+// v_mfma_f32_32x32x16_bf16 (queries = M, channels = N, targets = K); G = the queries' window
+// gradients (8 consecutive z per lane: contiguous in dwin), split into bf16 hi + lo as in 4b.
+// The B operand needs 8 consecutive targets per lane: k_transpose_targets first writes the
+// packed targets channel-major, Ttr[b][c][row] (+32 zero-filled slack elements).
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_transpose_targets(const bf16_t *__restrict__ Tt, bf16_t *__restrict__ Ttr,
+                                                           long long rows, long long rows_pad, int Cp) {
+    __shared__ __attribute__((aligned(16))) bf16_t tile[64][128 + 8];
+    const int b = blockIdx.y;
+    const long long r0 = (long long)blockIdx.x * 64;
+    const int nch = Cp / 8;
+    const bf16_t *src = Tt + (long long)b * rows * Cp;
+    for (int id = threadIdx.x; id < 64 * nch; id += 256) {
+        const int r = id / nch, ch = id - r * nch;
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (r0 + r < rows) v = *reinterpret_cast<const u32x4 *>(src + (r0 + r) * Cp + ch * 8);
+        *reinterpret_cast<u32x4 *>(&tile[r][ch * 8]) = v;
+    }
+    __syncthreads();
+    bf16_t *dst = Ttr + (long long)b * Cp * rows_pad;
+    for (int id = threadIdx.x; id < Cp * 32; id += 256) {
+        const int c = id >> 5, rp = id & 31;
+        if (r0 + 2 * rp < rows_pad) {
+            const unsigned lo = tile[2 * rp][c], hi = tile[2 * rp + 1][c];
+            *reinterpret_cast<unsigned *>(dst + (long long)c * rows_pad + r0 + 2 * rp) = lo | (hi << 16);
+        }
+    }
+}
+
+template <int NCT>   // channel tiles of 32 (C_pad / 32)
+__global__ __launch_bounds__(256) void k_grad_q_mfma(const bf16_t *__restrict__ Ttr, long long rows_pad,
+                                                     float *__restrict__ dQ, BwdArgs A) {
+    constexpr int NREG = 2 * NCT * 16;
+    __shared__ __attribute__((aligned(16))) float red[2][NREG][64];
+    const int lane = threadIdx.x & 63, m = lane & 31, h = lane >> 5;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nbz = (A.Dq + 3) >> 2, nbx = (A.Wq + 3) >> 2, nby = (A.Hq + 3) >> 2;
+    int t = blockIdx.x;
+    const int bz = t % nbz; t /= nbz;
+    const int bx = t % nbx; t /= nbx;
+    const int by = t % nby;
+    const int b = t / nby;
+    // lane-as-query view (union bounds): query i = lane of the box
+    const int qy = by * 4 + (lane >> 4), qx = bx * 4 + ((lane >> 2) & 3), qz = bz * 4 + (lane & 3);
+    const bool active = qy < A.Hq && qx < A.Wq && qz < A.Dq;
+    const long long q = active ? ((long long)qy * A.Wq + qx) * A.Dq + qz : 0;
+    float cy = 0.0f, cx = 0.0f, cz = 0.0f;
+    if (active) load_coords(A.coords, b, A.Nq, q, cy, cx, cz);
+    f32x16 acc[2][NCT];
+#pragma unroll
+    for (int T = 0; T < 2; ++T)
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[T][ct][i] = 0.0f;
+    const int BIG = 1 << 29;
+    const bf16_t *tb = Ttr + (long long)b * A.Cp * rows_pad;
+    for (int l = 0; l < A.L; ++l) {
+        if (A.zero[l]) continue;
+        const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
+        const int nh = A.nwh[l], nu = A.nwu[l], nv = A.nwv[l];
+        WinAxes ax;
+        bw_axes(A, l, cy, cx, cz, ax);
+        int ih, iu, iv;
+        bw_origin(A, l, A.R, ax, ih, iu, iv);
+        const bool live = active && !ax.dead;
+        const int ys = max(bw_wave_min(live ? ih : BIG), 0), ye = min(bw_wave_max(live ? ih : -BIG) + nh - 1, Hl - 1);
+        const int xs = max(bw_wave_min(live ? iu : BIG), 0), xe = min(bw_wave_max(live ? iu : -BIG) + nu - 1, Wl - 1);
+        const int nx = xe - xs + 1;
+        const int nrows = (ye >= ys && nx > 0) ? (ye - ys + 1) * nx : 0;
+        // A-operand rows: queries 32 T + m
+        int ohT[2], ouT[2], ovT[2];
+        bool lvT[2];
+        const float *gT[2];
+#pragma unroll
+        for (int T = 0; T < 2; ++T) {
+            const int src = 32 * T + m;
+            ohT[T] = __shfl(ih, src); ouT[T] = __shfl(iu, src); ovT[T] = __shfl(iv, src);
+            lvT[T] = __shfl((int)live, src) != 0;
+            const long long qT = (long long)__shfl((int)q, src);
+            gT[T] = A.gwin + A.goff[l] + ((long long)b * A.Nq + qT) * bw_nw3(A, l);
+        }
+        for (int row = w; row < nrows; row += 4) {
+            const int y = ys + row / nx, x = xs + row % nx;
+            bool rokT[2];
+            int gofT[2];
+#pragma unroll
+            for (int T = 0; T < 2; ++T) {
+                const int wy = y - ohT[T], wx = x - ouT[T];
+                rokT[T] = lvT[T] && (unsigned)wy < (unsigned)nh && (unsigned)wx < (unsigned)nu;
+                gofT[T] = (wy * nu + wx) * nv;
+            }
+            // z range of this row: the windows of the box's queries that contain it
+            const bool rk = live && (unsigned)(y - ih) < (unsigned)nh && (unsigned)(x - iu) < (unsigned)nu;
+            if (__ballot(rk) == 0) continue;
+            const int zlo = max(bw_wave_min(rk ? iv : BIG), 0);
+            const int zhi = min(bw_wave_max(rk ? iv : -BIG) + nv - 1, Dl - 1);
+            const long long trow = A.off[l] + ((long long)y * Wl + x) * Dpl;
+            for (int z0 = zlo; z0 <= zhi; z0 += 16) {
+                bf16x8 tbv[NCT];
+#pragma unroll
+                for (int ct = 0; ct < NCT; ++ct) {
+                    u32x4 v;
+                    __builtin_memcpy(&v, tb + (long long)(32 * ct + m) * rows_pad + trow + z0 + 8 * h, 16);
+                    tbv[ct] = __builtin_bit_cast(bf16x8, v);
+                }
+#pragma unroll
+                for (int T = 0; T < 2; ++T) {
+                    const int wz0 = z0 + 8 * h - ovT[T];
+                    bf16x8 ghi, glo;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const int wz = wz0 + k;
+                        const float g = rokT[T] && (unsigned)wz < (unsigned)nv ? gT[T][gofT[T] + wz] : 0.0f;
+                        const __bf16 hi = (__bf16)g;
+                        ghi[k] = hi;
+                        glo[k] = (__bf16)(g - (float)hi);
+                    }
+#pragma unroll
+                    for (int ct = 0; ct < NCT; ++ct) {
+                        acc[T][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ghi, tbv[ct], acc[T][ct], 0, 0, 0);
+                        acc[T][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(glo, tbv[ct], acc[T][ct], 0, 0, 0);
+                    }
+                }
+            }
+        }
+    }
+    auto put = [&](int slot) {
+#pragma unroll
+        for (int T = 0; T < 2; ++T)
+#pragma unroll
+            for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) red[slot][(T * NCT + ct) * 16 + i][lane] = acc[T][ct][i];
+    };
+    auto add = [&](int slot) {
+#pragma unroll
+        for (int T = 0; T < 2; ++T)
+#pragma unroll
+            for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc[T][ct][i] += red[slot][(T * NCT + ct) * 16 + i][lane];
+    };
+    __syncthreads();
+    if (w >= 2) put(w - 2);
+    __syncthreads();
+    if (w < 2) add(w);
+    __syncthreads();
+    if (w == 1) put(0);
+    __syncthreads();
+    if (w != 0) return;
+    add(0);
+    // acc[T][ct][i] = D[query 32 T + 8 (i / 4) + 4 h + i % 4][channel 32 ct + m]
+#pragma unroll
+    for (int T = 0; T < 2; ++T)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int qi = 32 * T + 8 * (i >> 2) + 4 * h + (i & 3);
+            const int y = by * 4 + (qi >> 4), x = bx * 4 + ((qi >> 2) & 3), z = bz * 4 + (qi & 3);
+            if (y < A.Hq && x < A.Wq && z < A.Dq) {
+                float *dst = dQ + ((long long)b * A.Nq + ((long long)y * A.Wq + x) * A.Dq + z) * A.Cp + m;
+#pragma unroll
+                for (int ct = 0; ct < NCT; ++ct) dst[32 * ct] = acc[T][ct][i] * A.scale;
+            }
+        }
+}
+
+// ---------------------------------------------------------------------------------
 // 3. queries of (b, l) keyed by window-origin cell: o' = origin + nw - 1 per axis, in
 // [0, S_l + nw - 2] exactly when the window meets the level; others sort last.
 // ---------------------------------------------------------------------------------
@@ -534,6 +705,187 @@ __global__ __launch_bounds__(256) void k_grad_t(const TT *__restrict__ Qp, const
     }
 }
 
+// ---------------------------------------------------------------------------------
+// 4b. bf16 path of step 4 on the matrix cores.  Per target brick and batch of 16 streamed
+// queries, dT[64 targets][Cp] += G[64 targets][16 queries] x Q[16 queries][Cp] on
+// v_mfma_f32_32x32x16_bf16 (targets = M, channels = N, queries = K).  G (the fp32 window
+// gradients) enters as two bf16 terms, hi = bf16(g) and lo = bf16(g - hi), so the product
+// keeps ~16 mantissa bits of g (Q is bf16 already): two MFMAs per tile.  The B operand needs 8
+// consecutive queries per lane: k_qt_sorted first writes Q transposed and permuted into the
+// level's sorted order, Qt[c][i] = Q[q_i][c] (zeros past Nq), so a lane's 8 queries are one
+// 16-byte load.
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_qt_sorted(const bf16_t *__restrict__ Q,
+                                                   const unsigned long long *__restrict__ keys,
+                                                   bf16_t *__restrict__ Qt, long long Nq, long long NqPad, int Cp,
+                                                   int b) {
+    __shared__ __attribute__((aligned(16))) bf16_t tile[64][128 + 8];
+    const long long i0 = (long long)blockIdx.x * 64;
+    const int nch = Cp / 8;
+    for (int id = threadIdx.x; id < 64 * nch; id += 256) {
+        const int r = id / nch, ch = id - r * nch;
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (i0 + r < Nq) {
+            const long long q = (long long)(keys[i0 + r] & 0xffffffffull);
+            v = *reinterpret_cast<const u32x4 *>(Q + ((long long)b * Nq + q) * Cp + ch * 8);
+        }
+        *reinterpret_cast<u32x4 *>(&tile[r][ch * 8]) = v;
+    }
+    __syncthreads();
+    for (int id = threadIdx.x; id < Cp * 32; id += 256) {
+        const int c = id >> 5, qp = id & 31;
+        const unsigned lo = tile[2 * qp][c], hi = tile[2 * qp + 1][c];
+        *reinterpret_cast<unsigned *>(Qt + (long long)c * NqPad + i0 + 2 * qp) = lo | (hi << 16);
+    }
+}
+
+template <int NCT>   // channel tiles of 32 (C_pad / 32)
+__global__ __launch_bounds__(256) void k_grad_t_mfma(const bf16_t *__restrict__ Qt, long long NqPad,
+                                                     const unsigned long long *__restrict__ keys,
+                                                     const int *__restrict__ starts, float *__restrict__ dT,
+                                                     float *__restrict__ dTp, int nsplit, BwdArgs A, int b, int l) {
+    constexpr int NREG = 2 * NCT * 16;   // accumulator floats per lane
+    __shared__ __attribute__((aligned(16))) float red[2][NREG][64];
+    const int lane = threadIdx.x & 63, m = lane & 31, h = lane >> 5;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
+    const int nh = A.nwh[l], nu = A.nwu[l], nv = A.nwv[l];
+    const long long nw3 = bw_nw3(A, l);
+    const int nbz = (Dl + 3) >> 2, nbx = (Wl + 3) >> 2;
+    const int split = (int)(blockIdx.x % nsplit);
+    const int brick = (int)(blockIdx.x / nsplit);
+    int t = brick;
+    const int bz = t % nbz; t /= nbz;
+    const int bx = t % nbx;
+    const int by = t / nbx;
+    // this lane's A-operand rows: targets 32 T + m of the brick
+    int tyT[2], txT[2], tzT[2];
+    bool tvT[2];
+#pragma unroll
+    for (int T = 0; T < 2; ++T) {
+        const int i = 32 * T + m;
+        tyT[T] = by * 4 + (i >> 4); txT[T] = bx * 4 + ((i >> 2) & 3); tzT[T] = bz * 4 + (i & 3);
+        tvT[T] = tyT[T] < Hl && txT[T] < Wl && tzT[T] < Dl;
+    }
+    const int CX = Wl + nu - 1, CZ = Dl + nv - 1;
+    const int oy0 = by * 4, oy1 = min(by * 4 + 3, Hl - 1) + nh - 1;
+    const int ox0 = bx * 4, ox1 = min(bx * 4 + 3, Wl - 1) + nu - 1;
+    const int oz0 = bz * 4, oz1 = min(bz * 4 + 3, Dl - 1) + nv - 1;
+    const int nox = ox1 - ox0 + 1, nrows = (oy1 - oy0 + 1) * nox;
+    const float *gl = A.gwin + A.goff[l] + (long long)b * A.Nq * nw3;
+    f32x16 acc[2][NCT];
+#pragma unroll
+    for (int T = 0; T < 2; ++T)
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[T][ct][i] = 0.0f;
+    for (int row = 4 * split + w; row < nrows; row += 4 * nsplit) {
+        const int oy = oy0 + row / nox, ox = ox0 + row % nox;
+        const long long cbase = ((long long)oy * CX + ox) * CZ;
+        const int s = starts[cbase + oz0], e = starts[cbase + oz1 + 1];
+        int pyxT[2];
+        bool yxT[2];
+#pragma unroll
+        for (int T = 0; T < 2; ++T) {
+            const int py = tyT[T] - oy + nh - 1, px = txT[T] - ox + nu - 1;
+            yxT[T] = tvT[T] && (unsigned)py < (unsigned)nh && (unsigned)px < (unsigned)nu;
+            pyxT[T] = (py * nu + px) * nv;
+        }
+        for (int base = s; base < e; base += 64) {
+            const int nk = min(64, e - base);
+            const unsigned long long key = lane < nk ? keys[base + lane] : 0ull;
+            const int qq_l = (int)(unsigned)(key & 0xffffffffu);
+            const int oz_l = (int)((long long)(key >> 32) - cbase);
+            for (int kb = 0; 16 * kb < nk; ++kb) {
+                const int k0 = 16 * kb + 8 * h;   // this lane's 8 queries: stream slots k0 .. k0 + 7
+                // B operands first (their loads fly while G is gathered)
+                bf16x8 qb[NCT];
+#pragma unroll
+                for (int ct = 0; ct < NCT; ++ct) {
+                    const bf16_t *src = Qt + (long long)(32 * ct + m) * NqPad + base + k0;
+                    u32x4 v;
+                    __builtin_memcpy(&v, src, 16);   // 2-byte aligned 16-byte load
+                    qb[ct] = __builtin_bit_cast(bf16x8, v);
+                }
+                float g[2][8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int idx = k0 + k;
+                    const bool in = idx < nk;
+                    const int qq = __shfl(qq_l, in ? idx : 0);
+                    const int oz = __shfl(oz_l, in ? idx : 0);
+#pragma unroll
+                    for (int T = 0; T < 2; ++T) {
+                        const int pz = tzT[T] - oz + nv - 1;
+                        const bool ok = in && yxT[T] && (unsigned)pz < (unsigned)nv;
+                        g[T][k] = ok ? gl[(long long)qq * nw3 + pyxT[T] + pz] : 0.0f;
+                    }
+                }
+#pragma unroll
+                for (int T = 0; T < 2; ++T) {
+                    bf16x8 ghi, glo;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const __bf16 hi = (__bf16)g[T][k];
+                        ghi[k] = hi;
+                        glo[k] = (__bf16)(g[T][k] - (float)hi);
+                    }
+#pragma unroll
+                    for (int ct = 0; ct < NCT; ++ct) {
+                        acc[T][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ghi, qb[ct], acc[T][ct], 0, 0, 0);
+                        acc[T][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(glo, qb[ct], acc[T][ct], 0, 0, 0);
+                    }
+                }
+            }
+        }
+    }
+    // cross-wave sum in a fixed order: waves 2, 3 -> 0, 1; wave 1 -> 0
+    auto put = [&](int slot) {
+#pragma unroll
+        for (int T = 0; T < 2; ++T)
+#pragma unroll
+            for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) red[slot][(T * NCT + ct) * 16 + i][lane] = acc[T][ct][i];
+    };
+    auto add = [&](int slot) {
+#pragma unroll
+        for (int T = 0; T < 2; ++T)
+#pragma unroll
+            for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc[T][ct][i] += red[slot][(T * NCT + ct) * 16 + i][lane];
+    };
+    __syncthreads();
+    if (w >= 2) put(w - 2);
+    __syncthreads();
+    if (w < 2) add(w);
+    __syncthreads();
+    if (w == 1) put(0);
+    __syncthreads();
+    if (w != 0) return;
+    add(0);
+    // D layout (32x32 MFMA): acc[T][ct][i] = D[target 32 T + 8 (i / 4) + 4 h + i % 4][channel 32 ct + m]
+    const float sc = A.scale;
+#pragma unroll
+    for (int T = 0; T < 2; ++T)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int ti = 32 * T + 8 * (i >> 2) + 4 * h + (i & 3);
+            const int y = by * 4 + (ti >> 4), x = bx * 4 + ((ti >> 2) & 3), z = bz * 4 + (ti & 3);
+            if (nsplit > 1) {
+                float *pp = dTp + (((long long)split * gridDim.x / nsplit + brick) * 64 + ti) * A.Cp + m;
+#pragma unroll
+                for (int ct = 0; ct < NCT; ++ct) pp[32 * ct] = acc[T][ct][i];
+            } else if (y < Hl && x < Wl && z < Dl) {
+                float *dst = dT + ((long long)b * A.row_stride + A.off[l] + ((long long)y * Wl + x) * Dpl + z) * A.Cp + m;
+#pragma unroll
+                for (int ct = 0; ct < NCT; ++ct) dst[32 * ct] = acc[T][ct][i] * sc;
+            }
+        }
+}
+
 // dT rows of level l <- scale * sum over the nsplit partials (split order: deterministic).  One thread per
 // (brick target, channel pair).
 __global__ __launch_bounds__(256) void k_grad_t_reduce(const float *__restrict__ dTp, float *__restrict__ dT,
@@ -610,7 +962,9 @@ __global__ __launch_bounds__(256) void k_unpack_sum(UnpackArgs U) {
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct BwdPlan {
-    size_t gwin, dq, dt, keys, starts, temp, part, total;
+    size_t gwin, dq, dt, keys, starts, temp, part, qt, ttr, total;
+    long long rows_pad;  // Ttr row length (pyramid rows + slack for the 16-target batches)
+    long long nq_pad;   // Qt row length (sorted queries + zero padding for the 16-query batches)
     int nw[DVC_MAX_LEVELS][3];   // window box (h, u, v) per level
     long long goff[DVC_MAX_LEVELS];
 };
@@ -669,7 +1023,11 @@ static void bwd_plan(int B, long long Nq, const dvc_layout &lay, int radius, boo
                                    (size_t)Nq, 0u, 64u, (hipStream_t)0);
     P.temp = al256(tb);
     P.part = al256(std::max<size_t>(part, 256));
-    P.total = P.gwin + P.dq + P.dt + 2 * P.keys + P.starts + P.temp + P.part;
+    P.nq_pad = ((Nq + 16 + 63) / 64) * 64;
+    P.qt = al256((size_t)P.nq_pad * lay.c_pad * sizeof(bf16_t));   // bf16 path only (sized always)
+    P.rows_pad = ((lay.row_stride + 32 + 1) / 2) * 2;
+    P.ttr = al256((size_t)B * lay.c_pad * P.rows_pad * sizeof(bf16_t));   // bf16 path only (sized always)
+    P.total = P.gwin + P.dq + P.dt + 2 * P.keys + P.starts + P.temp + P.part + P.qt + P.ttr;
 }
 
 // workspace for either convention (the legacy plan is larger only when a level has W != D)
@@ -690,6 +1048,8 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     int *starts = (int *)(ws + P.gwin + P.dq + P.dt + 2 * P.keys);
     void *temp = ws + P.gwin + P.dq + P.dt + 2 * P.keys + P.starts;
     float *dtp = (float *)(ws + P.gwin + P.dq + P.dt + 2 * P.keys + P.starts + P.temp);
+    bf16_t *qt = (bf16_t *)(ws + P.gwin + P.dq + P.dt + 2 * P.keys + P.starts + P.temp + P.part);
+    bf16_t *ttr = (bf16_t *)(ws + P.gwin + P.dq + P.dt + 2 * P.keys + P.starts + P.temp + P.part + P.qt);
     A.gwin = (float *)ws;
     auto launched = [&](const char *what) {
         hipError_t e = hipGetLastError();
@@ -709,7 +1069,18 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
         if (!launched("win_grad_generic")) return DVC_ERR_LAUNCH;
     }
     const long long boxes = (long long)A.B * ((A.Hq + 3) / 4) * ((A.Wq + 3) / 4) * ((A.Dq + 3) / 4);
-    k_grad_q<TT, R><<<(unsigned)boxes, 256, 0, s>>>(Tt, dq, A);
+    if constexpr (std::is_same<TT, bf16_t>::value) {
+        dim3 tg((unsigned)((P.rows_pad + 63) / 64), (unsigned)A.B);
+        k_transpose_targets<<<tg, 256, 0, s>>>(Tt, ttr, A.row_stride, P.rows_pad, A.Cp);
+        if (!launched("transpose_targets")) return DVC_ERR_LAUNCH;
+        switch (A.Cp / 32) {
+        case 1: k_grad_q_mfma<1><<<(unsigned)boxes, 256, 0, s>>>(ttr, P.rows_pad, dq, A); break;
+        case 2: k_grad_q_mfma<2><<<(unsigned)boxes, 256, 0, s>>>(ttr, P.rows_pad, dq, A); break;
+        default: k_grad_q_mfma<4><<<(unsigned)boxes, 256, 0, s>>>(ttr, P.rows_pad, dq, A); break;
+        }
+    } else {
+        k_grad_q<TT, R><<<(unsigned)boxes, 256, 0, s>>>(Tt, dq, A);
+    }
     if (!launched("grad_q")) return DVC_ERR_LAUNCH;
     for (int b = 0; b < A.B; ++b)
         for (int l = 0; l < A.L; ++l) {
@@ -728,7 +1099,19 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
             if (!launched("cell_starts")) return DVC_ERR_LAUNCH;
             const long long bricks = (long long)((A.H[l] + 3) / 4) * ((A.W[l] + 3) / 4) * ((A.D[l] + 3) / 4);
             const int sp = grad_t_splits(lay, l, P.nw[l]);
-            k_grad_t<TT, R><<<(unsigned)(bricks * sp), 256, 0, s>>>(Q, kout, starts, dt, dtp, sp, A, b, l);
+            if constexpr (std::is_same<TT, bf16_t>::value) {
+                // matrix-core path: sorted + transposed query rows, then 16-query MFMA batches
+                k_qt_sorted<<<(unsigned)(P.nq_pad / 64), 256, 0, s>>>(Q, kout, qt, A.Nq, P.nq_pad, A.Cp, b);
+                if (!launched("qt_sorted")) return DVC_ERR_LAUNCH;
+                const unsigned g = (unsigned)(bricks * sp);
+                switch (A.Cp / 32) {
+                case 1: k_grad_t_mfma<1><<<g, 256, 0, s>>>(qt, P.nq_pad, kout, starts, dt, dtp, sp, A, b, l); break;
+                case 2: k_grad_t_mfma<2><<<g, 256, 0, s>>>(qt, P.nq_pad, kout, starts, dt, dtp, sp, A, b, l); break;
+                default: k_grad_t_mfma<4><<<g, 256, 0, s>>>(qt, P.nq_pad, kout, starts, dt, dtp, sp, A, b, l); break;
+                }
+            } else {
+                k_grad_t<TT, R><<<(unsigned)(bricks * sp), 256, 0, s>>>(Q, kout, starts, dt, dtp, sp, A, b, l);
+            }
             if (!launched("grad_t")) return DVC_ERR_LAUNCH;
             if (sp > 1) {
                 const long long nt = bricks * 64 * (A.Cp / 2);
@@ -790,7 +1173,7 @@ int corr_backward(const void *packed_q, const void *packed_t, const float *coord
     BwdArgs A{};
     A.coords = coords; A.gout = grad_out; A.Nq = Nq; A.row_stride = lay.row_stride;
     A.B = B; A.L = lay.num_levels; A.legacy = legacy; A.Wq = lay.W[0]; A.Dq = lay.D[0];
-    A.Hq = (int)(Nq / plane); A.Cp = lay.c_pad; A.scale = 1.0f / sqrtf((float)C);
+    A.Hq = (int)(Nq / plane); A.Cp = lay.c_pad; A.R = radius; A.scale = 1.0f / sqrtf((float)C);
     for (int l = 0; l < DVC_MAX_LEVELS; ++l) {
         A.H[l] = lay.H[l]; A.W[l] = lay.W[l]; A.D[l] = lay.D[l]; A.Dp[l] = lay.Dp[l];
         A.zero[l] = lay.zero_level[l]; A.off[l] = lay.offset[l];
