@@ -559,7 +559,7 @@ def backward_timing(args, f1, f2, coords, dims, dev, stream):
     nbytes = gout.numel() * 4 + cf.numel() * 4 + (q.numel() + t.numel()) * esz + 2 * B * C * Nq * 4
     flops = 2.0 * 2 * C * (2 * R + 2) ** 3 * L * B * Nq
     peak = BF16_PEAK_TFS if args.precision == "bf16" else F32_PEAK_TFS
-    return {"kernels": "k_win_grad + k_grad_q + radix sort + k_grad_t + k_unpack_sum (dvc_corr_backward)",
+    return {"kernels": "k_win_grad + k_grad_q_mfma + radix sort + k_grad_t_mfma + k_unpack_sum (dvc_corr_backward, bf16 path)",
             "avg_ms": round(ms, 4), "algorithmic_bytes": nbytes, "GB/s": round(nbytes / (ms * 1e-3) / 1e9, 1),
             "hbm_frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "flops": flops,
             "TFLOP/s": round(flops / (ms * 1e-3) / 1e12, 2),

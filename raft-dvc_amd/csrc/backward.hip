@@ -143,19 +143,28 @@ __global__ __launch_bounds__(256) void k_win_grad(BwdArgs A) {
     }
     const long long chu = A.legacy ? 1 : n, chv = A.legacy ? n : 1;
     const float *g = A.gout + (long long)bl * n * n * n * A.Nq + q;
-    for (int i = 0; i < NW; ++i) {
-        // window plane i collects output row a = i (corner 0) and a = i - 1 (corner 1)
+    // Window plane i collects output row a = i (corner 0) and a = i - 1 (corner 1).  Each output row
+    // is loaded once: row i - 1 stays in registers from the previous plane (ping-pong buffers).
+    float rowA[n][n], rowB[n][n];
+#pragma unroll
+    for (int j = 0; j < n; ++j)
+#pragma unroll
+        for (int v = 0; v < n; ++v) rowB[j][v] = 0.0f;
+    auto plane = [&](int i, float (&cur)[n][n], const float (&prev)[n][n]) {
         float wa0 = 0.0f, wa1 = 0.0f, t0, t1;
         if (i < n) {
             axis_weights(ax.ph, ax.kh, i - R, ax.hs, ax.hs, t0, t1);
             wa0 = (unsigned)(ih + i) < (unsigned)Hl ? t0 : 0.0f;
+            const float *g0 = g + (long long)i * n * n * A.Nq;   // output row a = i
+#pragma unroll
+            for (int j = 0; j < n; ++j)
+#pragma unroll
+                for (int v = 0; v < n; ++v) cur[j][v] = g0[(j * chu + v * chv) * A.Nq];
         }
         if (i >= 1) {
             axis_weights(ax.ph, ax.kh, i - 1 - R, ax.hs, ax.hs, t0, t1);
             wa1 = (unsigned)(ih + i) < (unsigned)Hl ? t1 : 0.0f;
         }
-        const float *g0 = g + (long long)i * n * n * A.Nq;         // output row a = i
-        const float *g1 = g + (long long)(i - 1) * n * n * A.Nq;   // output row a = i - 1
         float Pp[n];
 #pragma unroll
         for (int v = 0; v < n; ++v) Pp[v] = 0.0f;
@@ -167,11 +176,11 @@ __global__ __launch_bounds__(256) void k_win_grad(BwdArgs A) {
             if (j < n) {
                 if (i < n) {
 #pragma unroll
-                    for (int v = 0; v < n; ++v) Pc[v] = wa0 * g0[(j * chu + v * chv) * A.Nq];
+                    for (int v = 0; v < n; ++v) Pc[v] = wa0 * cur[j < n ? j : 0][v];
                 }
                 if (i >= 1) {
 #pragma unroll
-                    for (int v = 0; v < n; ++v) Pc[v] = __builtin_fmaf(wa1, g1[(j * chu + v * chv) * A.Nq], Pc[v]);
+                    for (int v = 0; v < n; ++v) Pc[v] = __builtin_fmaf(wa1, prev[j < n ? j : 0][v], Pc[v]);
                 }
             }
             const float wj0 = j < n ? wx0[j < n ? j : 0] : 0.0f;
@@ -191,6 +200,10 @@ __global__ __launch_bounds__(256) void k_win_grad(BwdArgs A) {
 #pragma unroll
             for (int v = 0; v < n; ++v) Pp[v] = Pc[v];
         }
+    };
+    for (int i = 0; i < NW; i += 2) {   // NW is even
+        plane(i, rowA, rowB);
+        plane(i + 1, rowB, rowA);
     }
 }
 
@@ -587,14 +600,21 @@ __global__ __launch_bounds__(256) void k_bw_keys(BwdArgs A, int b, int l, unsign
     keys[q] = ((unsigned long long)cell << 32) | (unsigned long long)(unsigned)q;
 }
 
-// starts[c] = first sorted index whose cell >= c, for c in [0, ncell]
+// starts[c] = first sorted index whose cell >= c, for c in [0, ncell]: one thread per cell, a binary
+// search over the sorted keys (a thread per key writing the cells up to the next key serialises the
+// long empty stretch after the last key)
 __global__ __launch_bounds__(256) void k_cell_starts(const unsigned long long *__restrict__ keys, long long Nq,
                                                      long long ncell, int *__restrict__ starts) {
-    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-    if (i > Nq) return;
-    const long long prev = i > 0 ? (long long)(keys[i - 1] >> 32) : -1;
-    const long long cur = i < Nq ? min((long long)(keys[i] >> 32), ncell) : ncell;
-    for (long long c = prev + 1; c <= cur; ++c) starts[c] = (int)i;
+    const long long c = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (c > ncell) return;
+    long long lo = 0, hi = Nq;   // first index in [lo, hi] with min(cell, ncell) >= c
+    while (lo < hi) {
+        const long long mid = (lo + hi) >> 1;
+        const long long cm = min((long long)(keys[mid] >> 32), ncell);
+        if (cm < c) lo = mid + 1;
+        else hi = mid;
+    }
+    starts[c] = (int)lo;
 }
 
 // ---------------------------------------------------------------------------------
@@ -1095,7 +1115,7 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
                 snprintf(err, errlen, "corr_backward: radix sort failed");
                 return DVC_ERR_RUNTIME;
             }
-            k_cell_starts<<<(unsigned)((A.Nq + 1 + 255) / 256), 256, 0, s>>>(kout, A.Nq, ncell, starts);
+            k_cell_starts<<<(unsigned)((ncell + 1 + 255) / 256), 256, 0, s>>>(kout, A.Nq, ncell, starts);
             if (!launched("cell_starts")) return DVC_ERR_LAUNCH;
             const long long bricks = (long long)((A.H[l] + 3) / 4) * ((A.W[l] + 3) / 4) * ((A.D[l] + 3) / 4);
             const int sp = grad_t_splits(lay, l, P.nw[l]);
