@@ -481,6 +481,9 @@ __global__ __launch_bounds__(256) void k_grad_q_mfma(const bf16_t *__restrict__ 
         const int xs = max(bw_wave_min(live ? iu : BIG), 0), xe = min(bw_wave_max(live ? iu : -BIG) + nu - 1, Wl - 1);
         const int nx = xe - xs + 1;
         const int nrows = (ye >= ys && nx > 0) ? (ye - ys + 1) * nx : 0;
+        // z range of the box's windows (at most 16 + 2r wide: one or two 16-target batches per row)
+        const int zlo = max(bw_wave_min(live ? iv : BIG), 0);
+        const int zhi = min(bw_wave_max(live ? iv : -BIG) + nv - 1, Dl - 1);
         // A-operand rows: queries 32 T + m
         int ohT[2], ouT[2], ovT[2];
         bool lvT[2];
@@ -503,11 +506,9 @@ __global__ __launch_bounds__(256) void k_grad_q_mfma(const bf16_t *__restrict__ 
                 rokT[T] = lvT[T] && (unsigned)wy < (unsigned)nh && (unsigned)wx < (unsigned)nu;
                 gofT[T] = (wy * nu + wx) * nv;
             }
-            // z range of this row: the windows of the box's queries that contain it
+            // rows of the union box that no window of the box contains
             const bool rk = live && (unsigned)(y - ih) < (unsigned)nh && (unsigned)(x - iu) < (unsigned)nu;
             if (__ballot(rk) == 0) continue;
-            const int zlo = max(bw_wave_min(rk ? iv : BIG), 0);
-            const int zhi = min(bw_wave_max(rk ? iv : -BIG) + nv - 1, Dl - 1);
             const long long trow = A.off[l] + ((long long)y * Wl + x) * Dpl;
             for (int z0 = zlo; z0 <= zhi; z0 += 16) {
                 bf16x8 tbv[NCT];
@@ -520,11 +521,16 @@ __global__ __launch_bounds__(256) void k_grad_q_mfma(const bf16_t *__restrict__ 
 #pragma unroll
                 for (int T = 0; T < 2; ++T) {
                     const int wz0 = z0 + 8 * h - ovT[T];
+                    // the 8 window values as two 16-byte loads (neighbouring rows' values and the 256-byte
+                    // guards around dwin are read and masked): row offset clamped to the query's window
+                    const float *gp = gT[T] + (rokT[T] ? gofT[T] : 0) + wz0;
+                    float gv[8];
+                    __builtin_memcpy(gv, gp, 32);
                     bf16x8 ghi, glo;
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
                         const int wz = wz0 + k;
-                        const float g = rokT[T] && (unsigned)wz < (unsigned)nv ? gT[T][gofT[T] + wz] : 0.0f;
+                        const float g = rokT[T] && (unsigned)wz < (unsigned)nv ? gv[k] : 0.0f;
                         const __bf16 hi = (__bf16)g;
                         ghi[k] = hi;
                         glo[k] = (__bf16)(g - (float)hi);
@@ -1033,7 +1039,7 @@ static void bwd_plan(int B, long long Nq, const dvc_layout &lay, int radius, boo
         const long long bricks = (long long)((lay.H[l] + 3) / 4) * ((lay.W[l] + 3) / 4) * ((lay.D[l] + 3) / 4);
         if (sp > 1) part = std::max<size_t>(part, (size_t)sp * (size_t)bricks * 64 * (size_t)lay.c_pad * sizeof(float));
     }
-    P.gwin = al256(gw);
+    P.gwin = al256(gw) + 512;   // + 256-byte guards before and after (k_grad_q_mfma's 8-float loads)
     P.dq = al256((size_t)B * Nq * lay.c_pad * sizeof(float));
     P.dt = al256((size_t)B * lay.row_stride * lay.c_pad * sizeof(float));
     P.keys = al256((size_t)Nq * sizeof(unsigned long long));
@@ -1070,7 +1076,7 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     float *dtp = (float *)(ws + P.gwin + P.dq + P.dt + 2 * P.keys + P.starts + P.temp);
     bf16_t *qt = (bf16_t *)(ws + P.gwin + P.dq + P.dt + 2 * P.keys + P.starts + P.temp + P.part);
     bf16_t *ttr = (bf16_t *)(ws + P.gwin + P.dq + P.dt + 2 * P.keys + P.starts + P.temp + P.part + P.qt);
-    A.gwin = (float *)ws;
+    A.gwin = (float *)(ws + 256);
     auto launched = [&](const char *what) {
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) {
