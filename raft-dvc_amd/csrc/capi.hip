@@ -79,7 +79,8 @@ static thread_local int g_build_variant = 1;      // 1 = two-barrier bf16-store 
 // 3 = k_fused_box 4x4x4 cubes, 8 waves, 4 = k_fused_box 2x2x16, 4 waves, 1 = k_fused_tile, 0 = two-stage VALU
 static thread_local int g_fused_variant = 2;
 static thread_local int g_upflow_rows = 8;        // output rows per k_upflow work item
-static thread_local int g_upflow_wgs = 1024;      // k_upflow grid (workgroups striding over the items)
+static thread_local int g_upflow_wgs = 1 << 30;   // k_upflow grid cap (workgroups striding over the items); round 2: one
+                                                  // workgroup per item, 178 -> 152 us at the #5 tail (tools/ab_upflow.py)
 static thread_local int g_pack_variant = 1;       // 1 = single-pass k_pack_pyramid where L <= 4, 0 = per-level launches
 static thread_local int g_fused_ablate = 0;       // diagnostics only: 1 = skip output stores, 2 = skip window dots (cube kernel)
 
