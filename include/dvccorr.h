@@ -206,6 +206,7 @@ int dvc_flow_step(const float *coords1, const float *delta_flow, float *coords1_
  * launches, on any stream), so the library holds no process-wide mutable state.
  *   "lookup_variant" 2 = LDS-staged tile kernel (default), 0 = walk with unaligned
  *                    16-byte run loads, 1 = walk with aligned chunks + v_perm shifter;
+ *   "upflow_staged"  1 = k_upflow through an LDS-staged low-res box (default), 0 = direct;
  *   "fused_variant", "build_variant", "upflow_rows", ... see capi.hip;
  *   "*_ablate"       diagnostics only, invalidates outputs. */
 int dvc_set_tuning(const char *key, int value);

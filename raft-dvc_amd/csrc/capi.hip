@@ -56,7 +56,7 @@ int corr_backward(const void *packed_q, const void *packed_t, const float *coord
                   size_t errlen);
 size_t backward_workspace_bytes(int B, long long Nq, const dvc_layout &lay, int radius);
 __global__ void k_coords_grid(float *, long long, int, int, int);
-template <bool DELTA, bool SUBGRID, int VEC>
+template <bool DELTA, bool SUBGRID, int VEC, bool STAGED>
 __global__ void k_upflow(const float *, const float *, float *, float *, long long, int, int, int, int, int, int, int,
                          float, float, float, float, float, float, int, int, int);
 }  // namespace dvc
@@ -78,9 +78,10 @@ static thread_local int g_build_variant = 1;      // 1 = two-barrier bf16-store 
 // fused lookup kernel where the MFMA path applies: 2 = k_fused_box 2x2x16, 8 waves (default),
 // 3 = k_fused_box 4x4x4 cubes, 8 waves, 4 = k_fused_box 2x2x16, 4 waves, 1 = k_fused_tile, 0 = two-stage VALU
 static thread_local int g_fused_variant = 2;
-static thread_local int g_upflow_rows = 8;        // output rows per k_upflow work item
+static thread_local int g_upflow_rows = 12;       // output rows per k_upflow work item (tools/ab_upflow.py)
 static thread_local int g_upflow_wgs = 1 << 30;   // k_upflow grid cap (workgroups striding over the items); round 2: one
                                                   // workgroup per item, 178 -> 152 us at the #5 tail (tools/ab_upflow.py)
+static thread_local int g_upflow_staged = 1;      // 1 = k_upflow stages an item's low-res box in LDS (all ratios <= 1)
 static thread_local int g_pack_variant = 1;       // 1 = single-pass k_pack_pyramid where L <= 4, 0 = per-level launches
 static thread_local int g_fused_ablate = 0;       // diagnostics only: 1 = skip output stores, 2 = skip window dots (cube kernel)
 
@@ -267,6 +268,11 @@ int dvc_set_tuning(const char *key, int value) {
     if (!strcmp(key, "upflow_rows")) {
         if (value < 1 || value > 64) return fail(DVC_ERR_INVALID, "set_tuning: upflow_rows %d outside [1, 64]", value);
         g_upflow_rows = value;
+        return DVC_OK;
+    }
+    if (!strcmp(key, "upflow_staged")) {
+        if (value < 0 || value > 1) return fail(DVC_ERR_INVALID, "set_tuning: upflow_staged %d", value);
+        g_upflow_staged = value;
         return DVC_OK;
     }
     if (!strcmp(key, "upflow_wgs")) {
@@ -715,16 +721,33 @@ static int launch_upflow(const float *lo, const float *delta, float *lo_out, flo
     // flow_up[:, c] *= target/in (a Python float, applied in float32), corr.py:242-251
     const float sh = (float)((double)H / h), sw = (float)((double)W / w), sd = (float)((double)D / d);
     hipStream_t s = (hipStream_t)stream;
-#define DVC_UPFLOW(DL, SG, V)                                                                                      \
-    k_upflow<DL, SG, V><<<blocks, 256, 0, s>>>(lo, DL ? delta : nullptr, SG ? lo_out : nullptr, up, B, C, h, w, d, \
-                                               H, W, D, rh, rw, rd, sh, sw, sd, nx, ny, rows)
-    if (!subgrid) {
-        if (vec == 4) DVC_UPFLOW(false, false, 4); else DVC_UPFLOW(false, false, 1);
-    } else if (delta) {
-        if (vec == 4) DVC_UPFLOW(true, true, 4); else DVC_UPFLOW(true, true, 1);
-    } else {
-        if (vec == 4) DVC_UPFLOW(false, true, 4); else DVC_UPFLOW(false, true, 1);
+    // staged kernel where every item's low-res box fits k_upflow's LDS tile (8192 floats; flow.hip):
+    // y rows <= floor((rows - 1) rh) + 3, x rows of a 1024-output chunk <= floor((nox - 1) rw) + 3,
+    // z <= d, or floor(1023 rd) + 3 when chunks never straddle two x rows (D % 1024 == 0)
+    bool staged = g_upflow_staged && vec == 4 && rh <= 1.0f && rw <= 1.0f && rd <= 1.0f;
+    if (staged) {
+        const long long nox = D >= 1024 ? 2 : 1023 / D + 2;
+        const long long nly = (long long)std::floor((double)(rows - 1) * rh) + 3;
+        const long long nlx = std::min<long long>((long long)std::floor((double)(nox - 1) * rw) + 3, w);
+        const long long nlz = D % 1024 == 0 ? std::min<long long>((long long)std::floor(1023.0 * rd) + 3, d) : d;
+        staged = std::min<long long>(nly, h) * nlx * nlz <= 8192;
     }
+#define DVC_UPFLOW(DL, SG, V, ST)                                                                                      \
+    k_upflow<DL, SG, V, ST><<<blocks, 256, 0, s>>>(lo, DL ? delta : nullptr, SG ? lo_out : nullptr, up, B, C, h, w, d, \
+                                                   H, W, D, rh, rw, rd, sh, sw, sd, nx, ny, rows)
+#define DVC_UPFLOW4(DL, SG)                         \
+    do {                                            \
+        if (staged) DVC_UPFLOW(DL, SG, 4, true);    \
+        else DVC_UPFLOW(DL, SG, 4, false);          \
+    } while (0)
+    if (!subgrid) {
+        if (vec == 4) DVC_UPFLOW4(false, false); else DVC_UPFLOW(false, false, 1, false);
+    } else if (delta) {
+        if (vec == 4) DVC_UPFLOW4(true, true); else DVC_UPFLOW(true, true, 1, false);
+    } else {
+        if (vec == 4) DVC_UPFLOW4(false, true); else DVC_UPFLOW(false, true, 1, false);
+    }
+#undef DVC_UPFLOW4
 #undef DVC_UPFLOW
     return check_launch(what);
 }

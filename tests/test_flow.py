@@ -139,3 +139,37 @@ def test_gpu_upflow_extra_channels_and_errors():
         dvccorr.upflow_3d(torch.zeros(1, 2, 4, 4, 4, device=DEV), (8, 8, 8))
     with pytest.raises(ValueError):
         dvccorr.flow_step(torch.zeros(1, 3, 4, 4, 4, device=DEV), torch.zeros(1, 3, 4, 4, 2, device=DEV), (8, 8, 8))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lo,tgt", [
+    ((32, 32, 32), (128, 128, 128)),      # cfg #3 tail: 8 x-rows of 128 per 1024-output chunk
+    ((64, 16, 24), (128, 64, 96)),        # x2 / x4 / x4 per axis
+    ((20, 8, 12), (21, 16, 24)),          # ratio ~0.95 in h
+    ((7, 5, 6), (7, 10, 12)),             # identity in h (ratio 1)
+    ((4, 3, 700), (8, 5, 2048)),          # D > 1024: a chunk is part of one x row (z sub-range staged)
+    ((40, 2, 3000), (44, 3, 4096)),       # rows >= 8: box bound above the LDS tile, the host takes the direct kernel
+    ((6, 6, 6), (6, 6, 4)),               # downsampling in z: direct kernel (staged needs every ratio <= 1)
+])
+@pytest.mark.parametrize("rows", [1, 3, 8, 16])
+def test_gpu_upflow_staged_matches_direct(lo, tgt, rows):
+    """k_upflow's LDS-staged form (dvc_set_tuning "upflow_staged" 1, the default) and the direct
+    per-lane gathers (0) compute the same T values in the same order: bitwise equal outputs."""
+    import dvccorr
+    import prng
+    from dvccorr import _lib
+    h, w, d = lo
+    c1 = torch.from_numpy(prng.flow_coords(730 + h, 1, h, w, d, 3.0)).to(DEV)
+    dl = torch.from_numpy(prng.uniform(731 + w, (1, 3, h, w, d), -1.0, 1.0)).to(DEV)
+    outs = []
+    try:
+        _lib.set_tuning("upflow_rows", rows)
+        for st in (0, 1):
+            _lib.set_tuning("upflow_staged", st)
+            outs.append(dvccorr.flow_step(c1, dl, tgt)[1])
+    finally:
+        _lib.set_tuning("upflow_staged", 1)
+        _lib.set_tuning("upflow_rows", 12)   # the library default
+    assert torch.equal(outs[0], outs[1])
+    if rows == 8:
+        assert orc.rel_err(outs[1].cpu().numpy(), orc.flow_step(c1.cpu().numpy(), dl.cpu().numpy(), tgt)[1]) <= TOL

@@ -1,5 +1,5 @@
 """A/B of k_upflow rows per work item and grid size (dvc_set_tuning "upflow_rows" /
-"upflow_wgs") at the bench's
+"upflow_wgs", "upflow_staged") at the bench's
 iteration-tail shape (coords 32^3 -> flow_up 128^3): HIP-event average over 50 calls."""
 import os
 import sys
@@ -18,8 +18,9 @@ new = torch.empty_like(c1)
 up = torch.empty(1, 3, S * E, S * E, S * E, device=dev)
 st = torch.cuda.current_stream(dev)
 ref = None
-for rows, wgs in ((4, 1 << 30), (8, 1 << 30), (4, 512), (4, 1024), (4, 2048), (8, 512), (8, 1024), (2, 1024),
-                  (16, 1024)):
+for pf, rows, wgs in ((0, 8, 1 << 30), (1, 8, 1 << 30), (1, 8, 2048), (1, 12, 1 << 30), (1, 12, 2048),
+                      (1, 16, 1 << 30), (1, 16, 2048), (1, 16, 1024), (1, 16, 4096), (1, 24, 2048)):
+    _lib.set_tuning("upflow_staged", pf)
     _lib.set_tuning("upflow_rows", rows)
     _lib.set_tuning("upflow_wgs", wgs)
     call = lambda: _lib.check(_lib.lib().dvc_flow_step(c1.data_ptr(), dl.data_ptr(), new.data_ptr(), up.data_ptr(),
@@ -36,5 +37,5 @@ for rows, wgs in ((4, 1 << 30), (8, 1 << 30), (4, 512), (4, 1024), (4, 2048), (8
     if ref is None:
         ref = up.clone()
     same = torch.equal(ref, up)
-    print(f"rows {rows:2d} wgs {min(wgs, 99999):5d}: {ms * 1e3:.1f} us  {up.numel() * 4 * 1.0 / (ms * 1e-3) / 1e9:.0f} GB/s written  same={same}",
+    print(f"staged {pf} rows {rows:2d} wgs {min(wgs, 99999):5d}: {ms * 1e3:.1f} us  {up.numel() * 4 * 1.0 / (ms * 1e-3) / 1e9:.0f} GB/s written  same={same}",
           flush=True)
