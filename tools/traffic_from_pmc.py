@@ -1,0 +1,40 @@
+"""Regenerate profiles/traffic.json (bench.py's roofline "traffic" per launch) from the round's
+rocprofv3 --pmc summaries under profiles/: HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE
+(KB x 1024; the x2 is MI355X_MICROARCH.md's gfx950 streaming-read correction)."""
+import json
+import os
+
+P = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles")
+
+
+def hbm(entry):
+    return (2 * entry["FETCH_SIZE"] + entry["WRITE_SIZE"]) * 1024.0
+
+
+def pick(d, prefix):
+    keys = [k for k in d if isinstance(d[k], dict) and prefix in k]
+    assert len(keys) == 1, (prefix, keys)
+    return d[keys[0]]
+
+
+note = "HBM bytes per launch: 2 x FETCH_SIZE + WRITE_SIZE (KB x 1024), rocprofv3 --pmc, gfx950; source: {}"
+out = {}
+m = json.load(open(os.path.join(P, "r02_pmc_mat32.json")))
+out["materialised_bf16_32_L4_r4_n1"] = {
+    "build_hbm_bytes_per_launch": hbm(pick(m, "k_build_bf16_2b")),
+    "lookup_hbm_bytes_per_launch": hbm(pick(m, "k_lookup_tile")),
+    "note": note.format("profiles/r02_pmc_mat32.json")}
+f = json.load(open(os.path.join(P, "r02_pmc_fused128.json")))
+out["fused_bf16_128_L2_r4_n1"] = {
+    "lookup_hbm_bytes_per_launch": hbm(pick(f, "k_fused_box")),
+    "note": note.format("profiles/r02_pmc_fused128.json")}
+fp = json.load(open(os.path.join(P, "r02_pmc_fused128_convc1.json")))
+out["fused_bf16_128_L2_r4_n1_convc1_fused"] = {
+    "lookup_hbm_bytes_per_launch": sum(hbm(pick(fp, k)) for k in ("k_otf_keys", "k_fused_proj", "k_rows_to_channels")),
+    "note": note.format("profiles/r02_pmc_fused128_convc1.json") + " (k_otf_keys + k_fused_proj + k_rows_to_channels)"}
+old = json.load(open(os.path.join(P, "traffic.json")))
+for k, v in old.items():   # keep round-1 entries no round-2 pass replaced, marked as such
+    if k not in out:
+        out[k] = dict(v, note=v.get("note", "") + " (round 1)")
+json.dump(out, open(os.path.join(P, "traffic.json"), "w"), indent=1)
+print(json.dumps(out, indent=1))
