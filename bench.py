@@ -65,6 +65,11 @@ def parse(argv=None):
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--impl", default="materialised", choices=["materialised", "fused"])
     ap.add_argument("--max-flow", type=float, default=2.0)
+    ap.add_argument("--flow", default="random", choices=["random", "smooth"],
+                    help="synthetic displacement field: random = i.i.d. U(-max_flow, max_flow) per voxel and axis "
+                         "(default; the worst case for the union-of-windows fused kernels), smooth = a sum of "
+                         "three low-frequency sinusoids per axis bounded by max_flow (a deformation field, as "
+                         "RAFT-DVC's upsampled flow estimates are)")
     ap.add_argument("--convc1", nargs="?", const="fused", default=None, choices=["fused", "unfused"],
                     help="each lookup also applies MotionEncoder.convc1 + ReLU: fused into the lookup "
                          "(dvc_corr_lookup_proj) or unfused (lookup, then torch conv3d + relu on the GPU)")
@@ -325,6 +330,23 @@ def timed(runner, steps, warmup, dist, dev, participate=True):
     return elapsed
 
 
+def synthetic_flow(kind, B, S, max_flow, g):
+    """(B, 3, S, S, S) displacement: i.i.d. uniform, or per axis a sum of three sinusoids
+    (max_flow / 3) sin(2 pi k.p / S + phase) with random integer wave vectors k in [0, 2]^3."""
+    if kind == "random":
+        return (torch.rand(B, 3, S, S, S, generator=g) * 2 - 1) * max_flow
+    ax = torch.arange(S, dtype=torch.float32)
+    p = torch.stack(torch.meshgrid(ax, ax, ax, indexing="ij"))           # (3, S, S, S)
+    out = torch.zeros(B, 3, S, S, S)
+    for bb in range(B):
+        for c in range(3):
+            for _ in range(3):
+                k = torch.randint(0, 3, (3,), generator=g).float()
+                ph = float(torch.rand((), generator=g)) * 2 * torch.pi
+                out[bb, c] += (max_flow / 3) * torch.sin(2 * torch.pi * (k[:, None, None, None] * p).sum(0) / S + ph)
+    return out
+
+
 def gpu_inputs(S, C, iters, max_flow, seed, dev):
     """Seeded inputs generated on the GPU (identical on every rank of one node)."""
     g = torch.Generator(device=dev).manual_seed(seed)
@@ -373,8 +395,7 @@ def main():
     f1 = torch.randn(B, C, S, S, S, generator=g)
     f2 = torch.randn(B, C, S, S, S, generator=g)
     base = dvccorr.coords_grid_3d(B, S, S, S, torch.device("cpu"))
-    coords_list = [base + (torch.rand(B, 3, S, S, S, generator=g) * 2 - 1) * args.max_flow
-                   for _ in range(args.iters)]
+    coords_list = [base + synthetic_flow(args.flow, B, S, args.max_flow, g) for _ in range(args.iters)]
     if shard_diag:
         h0, h1 = slab_bounds(S, args.shard_of, args.shard_rank)
     else:
@@ -431,7 +452,7 @@ def main():
         bd_bytes = (nq_local + n_targets) * C * 4 + (nq_local + unpadded) * C * store_bytes
         bd_flops = 0.0
     traffic = None
-    if os.path.exists(args.traffic_file):
+    if os.path.exists(args.traffic_file) and not shard_diag and args.flow == "random":   # PMC passes are per workload
         try:
             tf = json.load(open(args.traffic_file))
             key = f"{args.impl}_{args.precision}_{S}_L{L}_r{R}_n{world if strong else 1}" + \
@@ -504,7 +525,10 @@ def main():
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
             "scaling": "strong" if strong else "weak", "vs_baseline": None,
             "dtype": "bf16" if args.precision == "bf16" else "f32",
-            "data": "synthetic: N(0,1) feature maps, coords = identity + U(-2,2), 12 coord fields per step",
+            "data": (f"synthetic: N(0,1) feature maps, coords = identity + "
+                     + (f"U(-{args.max_flow:g},{args.max_flow:g}) i.i.d. per voxel" if args.flow == "random" else
+                        f"a smooth field (3 sinusoids per axis, |flow| <= {args.max_flow:g})")
+                     + f", {args.iters} coord fields per step"),
             "config": {"workload": f"corr build + {args.iters} lookups{f' + convc1 ({args.convc1})' if args.convc1 else ''}, {S}^3 x {C} fmaps ({args.encoder * S}^3 "
                                    f"input, 1/{args.encoder} encoder), L={L}, r={R}, {args.impl}, {args.precision} build / fp32 lookup",
                        "global_batch": B if strong else B * world, "query_voxels": nq_total, "levels": L,

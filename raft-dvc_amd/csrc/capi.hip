@@ -24,7 +24,7 @@ struct PyrGeo {
     long long row_stride;
     int ncx, ncy, ncz;
 };
-template <typename T> __global__ void k_pack_pyramid(const float *, T *, PyrGeo);
+template <typename T, int CG> __global__ void k_pack_pyramid(const float *, T *, PyrGeo);
 template <typename T> __global__ void k_pack_queries(const float *, T *, int, int, long long);
 template <int NCH, bool STORE_F32, int ABL>
 __global__ void k_build_bf16(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long, long long, long long,
@@ -381,9 +381,16 @@ int dvc_pack_targets(const float *fmap2, void *packed, float *workspace, int B, 
             g.H[l] = lay.H[l]; g.W[l] = lay.W[l]; g.D[l] = lay.D[l]; g.Dp[l] = lay.Dp[l]; g.off[l] = lay.offset[l];
         }
         g.ncy = (H + 7) / 8; g.ncx = (W + 7) / 8; g.ncz = (D + 7) / 8;
-        dim3 grid((unsigned)(g.ncy * g.ncx * g.ncz), (unsigned)ceil_div(Cp, 16), (unsigned)B);
-        if (dtype == DVC_BF16) k_pack_pyramid<bf16_t><<<grid, 256, 0, s>>>(fmap2, (bf16_t *)packed, g);
-        else k_pack_pyramid<float><<<grid, 256, 0, s>>>(fmap2, (float *)packed, g);
+        const long long ncells = (long long)g.ncy * g.ncx * g.ncz;
+        const bool cg32 = ncells * ceil_div(Cp, 32) * B >= 2048;   // 32 channels per workgroup on big volumes
+        dim3 grid((unsigned)(8 * ceil_div(ncells, 8)), (unsigned)ceil_div(Cp, cg32 ? 32 : 16), (unsigned)B);
+        if (dtype == DVC_BF16) {
+            if (cg32) k_pack_pyramid<bf16_t, 32><<<grid, 256, 0, s>>>(fmap2, (bf16_t *)packed, g);
+            else k_pack_pyramid<bf16_t, 16><<<grid, 256, 0, s>>>(fmap2, (bf16_t *)packed, g);
+        } else {
+            if (cg32) k_pack_pyramid<float, 32><<<grid, 256, 0, s>>>(fmap2, (float *)packed, g);
+            else k_pack_pyramid<float, 16><<<grid, 256, 0, s>>>(fmap2, (float *)packed, g);
+        }
         return check_launch("pack_targets");
     }
     if (hipMemsetAsync(packed, 0, (size_t)B * lay.row_stride * Cp * esz, s) != hipSuccess)

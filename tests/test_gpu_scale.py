@@ -277,10 +277,11 @@ def test_fp32_block_convc1_is_exact():
 
 @pytest.mark.parametrize("shape,C,L", [((9, 7, 8), 16, 3), ((16, 16, 16), 128, 4), ((33, 20, 17), 40, 4),
                                        ((8, 8, 2), 64, 2), ((5, 6, 7), 32, 1), ((32, 32, 32), 128, 4),
-                                       ((24, 18, 40), 256, 4)])
+                                       ((24, 18, 40), 256, 4), ((64, 64, 64), 128, 4), ((96, 64, 37), 160, 3)])
 def test_single_pass_pack_matches_per_level(shape, C, L):
     """k_pack_pyramid (fmap2 -> every packed target level in one pass, pooled in LDS) writes exactly the
-    bytes of the per-level pool + pack launches (same (dy, dx, dz) summation order), both dtypes."""
+    bytes of the per-level pool + pack launches (same (dy, dx, dz) summation order), both dtypes.  The last
+    two shapes have >= 2048 (cell, 32-channel group) pairs: the 32-channel instance."""
     from dvccorr import _lib, ops
     H, W, D = shape
     g = torch.Generator(device="cpu").manual_seed(H + W + D + C + L)
