@@ -38,7 +38,7 @@ template <typename T>
 __global__ void k_corr_pool(T *, long long, long long, long long, int, int, long long, int, int, int, int);
 template <typename T, int R, bool WINBUF, bool ALIGNED> __global__ void k_lookup_win(LookupArgs);
 template <typename T> __global__ void k_lookup_generic(LookupArgs);
-template <typename T, int R, bool NT, int ABL, bool PROJ, int ACH> __global__ void k_lookup_tile(LookupArgs);
+template <typename T, int R, bool NT, int ABL, bool PROJ, int ACH, int NWV = 0> __global__ void k_lookup_tile(LookupArgs);
 __global__ void k_proj_pack(const float *, bf16_t *, int, int, int, long long);
 __global__ void k_sample3d(const float *, const float *, float *, int, int, int, int, int, long long, int);
 int fused_lookup(const void *packed_q, const void *packed_t, const float *coords, float *out, void *workspace, int B,
@@ -150,6 +150,11 @@ static bool tile_ok(const LookupArgs &A, size_t esz) {
 // split 39.1, ACH 5 41.2, ACH 3 43.6.
 static constexpr long long kSplitTiles = 512, kSplitRows = 512;
 static thread_local int g_split_ach = 5;          // rows per chunk of the row split (0 = no row split; 2, 3, 5)
+// r = 4 tile kernel: 4 = four waves of 3 + 2 + 2 + 2 output columns (default: two workgroups put two waves
+// on every SIMD), 0 = three 3-column waves.  Round 2 A/B (tools/ab_waves.py, bitwise-equal outputs, median
+// of 40 calls): config #3 bf16 151.8 -> 150.0 us, fp32 220.7 -> 213.9; one rank's slab of an 8 / 4 / 2-way
+// split 26.7 / 39.0 / 78.2 -> 26.2 / 38.9 / 77.4 us (bf16).
+static thread_local int g_lookup_waves = 4;
 
 template <typename T, bool NT, int ACH>
 static void launch_tile_r(const LookupArgs &A, dim3 blocks, unsigned threads, hipStream_t s) {
@@ -174,17 +179,23 @@ static void launch_tile_nt(const LookupArgs &A0, hipStream_t s) {
     const bool split_rows = NT && A.split_levels && tiles * A.nl < kSplitRows && n > ach && ach > 0;
     const dim3 blocks((unsigned)tiles, A.split_levels ? (unsigned)A.nl : 1u,
                       split_rows ? (unsigned)((n + ach - 1) / ach) : 1u);
-    const unsigned threads = 64u * (unsigned)((2 * A.r + 3) / 3);
+    const bool bal = NT && A.r == 4 && g_lookup_waves == 4 && (ach == 5 || !split_rows);
+    const unsigned threads = 64u * (bal ? 4u : (unsigned)((2 * A.r + 3) / 3));
     if constexpr (std::is_same<T, bf16_t>::value && NT) {
         if (A.r == 4 && A.ablate >= 1 && A.ablate <= 3) {   // diagnostics only
             const dim3 b1((unsigned)tiles, blocks.y);
-            if (A.ablate == 1) k_lookup_tile<T, 4, NT, 1, false, 0><<<b1, threads, 0, s>>>(A);
-            else if (A.ablate == 2) k_lookup_tile<T, 4, NT, 2, false, 0><<<b1, threads, 0, s>>>(A);
-            else k_lookup_tile<T, 4, NT, 3, false, 0><<<b1, threads, 0, s>>>(A);
+            if (A.ablate == 1) k_lookup_tile<T, 4, NT, 1, false, 0><<<b1, 192, 0, s>>>(A);
+            else if (A.ablate == 2) k_lookup_tile<T, 4, NT, 2, false, 0><<<b1, 192, 0, s>>>(A);
+            else k_lookup_tile<T, 4, NT, 3, false, 0><<<b1, 192, 0, s>>>(A);
             return;
         }
     }
     if constexpr (NT) {
+        if (bal) {
+            if (split_rows) k_lookup_tile<T, 4, true, 0, false, 5, 4><<<blocks, threads, 0, s>>>(A);
+            else k_lookup_tile<T, 4, true, 0, false, 0, 4><<<blocks, threads, 0, s>>>(A);
+            return;
+        }
         if (split_rows) {
             if (ach == 2) launch_tile_r<T, NT, 2>(A, blocks, threads, s);
             else if (ach == 5) launch_tile_r<T, NT, 5>(A, blocks, threads, s);
@@ -243,6 +254,11 @@ int dvc_set_tuning(const char *key, int value) {
     if (!strcmp(key, "lookup_ldpol")) {
         if (value < 0 || value > 3) return fail(DVC_ERR_INVALID, "set_tuning: lookup_ldpol %d", value);
         g_lookup_ldpol = value;
+        return DVC_OK;
+    }
+    if (!strcmp(key, "lookup_waves")) {
+        if (value != 0 && value != 4) return fail(DVC_ERR_INVALID, "set_tuning: lookup_waves %d (0 or 4)", value);
+        g_lookup_waves = value;
         return DVC_OK;
     }
     if (!strcmp(key, "split_ach")) {

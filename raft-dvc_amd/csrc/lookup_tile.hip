@@ -33,14 +33,17 @@
 
 namespace dvc {
 
-template <typename T, int R> struct TileCfg {
+// NWV = 0: ceil(n / 3) waves of 3 output columns (the last one takes the rest); NWV > 0: NWV waves
+// with the columns dealt as evenly as possible (n = 9, NWV = 4: 3 + 2 + 2 + 2), so that two workgroups
+// put exactly two waves on each SIMD.
+template <typename T, int R, int NWV = 0> struct TileCfg {
     static constexpr int n = 2 * R + 1;
     static constexpr int NW = 2 * R + 2;                        // window planes / columns / run length
     static constexpr int ES = (int)sizeof(T);
     static constexpr int CE = 16 / ES;                          // elements per 16-byte chunk
     static constexpr int ZWMAX = (NW + CE - 1 + CE - 1) / CE * CE;   // z-chunk span covering any run
-    static constexpr int COLS = 3;                              // output columns per wave
-    static constexpr int NWAVES = (n + COLS - 1) / COLS;
+    static constexpr int NWAVES = NWV > 0 ? NWV : (n + 2) / 3;
+    static constexpr int COLS = NWV > 0 ? (n + NWV - 1) / NWV : 3;   // output columns of the widest wave
     static constexpr int THREADS = 64 * NWAVES;
     static constexpr int SQMAX = NW * ZWMAX * ES + 8;           // bytes per query strip (+8: bank spread)
     static constexpr int SLOT = 64 * SQMAX;
@@ -112,9 +115,12 @@ struct ProjCfg {
 // ABL (diagnostics only, never the product path): 1 = skip output stores, 2 = skip loads.
 // ACH > 0: row split -- the workgroup computes output rows [ACH * blockIdx.z, + ACH) of its level only
 // (ACH + 1 window planes), for launches whose (tile, level) pairs alone cannot fill the chip.
-template <typename T, int R, bool NT, int ABL, bool PROJ, int ACH>
-__global__ __launch_bounds__(64 * ((2 * R + 3) / 3 + (PROJ ? 1 : 0)), 2) void k_lookup_tile(LookupArgs A) {
-    using C = TileCfg<T, R>;
+template <typename T, int R, bool NT, int ABL, bool PROJ, int ACH, int NWV = 0>
+__global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)), 2) void k_lookup_tile(LookupArgs A) {
+    using C = TileCfg<T, R, NWV>;
+    static_assert(!PROJ || NWV == 0, "the convc1 weight packing assumes the 3-column waves");
+    constexpr bool BAL = NWV > 0;
+    constexpr int FLO = BAL ? C::n / C::NWAVES : 0, REM = BAL ? C::n % C::NWAVES : 0;
     constexpr int n = C::n, NW = C::NW, ES = C::ES, CE = C::CE, NP = n / 2;
     constexpr long long n3 = (long long)n * n * n;
     constexpr int NU_LAST = n - C::COLS * (C::NWAVES - 1);   // output columns of the last wave
@@ -138,7 +144,7 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3 + (PROJ ? 1 : 0)), 2) void k_
 
     if constexpr (PROJ) {
         if (wave == C::NWAVES) {   // the convc1 consumer wave
-            constexpr int OT = ProjCfg::OT, NWV = C::NWAVES;
+            constexpr int OT = ProjCfg::OT, NWP = C::NWAVES;
             const int m16 = lane & 15, h4 = lane >> 4;
             f32x4 acc[OT][4];   // acc[ot][j][i] = D[o = 16 ot + 4 h4 + i][query 16 j + m16]
 #pragma unroll
@@ -155,16 +161,16 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3 + (PROJ ? 1 : 0)), 2) void k_
                 __syncthreads();   // planes 0 and 1 staged
                 for (int a = 0; a < n; ++a) {
                     // this row's weight block, [wave slice ks][16-channel tile ot][lane] x 8 fp16
-                    const f16x8 *wr = wp + (long long)(l * n + a) * NWV * OT * 64;
-                    f16x8 wa[NWV][OT];
+                    const f16x8 *wr = wp + (long long)(l * n + a) * NWP * OT * 64;
+                    f16x8 wa[NWP][OT];
 #pragma unroll
-                    for (int ks = 0; ks < NWV; ++ks)
+                    for (int ks = 0; ks < NWP; ++ks)
 #pragma unroll
                         for (int ot = 0; ot < OT; ++ot) wa[ks][ot] = wr[(ks * OT + ot) * 64];
                     __syncthreads();   // the producers may overwrite X: row a-1 has been read
                     __syncthreads();   // row a complete in X
 #pragma unroll
-                    for (int ks = 0; ks < NWV; ++ks) {
+                    for (int ks = 0; ks < NWP; ++ks) {
                         f16x8 xb[4];
 #pragma unroll
                         for (int j = 0; j < 4; ++j)
@@ -216,7 +222,7 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3 + (PROJ ? 1 : 0)), 2) void k_
     const int q4 = active ? (int)(q * 4) : 0x7ffffff0;
     const int chstep_u = A.legacy ? 1 : n;       // output-channel step per U (W-axis) offset
     const int chstep_v = A.legacy ? n : 1;       // ... per V (D-axis) offset
-    const int u0 = wave * C::COLS;               // this wave's output columns u0 .. u0 + NU - 1
+    const int u0 = BAL ? wave * FLO + min(wave, REM) : wave * C::COLS;   // this wave's columns u0 .. u0 + NU - 1
     const int ldpol = A.ldpol;
 
     // store of output (row a, column u, offset v) of this lane's query
@@ -459,8 +465,14 @@ __global__ __launch_bounds__(64 * ((2 * R + 3) / 3 + (PROJ ? 1 : 0)), 2) void k_
     for (int li = li0; li < li1; ++li) {
         const int l = A.l0 + (rev ? A.nl - 1 - li : li);
         if (A.generic[l] && !A.zero[l]) continue;   // legacy level with W != D: k_lookup_generic
-        if (NU_LAST == C::COLS || wave < C::NWAVES - 1) rows(l, std::integral_constant<int, C::COLS>{});
-        else rows(l, std::integral_constant<int, NU_LAST>{});
+        if constexpr (BAL) {
+            if (REM > 0 && wave < REM) rows(l, std::integral_constant<int, FLO + 1>{});
+            else rows(l, std::integral_constant<int, FLO>{});
+        } else if (NU_LAST == C::COLS || wave < C::NWAVES - 1) {
+            rows(l, std::integral_constant<int, C::COLS>{});
+        } else {
+            rows(l, std::integral_constant<int, NU_LAST>{});
+        }
     }
 }
 
@@ -474,6 +486,11 @@ DVC_TILE_INST(float, 1) DVC_TILE_INST(float, 2) DVC_TILE_INST(float, 3)
 DVC_TILE_INST(float, 4) DVC_TILE_INST(float, 5) DVC_TILE_INST(float, 6)
 DVC_TILE_INST(bf16_t, 1) DVC_TILE_INST(bf16_t, 2) DVC_TILE_INST(bf16_t, 3)
 DVC_TILE_INST(bf16_t, 4) DVC_TILE_INST(bf16_t, 5) DVC_TILE_INST(bf16_t, 6)
+// balanced four-wave instances (tuning "lookup_waves" = 4)
+template __global__ void k_lookup_tile<float, 4, true, 0, false, 0, 4>(LookupArgs);
+template __global__ void k_lookup_tile<bf16_t, 4, true, 0, false, 0, 4>(LookupArgs);
+template __global__ void k_lookup_tile<float, 4, true, 0, false, 5, 4>(LookupArgs);
+template __global__ void k_lookup_tile<bf16_t, 4, true, 0, false, 5, 4>(LookupArgs);
 template __global__ void k_lookup_tile<bf16_t, 4, true, 1, false, 0>(LookupArgs);
 template __global__ void k_lookup_tile<bf16_t, 4, true, 2, false, 0>(LookupArgs);
 template __global__ void k_lookup_tile<bf16_t, 4, true, 3, false, 0>(LookupArgs);

@@ -259,7 +259,7 @@ def test_lookup_variants(variant):
 
 @pytest.mark.parametrize("shape,L,r", [((9, 7, 5), 2, 1), ((12, 10, 16), 3, 2), ((16, 16, 16), 4, 3),
                                        ((20, 13, 24), 3, 4), ((32, 32, 32), 4, 4), ((24, 26, 28), 2, 5),
-                                       ((30, 28, 40), 2, 6), ((40, 36, 33), 3, 4)])
+                                       ((30, 28, 40), 2, 6), ((40, 36, 33), 3, 4), ((16, 12, 20), 4, 4)])
 def test_tile_kernel_matches_walk(shape, L, r):
     """The LDS-staged tile kernel (variant 2) is bit-identical to the lane-per-query walk (variant 0):
     same per-axis weights, same separable summation order.  Ragged tiles (Nq % 64 != 0), non-cubic and
@@ -285,12 +285,19 @@ def test_tile_kernel_matches_walk(shape, L, r):
                 for v in (0, 2):
                     _lib.set_tuning("lookup_variant", v)
                     outs.append(blk(c))
+                if r == 4:   # three 3-column waves (lookup_waves 0) vs the default four balanced waves
+                    _lib.set_tuning("lookup_waves", 0)
+                    outs.append(blk(c))
+                    _lib.set_tuning("lookup_waves", 4)
                 torch.cuda.synchronize()
+                for o in outs[2:]:
+                    assert torch.equal(outs[0], o), (shape, L, r, prec, legacy, "lookup_waves 0")
                 assert torch.isfinite(outs[1]).all(), (prec, legacy)
                 assert torch.equal(outs[0], outs[1]), (shape, L, r, prec, legacy,
                                                         float((outs[0] - outs[1]).abs().max()))
     finally:
         _lib.set_tuning("lookup_variant", 2)
+        _lib.set_tuning("lookup_waves", 4)
 
 
 @pytest.mark.parametrize("shape,C,L,r", [((9, 7, 5), 32, 2, 1), ((12, 10, 16), 64, 3, 2), ((16, 16, 16), 32, 4, 3),

@@ -20,6 +20,8 @@ ap.add_argument("--variant", type=int, default=0)
 ap.add_argument("--impl", default="materialised")
 ap.add_argument("--tune", default="", help="comma list key=value of dvc_set_tuning knobs")
 ap.add_argument("--convc1", action="store_true", help="lookup_convc1 (convc1 fused) instead of the lookup")
+ap.add_argument("--build", default="gemm", choices=["gemm", "pool"],
+                help="materialised pyramid: GEMM against pooled targets (default) or level-0 GEMM + k_corr_pool")
 a = ap.parse_args()
 _lib.set_tuning("lookup_variant", a.variant)
 for kv in filter(None, a.tune.split(",")):
@@ -33,7 +35,8 @@ f2 = torch.randn(1, 128, S, S, S, generator=g).to(dev)
 c = (dvccorr.coords_grid_3d(1, S, S, S, torch.device("cpu")) + (torch.rand(1, 3, S, S, S, generator=g) * 4 - 2)).to(dev)
 with torch.no_grad():
     cls = dvccorr.CorrBlock if a.impl == "materialised" else dvccorr.CorrBlockFused
-    blk = cls(f1, f2, a.levels, 4, precision=a.precision)
+    kw = {"build": a.build} if a.impl == "materialised" else {}
+    blk = cls(f1, f2, a.levels, 4, precision=a.precision, **kw)
     K = a.levels * 729
     w = ((torch.rand(96, K, generator=g) * 2 - 1) / K ** 0.5).to(dev)
     bias = ((torch.rand(96, generator=g) * 2 - 1) / K ** 0.5).to(dev)
