@@ -182,9 +182,10 @@ static void launch_tile_nt(const LookupArgs &A0, hipStream_t s) {
     const bool bal = NT && A.r == 4 && g_lookup_waves == 4 && (ach == 5 || !split_rows);
     const unsigned threads = 64u * (bal ? 4u : (unsigned)((2 * A.r + 3) / 3));
     if constexpr (std::is_same<T, bf16_t>::value && NT) {
-        if (A.r == 4 && A.ablate >= 1 && A.ablate <= 3) {   // diagnostics only
+        if (A.r == 4 && A.ablate >= 1 && A.ablate <= 4) {   // diagnostics only
             const dim3 b1((unsigned)tiles, blocks.y);
-            if (A.ablate == 1) k_lookup_tile<T, 4, NT, 1, false, 0><<<b1, 192, 0, s>>>(A);
+            if (A.ablate == 4) k_lookup_tile<T, 4, NT, 4, false, 0><<<b1, 192, 0, s>>>(A);
+            else if (A.ablate == 1) k_lookup_tile<T, 4, NT, 1, false, 0><<<b1, 192, 0, s>>>(A);
             else if (A.ablate == 2) k_lookup_tile<T, 4, NT, 2, false, 0><<<b1, 192, 0, s>>>(A);
             else k_lookup_tile<T, 4, NT, 3, false, 0><<<b1, 192, 0, s>>>(A);
             return;

@@ -112,7 +112,9 @@ struct ProjCfg {
     static constexpr int COUT = 96, OT = COUT / 16, KW = 32;
 };
 
-// ABL (diagnostics only, never the product path): 1 = skip output stores, 2 = skip loads.
+// ABL (diagnostics only, never the product path): 1 = skip output stores, 2 = skip loads, 4 = the same
+// output bytes as 16-byte stores (a column's 9 values leave as 2 x dwordx4 + 1 dword per lane, at
+// query-major addresses -- wrong layout, a third of the store instructions).
 // ACH > 0: row split -- the workgroup computes output rows [ACH * blockIdx.z, + ACH) of its level only
 // (ACH + 1 window planes), for launches whose (tile, level) pairs alone cannot fill the chip.
 template <typename T, int R, bool NT, int ABL, bool PROJ, int ACH, int NWV = 0>
@@ -404,6 +406,7 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
                     const float p01 = wx0[uu] * wy1, p11 = wx1[uu] * wy1;
                     const f32x2 P00 = {p00, p00}, P10 = {p10, p10}, P01 = {p01, p01}, P11 = {p11, p11};
                     const __amdgpu_buffer_rsrc_t rs = out_rsrc(obase, a, u0 + uu);
+                    [[maybe_unused]] float wide[2 * NP + 1];
 #pragma unroll
                     for (int i = 0; i < NP; ++i) {
                         f32x2 acc = P00 * zp[uu].p[i];
@@ -412,6 +415,9 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
                         acc = __builtin_elementwise_fma(P11, zcur.p[i], acc);
                         if constexpr (PROJ) {
                             xr[uu * NP + i] = __builtin_bit_cast(unsigned, __builtin_convertvector(acc, f16x2));
+                        } else if constexpr ((ABL & 4) != 0) {
+                            wide[2 * i] = acc[0];
+                            wide[2 * i + 1] = acc[1];
                         } else {
                             store(rs, 2 * i, acc[0]);
                             store(rs, 2 * i + 1, acc[1]);
@@ -421,8 +427,20 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
                     acc = __builtin_fmaf(p10, zp[uu + 1].t, acc);
                     acc = __builtin_fmaf(p01, zprev.t, acc);
                     acc = __builtin_fmaf(p11, zcur.t, acc);
-                    if constexpr (PROJ) xt[uu] = acc;
-                    else store(rs, n - 1, acc);
+                    if constexpr (PROJ) {
+                        xt[uu] = acc;
+                    } else if constexpr ((ABL & 4) != 0) {   // diagnostics: same bytes, 16-byte stores
+                        wide[n - 1] = acc;
+#pragma unroll
+                        for (int g4 = 0; g4 + 4 <= n - 1; g4 += 4)
+                            __builtin_amdgcn_raw_buffer_store_b128(
+                                u32x4{__float_as_uint(wide[g4]), __float_as_uint(wide[g4 + 1]),
+                                      __float_as_uint(wide[g4 + 2]), __float_as_uint(wide[g4 + 3])},
+                                rs, q4 * 4, (int)(g4 * Nq * 4), 2);
+                        store(rs, n - 1, acc);
+                    } else {
+                        store(rs, n - 1, acc);
+                    }
                     zp[uu] = zprev;
                 }
                 zprev = zcur;
@@ -492,6 +510,7 @@ template __global__ void k_lookup_tile<bf16_t, 4, true, 0, false, 0, 4>(LookupAr
 template __global__ void k_lookup_tile<float, 4, true, 0, false, 5, 4>(LookupArgs);
 template __global__ void k_lookup_tile<bf16_t, 4, true, 0, false, 5, 4>(LookupArgs);
 template __global__ void k_lookup_tile<bf16_t, 4, true, 1, false, 0>(LookupArgs);
+template __global__ void k_lookup_tile<bf16_t, 4, true, 4, false, 0>(LookupArgs);
 template __global__ void k_lookup_tile<bf16_t, 4, true, 2, false, 0>(LookupArgs);
 template __global__ void k_lookup_tile<bf16_t, 4, true, 3, false, 0>(LookupArgs);
 // convc1-fused instances (radii whose (2r+1) x 3 row values fit one 32-k slice)
