@@ -58,3 +58,19 @@ def test_lookup_algorithmic_bytes_brute_force():
             win += n
     n3 = (2 * r + 1) ** 3
     assert got == pytest.approx(win * 2 + H * W * D * (4 * 2 * n3 + 12))
+
+
+@pytest.mark.parametrize("kind", ["random", "smooth"])
+def test_synthetic_flow_bounded_and_seeded(kind):
+    """--flow random (the default: i.i.d. per voxel and axis) and --flow smooth (three sinusoids per axis) stay
+    within +-max_flow and are reproducible from the generator seed; the smooth field varies slowly."""
+    g1, g2 = torch.Generator().manual_seed(11), torch.Generator().manual_seed(11)
+    a = bench.synthetic_flow(kind, 2, 16, 2.0, g1)
+    b = bench.synthetic_flow(kind, 2, 16, 2.0, g2)
+    assert a.shape == (2, 3, 16, 16, 16) and torch.equal(a, b)
+    assert float(a.abs().max()) <= 2.0 + 1e-6
+    step = max(float((a.diff(dim=d)).abs().max()) for d in (2, 3, 4))
+    if kind == "smooth":
+        assert step < 2.0 * 2 * torch.pi * 2 / 16   # |d/dp| <= 3 * (2/3) * 2 pi |k| / S per voxel
+    else:
+        assert step > 2.0                           # i.i.d.: neighbours differ by up to 4
