@@ -40,6 +40,8 @@
  *   corr pyramid   [B][Nq][row_stride]    store dtype; row q holds every level of query q:
  *                  level l voxel (y,x,z) at offset[l] + (y*W_l + x)*Dp_l + z, Dp_l = ceil8(D_l),
  *                  padding columns are 0; DVC_CORR_GUARD_BYTES of zeros before and after.
+ *                  With DVC_BRICKED (below) the bricked levels hold the same values in
+ *                  (1, 8, 8) bricks: offset[l] + ((y*W_l/8 + x/8)*Dp_l/8 + z/8)*64 + (x%8)*8 + z%8.
  * Nq is the number of query voxels per batch element; Nq == H*W*D for the
  * reference CorrBlock, Nq < H*W*D for one rank's query slab (sharded path).
  */
@@ -72,6 +74,17 @@ typedef enum {
 
 typedef enum { DVC_F32 = 0, DVC_BF16 = 1 } dvc_dtype;
 
+/* Layout flag ORed into the dtype of dvc_pack_targets and the store_dtype of dvc_corr_lookup /
+ * dvc_corr_lookup_proj (dvc_corr_build is layout-blind: it writes the columns in packed-target
+ * order, so bricked targets give a bricked pyramid).  The levels dvc_bricked_levels() names
+ * (Dp_l >= 32 and W_l % 8 == 0: a z-row of at least 64 bytes) are stored in (1, 8, 8) bricks of
+ * one 128-byte line (bf16), so a lookup window's plane strip touches lines of 8 columns x 8 z
+ * instead of 2 columns x 32 z -- fewer HBM lines per query (the lookup is bound by its bytes).
+ * Only the tile lookup kernels read it: radius 1..6, no legacy W != D bricked level, and
+ * num_levels <= 4 for the pack; other uses return DVC_ERR_UNSUPPORTED (dvc_corr_pool, the
+ * on-the-fly and backward paths and dvc_corr_build take the plain dtype). */
+#define DVC_BRICKED 0x100
+
 /* corr_sampler_version 2 = fixed, 1 = legacy W<->D swap (raft_dvc.py:71-77, corr.py:49-52). */
 typedef enum { DVC_FIXED = 0, DVC_LEGACY = 1 } dvc_convention;
 
@@ -93,6 +106,9 @@ typedef struct {
 /* Pure host function (no GPU).  Fails (DVC_ERR_INVALID) exactly where the
  * reference constructor raises: pooling an axis of size < 2. */
 int dvc_layout_init(int H, int W, int D, int num_levels, int C, dvc_layout *out);
+
+/* Bit mask of the levels DVC_BRICKED stores in bricks (pure host function). */
+int dvc_bricked_levels(const dvc_layout *lay);
 
 /* Bytes of float32 workspace dvc_pack_targets needs (pooled fmap2 levels 1..L-1; 0 for
  * num_levels <= 4, whose levels are pooled in LDS by one single-pass kernel). */

@@ -23,6 +23,7 @@ struct PyrGeo {
     long long off[4];
     long long row_stride;
     int ncx, ncy, ncz;
+    int brick;   // bit l: level l in (1, 8, 8) bricks (DVC_BRICKED)
 };
 template <typename T, int CG> __global__ void k_pack_pyramid(const float *, T *, PyrGeo);
 template <typename T> __global__ void k_pack_queries(const float *, T *, int, int, long long);
@@ -83,7 +84,8 @@ static thread_local int g_upflow_wgs = 1 << 30;   // k_upflow grid cap (workgrou
                                                   // workgroup per item, 178 -> 152 us at the #5 tail (tools/ab_upflow.py)
 static thread_local int g_upflow_staged = 1;      // 1 = k_upflow stages an item's low-res box in LDS (all ratios <= 1)
 static thread_local int g_pack_variant = 1;       // 1 = single-pass k_pack_pyramid where L <= 4, 0 = per-level launches
-static thread_local int g_fused_ablate = 0;       // diagnostics only: 1 = skip output stores, 2 = skip window dots (cube kernel)
+static thread_local int g_fused_ablate = 0;
+       // diagnostics only: 1 = skip output stores, 2 = skip window dots (cube kernel)
 
 static int fail(int code, const char *fmt, ...) {
     va_list ap;
@@ -121,6 +123,7 @@ static int fill_lookup_args(LookupArgs &A, const dvc_layout &lay, const void *co
     A.ldpol = g_lookup_ldpol;
     A.proj_w = nullptr; A.proj_b = nullptr; A.proj_out = nullptr;
     A.split_levels = 0;
+    A.brick = 0;
     return DVC_OK;
 }
 
@@ -352,6 +355,14 @@ int dvc_layout_init(int H, int W, int D, int num_levels, int C, dvc_layout *out)
     return DVC_OK;
 }
 
+int dvc_bricked_levels(const dvc_layout *lay) {
+    int m = 0;
+    if (!lay) return 0;
+    for (int l = 0; l < lay->num_levels && l < 4; ++l)
+        if (!lay->zero_level[l] && lay->Dp[l] >= 32 && lay->W[l] % 8 == 0) m |= 1 << l;
+    return m;
+}
+
 size_t dvc_pack_workspace_bytes(int B, int C, int H, int W, int D, int num_levels) {
     dvc_layout lay;
     if (dvc_layout_init(H, W, D, num_levels, C, &lay)) return 0;
@@ -382,6 +393,10 @@ int dvc_pack_targets(const float *fmap2, void *packed, float *workspace, int B, 
     dvc_layout lay;
     int rc = dvc_layout_init(H, W, D, num_levels, C, &lay);
     if (rc) return rc;
+    const bool bricked = (dtype & DVC_BRICKED) != 0;
+    dtype &= ~DVC_BRICKED;
+    if (bricked && (num_levels > 4 || g_pack_variant != 1))
+        return fail(DVC_ERR_UNSUPPORTED, "pack_targets: DVC_BRICKED needs the single-pass pack (num_levels <= 4)");
     if (!fmap2 || !packed || (dvc_pack_workspace_bytes(B, C, H, W, D, num_levels) > 0 && !workspace))
         return fail(DVC_ERR_INVALID, "pack_targets: null pointer");
     if (B < 1) return fail(DVC_ERR_INVALID, "pack_targets: B=%d", B);
@@ -398,6 +413,7 @@ int dvc_pack_targets(const float *fmap2, void *packed, float *workspace, int B, 
             g.H[l] = lay.H[l]; g.W[l] = lay.W[l]; g.D[l] = lay.D[l]; g.Dp[l] = lay.Dp[l]; g.off[l] = lay.offset[l];
         }
         g.ncy = (H + 7) / 8; g.ncx = (W + 7) / 8; g.ncz = (D + 7) / 8;
+        g.brick = bricked ? dvc_bricked_levels(&lay) : 0;
         const long long ncells = (long long)g.ncy * g.ncx * g.ncz;
         const bool cg32 = ncells * ceil_div(Cp, 32) * B >= 2048;   // 32 channels per workgroup on big volumes
         dim3 grid((unsigned)(8 * ceil_div(ncells, 8)), (unsigned)ceil_div(Cp, cg32 ? 32 : 16), (unsigned)B);
@@ -562,9 +578,19 @@ int dvc_corr_lookup(const void *corr, const float *coords, float *out, int B, in
         return fail(DVC_ERR_UNSUPPORTED, "lookup: Nq=%lld too large for 32-bit output offsets", (long long)Nq);
     if (convention != DVC_FIXED && convention != DVC_LEGACY)
         return fail(DVC_ERR_INVALID, "lookup: bad convention %d", convention);
+    const bool bricked = (store_dtype & DVC_BRICKED) != 0;
+    store_dtype &= ~DVC_BRICKED;
     LookupArgs A;
     fill_lookup_args(A, lay, corr, coords, out, B, Nq, radius, convention);
     if (store_dtype != DVC_BF16 && store_dtype != DVC_F32) return fail(DVC_ERR_INVALID, "lookup: bad dtype %d", store_dtype);
+    if (bricked) {   // only the tile kernel reads bricked levels
+        A.brick = dvc_bricked_levels(&lay);
+        bool generic_brick = false;
+        for (int l = 0; l < lay.num_levels; ++l) generic_brick |= ((A.brick >> l) & 1) && A.generic[l];
+        if (lookup_variant() != 2 || !tile_ok(A, store_dtype == DVC_BF16 ? 2 : 4) || generic_brick)
+            return fail(DVC_ERR_UNSUPPORTED, "lookup: a DVC_BRICKED pyramid needs the tile kernel (radius 1..6, "
+                                             "no legacy W != D bricked level, lookup_variant 2)");
+    }
     const long long items = (long long)A.nl * A.nach * B * A.nqb;
     const unsigned blocks = (unsigned)ceil_div(items, 4);
     hipStream_t s = (hipStream_t)stream;
@@ -620,10 +646,13 @@ int dvc_corr_lookup_proj(const void *corr, const float *coords, const void *pack
         return fail(DVC_ERR_UNSUPPORTED, "lookup_proj: radius %d outside [1, %d]", radius, DVC_PROJ_MAX_RADIUS);
     if (convention != DVC_FIXED && convention != DVC_LEGACY)
         return fail(DVC_ERR_INVALID, "lookup_proj: bad convention %d", convention);
+    const bool bricked = (store_dtype & DVC_BRICKED) != 0;
+    store_dtype &= ~DVC_BRICKED;
     if (store_dtype != DVC_BF16 && store_dtype != DVC_F32)
         return fail(DVC_ERR_INVALID, "lookup_proj: bad dtype %d", store_dtype);
     LookupArgs A;
     fill_lookup_args(A, lay, corr, coords, nullptr, B, Nq, radius, convention);
+    if (bricked) A.brick = dvc_bricked_levels(&lay);   // (the tile kernel is the only PROJ path)
     for (int l = 0; l < lay.num_levels; ++l)
         if (A.generic[l] && !A.zero[l])
             return fail(DVC_ERR_UNSUPPORTED, "lookup_proj: legacy level %d with W != D (%d, %d)", l, lay.W[l],

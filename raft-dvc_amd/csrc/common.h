@@ -45,6 +45,7 @@ struct LookupArgs {
     int ldpol;                     // tile kernel: cache-policy bits of the plane loads
     int split_levels;              // tile kernel: one level per workgroup (blockIdx.y), for launches whose
                                    // query tiles alone cannot fill the chip (one rank's slab)
+    int brick;                     // tile kernel: bit l = level l stored in (1, 8, 8) bricks (DVC_BRICKED)
     long long off[DVC_MAX_LEVELS];
     // tile kernel with the motion encoder's convc1 fused (PROJ instances only):
     // packed bf16 weights (dvc_proj_pack), bias[96], out (B, 96, Nq)

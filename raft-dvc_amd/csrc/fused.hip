@@ -275,7 +275,7 @@ int fused_lookup(const void *packed_q, const void *packed_t, const float *coords
     const float scale = 1.0f / sqrtf((float)C);
     const int n = 2 * radius + 1;
     const long long n3 = (long long)n * n * n;
-    LookupArgs A;
+    LookupArgs A{};
     A.coords = coords; A.out = out; A.Nq = Nq; A.B = B; A.Ltot = lay.num_levels; A.nl = 1;
     A.legacy = convention == DVC_LEGACY; A.r = radius; A.ablate = 0;
     A.ach = n >= 3 ? 3 : n;

@@ -129,7 +129,7 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
     constexpr int XROW = C::NWAVES * ProjCfg::KW * 2 + 16;    // bytes per query row of X (+16: bank spread)
     static_assert(!PROJ || C::COLS * n <= ProjCfg::KW, "PROJ: one wave's row values must fit a 32-k slice");
     __shared__ __attribute__((aligned(16))) unsigned char smem[C::LDS];
-    __shared__ int tab[3][64];   // per query of the tile: ih, cs, za (element units)
+    __shared__ int tab[4][64];   // per query of the tile: ih, cs, za, iv (element units)
     __shared__ __attribute__((aligned(16))) unsigned char xs[PROJ ? 64 * XROW : 16];
 
     const int tid = threadIdx.x;
@@ -307,8 +307,14 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
             tab[0][lane] = min(max(ih, -2 * NW), Hl);
             tab[1][lane] = cs;
             tab[2][lane] = za;
+            tab[3][lane] = iv;
         }
         __syncthreads();
+        // a bricked level (DVC_BRICKED, bit l of A.brick): voxel (y, x, z) at
+        // ((y * W/8 + x/8) * Dp/8 + z/8) * 64 + (x%8) * 8 + z%8, i.e. (1, 8, 8) bricks of one 128-byte
+        // line, so the strip of a window plane touches lines of 8 columns x 8 z instead of 2 x 32
+        // (Dp = 32) or 1 x 64; the strip's z-chunk that the query's run never reaches is not loaded.
+        const bool bk8 = (A.brick >> l) & 1;
 
         // this thread's chunks of every plane: (query j, column c, z-chunk k).  voff =
         // byte offset of the chunk in window plane 0; window plane wp adds wp * plane_bytes.
@@ -328,22 +334,29 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
             const int jj = ok ? j : 0;
             const int ihj = tab[0][jj];
             const int plo = min(max(-ihj, 0), NW), phi = min(max(Hl - ihj, 0), NW);
-            const unsigned mask = ok && jj < nvalid ? ((1u << phi) - 1u) & ~((1u << plo) - 1u) : 0u;
-            pk[k] = (ok ? (unsigned)(jj * SQ + (c * ZW + zc * CE) * ES) >> 3 : 0xffffu) | (mask << 16);
-            voff[k] = (int)(((long long)jj * A.row_stride + A.off[l] + (long long)ihj * Wl * Dpl +
-                             (long long)(tab[1][jj] + c) * Dpl + tab[2][jj] + zc * CE) * ES);
+            unsigned mask = ok && jj < nvalid ? ((1u << phi) - 1u) & ~((1u << plo) - 1u) : 0u;
+            if (bk8) {
+                const int zs = tab[2][jj] + zc * CE, ivj = tab[3][jj], x = tab[1][jj] + c;
+                if (!(zs < ivj + NW && zs + CE > ivj)) mask = 0u;   // the run never reaches this chunk
+                pk[k] = (ok ? (unsigned)(jj * SQ + (c * ZW + zc * CE) * ES) >> 3 : 0xffffu) | (mask << 16);
+                voff[k] = (int)(((long long)jj * A.row_stride + A.off[l] + (long long)ihj * Wl * Dpl +
+                                 ((long long)(x >> 3) * (Dpl >> 3) + (zs >> 3)) * 64 + (x & 7) * 8 + (zs & 7)) * ES);
+            } else {
+                pk[k] = (ok ? (unsigned)(jj * SQ + (c * ZW + zc * CE) * ES) >> 3 : 0xffffu) | (mask << 16);
+                voff[k] = (int)(((long long)jj * A.row_stride + A.off[l] + (long long)ihj * Wl * Dpl +
+                                 (long long)(tab[1][jj] + c) * Dpl + tab[2][jj] + zc * CE) * ES);
+            }
         }
         auto load_plane = [&](int wp, u32x4 (&st)[C::MAXCH]) {
 #pragma unroll
             for (int k = 0; k < C::MAXCH; ++k) {
                 if constexpr ((ABL & 2) != 0) st[k] = u32x4{(unsigned)k, 0, 0, 0};
                 else if (pk[k] & (1u << (16 + wp))) {
+                    const int o = voff[k] + wp * plane_bytes;   // (bricks keep whole planes: same plane stride)
                     if (ldpol == 2)
-                        st[k] = __builtin_bit_cast(
-                            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, voff[k] + wp * plane_bytes, 0, 2));
+                        st[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, o, 0, 2));
                     else
-                        st[k] = __builtin_bit_cast(
-                            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, voff[k] + wp * plane_bytes, 0, 0));
+                        st[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, o, 0, 0));
                 }
             }
         };

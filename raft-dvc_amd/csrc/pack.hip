@@ -112,7 +112,16 @@ struct PyrGeo {
     long long off[4];
     long long row_stride;
     int ncx, ncy, ncz;   // cells per axis (level 0, ceil)
+    int brick;           // bit l: level l in (1, 8, 8) bricks (DVC_BRICKED, include/dvccorr.h)
 };
+
+// Packed-target row of level-l voxel (Y, X, Z): linear (Y W + X) Dp + Z, or its (1, 8, 8) brick slot.
+__device__ __forceinline__ long long pyr_row(const PyrGeo &g, int l, int Y, int X, int Z) {
+    if ((g.brick >> l) & 1)
+        return g.off[l] + (((long long)Y * (g.W[l] >> 3) + (X >> 3)) * (g.Dp[l] >> 3) + (Z >> 3)) * 64 + (X & 7) * 8 +
+               (Z & 7);
+    return g.off[l] + ((long long)Y * g.W[l] + X) * g.Dp[l] + Z;
+}
 
 // kPyrCG = channels per workgroup: 32 where the volume has enough cells to fill the chip (each voxel's
 // packed row then leaves as 64-byte segments; 66 KB of LDS, two workgroups per CU), else 16 (32-byte
@@ -208,7 +217,7 @@ __global__ __launch_bounds__(256) void k_pack_pyramid(const float *__restrict__ 
             const int Y = ly0 + y, X = lx0 + x, Z = lz0 + z;
             const int c = cg * kPyrCG + ch;
             if (Y >= g.H[l] || X >= g.W[l] || Z >= g.D[l] || c >= g.Cp) continue;
-            T *d = db + (g.off[l] + ((long long)Y * g.W[l] + X) * g.Dp[l] + Z) * g.Cp + c;
+            T *d = db + pyr_row(g, l, Y, X, Z) * g.Cp + c;
             float w[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) w[k] = s[v][ch + k];
@@ -232,7 +241,7 @@ __global__ __launch_bounds__(256) void k_pack_pyramid(const float *__restrict__ 
                 const int Y = ly0 + yx / e, X = lx0 + yx % e;
                 const int c = cg * kPyrCG + ck * 8;
                 if (Y >= g.H[l] || X >= g.W[l] || c >= g.Cp) continue;
-                T *d = db + (g.off[l] + ((long long)Y * g.W[l] + X) * g.Dp[l] + g.D[l] + zp) * g.Cp + c;
+                T *d = db + pyr_row(g, l, Y, X, g.D[l] + zp) * g.Cp + c;
                 if constexpr (sizeof(T) == 4) {
                     *reinterpret_cast<float4 *>(d) = float4{0.f, 0.f, 0.f, 0.f};
                     *reinterpret_cast<float4 *>(d + 4) = float4{0.f, 0.f, 0.f, 0.f};

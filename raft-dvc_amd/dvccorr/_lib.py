@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("DVCCORR_LIB") or os.path.join(_HERE, "libdvccorr.so")
 
 DVC_OK, DVC_ERR_INVALID, DVC_ERR_UNSUPPORTED, DVC_ERR_LAUNCH, DVC_ERR_RUNTIME = range(5)
 DVC_F32, DVC_BF16 = 0, 1
+DVC_BRICKED = 0x100     # layout flag ORed into a dtype (include/dvccorr.h)
 DVC_FIXED, DVC_LEGACY = 0, 1
 MAX_LEVELS = 8
 
@@ -26,7 +27,7 @@ EXPORTED = (
     "dvc_sample3d", "dvc_set_tuning", "dvc_last_error", "dvc_version", "dvc_abi_version",
     "dvc_corr_backward_workspace_bytes", "dvc_corr_backward", "dvc_proj_packed_bytes", "dvc_proj_pack",
     "dvc_corr_lookup_proj", "dvc_lookup_fused_proj_workspace_bytes", "dvc_corr_lookup_fused_proj",
-    "dvc_coords_grid", "dvc_upflow", "dvc_flow_step",
+    "dvc_coords_grid", "dvc_upflow", "dvc_flow_step", "dvc_bricked_levels",
 )
 PROJ_COUT = 96          # DVC_PROJ_COUT (convc1 output channels, update.py:222)
 PROJ_MAX_RADIUS = 4     # DVC_PROJ_MAX_RADIUS
@@ -71,6 +72,7 @@ def lib() -> ctypes.CDLL:
     i32, i64, vp, sz = ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t
     sig = {
         "dvc_layout_init": (i32, [i32, i32, i32, i32, i32, ctypes.POINTER(Layout)]),
+        "dvc_bricked_levels": (i32, [ctypes.POINTER(Layout)]),
         "dvc_pack_workspace_bytes": (sz, [i32, i32, i32, i32, i32, i32]),
         "dvc_pack_queries": (i32, [vp, vp, i32, i32, i64, i32, vp]),
         "dvc_pack_targets": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp]),
@@ -129,3 +131,8 @@ def layout(H: int, W: int, D: int, num_levels: int, C: int = 1) -> Layout:
     if rc != DVC_OK:
         raise RuntimeError(lib().dvc_last_error().decode(errors="replace"))
     return lay
+
+
+def bricked_levels(lay: Layout) -> int:
+    """Bit mask of the levels a DVC_BRICKED pyramid stores in (1, 8, 8) bricks."""
+    return int(lib().dvc_bricked_levels(ctypes.byref(lay)))

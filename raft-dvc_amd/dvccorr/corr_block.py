@@ -137,6 +137,28 @@ class _Block:
         return out.view(B, -1, H, W, D)
 
 
+def brick_flag(lay, radius: int, legacy: bool, eligible: bool, bricked: Optional[bool] = None) -> int:
+    """DVC_BRICKED when the materialised pyramid should store its wide levels in (1, 8, 8) bricks: a GEMM-built
+    inference pyramid (the pooled build and the backward read the linear layout) whose lookups run on the tile
+    kernel (radius 1..6, <= 4 levels, no legacy W != D bricked level).  bricked=False forces the linear layout
+    (e.g. to A/B the walk kernels); DVCCORR_BRICKED=0 turns the default off."""
+    if bricked is False or not eligible or os.environ.get("DVCCORR_BRICKED", "1") == "0":
+        return 0
+    if not (1 <= radius <= 6) or lay.num_levels > 4:
+        return 0
+    m = ops.bricked_levels(lay)
+    if m == 0 or (legacy and any((m >> l) & 1 and lay.W[l] != lay.D[l] for l in range(lay.num_levels))):
+        return 0
+    return ops.DVC_BRICKED
+
+
+def brick_index(h: int, w: int, dp: int, device) -> torch.Tensor:
+    """Brick slot of each level voxel in (y, x, z) order: ((y w/8 + x/8) dp/8 + z/8) 64 + (x%8) 8 + z%8."""
+    y, x, z = torch.meshgrid(torch.arange(h, device=device), torch.arange(w, device=device),
+                             torch.arange(dp, device=device), indexing="ij")
+    return ((((y * (w // 8)) + x // 8) * (dp // 8) + z // 8) * 64 + (x % 8) * 8 + z % 8).reshape(-1)
+
+
 def _check_fmaps(fmap1: torch.Tensor, fmap2: torch.Tensor) -> None:
     if fmap1.ndim != 5:
         raise ValueError(f"Expected 5D feature maps (B, C, H, W, D); got {fmap1.ndim}D")
@@ -149,7 +171,8 @@ class CorrBlock(_Block):
     """All-pairs 3-D correlation pyramid + radius-r trilinear lookup (materialised)."""
 
     def __init__(self, fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int = 4, radius: int = 4,
-                 legacy_wd_swap: bool = False, *, precision: Optional[str] = None, build: str = "gemm"):
+                 legacy_wd_swap: bool = False, *, precision: Optional[str] = None, build: str = "gemm",
+                 bricked: Optional[bool] = None):
         _check_fmaps(fmap1, fmap2)
         self.num_levels = num_levels
         self.radius = radius
@@ -172,8 +195,12 @@ class CorrBlock(_Block):
                 f"dvccorr.CorrBlock: the materialised {self.precision} pyramid of ({H},{W},{D}) x {num_levels} levels "
                 f"needs {need / 2**30:.1f} GiB, {avail / 2**30:.1f} GiB of HBM is available; use "
                 f"CorrBlockFused (corr_impl 'mi355x_fused' / 'mi355x_auto'), which never materialises it")
+        # levels with >= 64-byte z-rows in (1, 8, 8) bricks (DVC_BRICKED): fewer HBM lines per lookup window
+        self._brick = brick_flag(self._lay, radius, legacy_wd_swap, build == "gemm" and self._grad_fmaps is None,
+                                 bricked)
+        self._ldt = self._dt | self._brick              # the lookups' store dtype code (with the layout flag)
         q = ops.pack_queries(fmap1.detach().reshape(B, C, H * W * D), self._dt)
-        t = ops.pack_targets(fmap2.detach(), num_levels, self._dt)
+        t = ops.pack_targets(fmap2.detach(), num_levels, self._ldt)
         # the backward needs the packed operands (O(C * voxels)): keep them only then
         self._q, self._t = (q, t) if self._grad_fmaps is not None else (None, None)
         if build == "gemm":       # every level from the pooled targets, one launch
@@ -187,21 +214,25 @@ class CorrBlock(_Block):
 
     @property
     def corr_pyramid(self) -> List[torch.Tensor]:
-        """Zero-copy views shaped like the reference's list: (B*N, 1, H_l, W_l, D_l) per level."""
+        """The pyramid shaped like the reference's list: (B*N, 1, H_l, W_l, D_l) per level -- zero-copy views,
+        except for bricked levels (DVC_BRICKED), which are gathered back into (h, w, d) order."""
         B, _, H, W, D = self.shape
         flat = self._corr.reshape(B * H * W * D, self._lay.row_stride)
+        mask = ops.bricked_levels(self._lay) if self._brick else 0
         views = []
         for l, (h, w, d) in enumerate(self._lay.levels()):
             dp = self._lay.Dp[l]
             off = self._lay.offset[l]
-            v = flat[:, off:off + h * w * dp].reshape(B * H * W * D, 1, h, w, dp)[..., :d]
-            views.append(v)
+            sec = flat[:, off:off + h * w * dp]
+            if (mask >> l) & 1:
+                sec = sec[:, brick_index(h, w, dp, flat.device)]
+            views.append(sec.reshape(B * H * W * D, 1, h, w, dp)[..., :d])
         return views
 
     def _lookup_flat(self, coords_flat: torch.Tensor) -> torch.Tensor:
         _, _, H, W, D = self.shape
         return library.lookup(self._corr, coords_flat, H, W, D, self.num_levels, self.radius, self.legacy_wd_swap,
-                              self._dt)
+                              self._ldt)
 
     def lookup_convc1(self, coords: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
         """F.relu(convc1(self(coords))) -> (B, 96, H, W, D) fp32 with convc1 fused into the lookup.
@@ -219,7 +250,7 @@ class CorrBlock(_Block):
             return self._convc1_composition(coords, w, bias)
         packed = ops.proj_pack_cached(weight, self.num_levels, self.radius, self.legacy_wd_swap)
         out = ops.lookup_proj(self._corr, coords.reshape(B, 3, H * W * D), packed, bias, H, W, D,
-                              self.num_levels, self.radius, self.legacy_wd_swap, self._dt)
+                              self.num_levels, self.radius, self.legacy_wd_swap, self._ldt)
         return out.view(B, -1, H, W, D)
 
 

@@ -23,9 +23,17 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import DVC_BF16, DVC_F32, DVC_FIXED, DVC_LEGACY, check, layout, lib
+from ._lib import DVC_BF16, DVC_BRICKED, DVC_F32, DVC_FIXED, DVC_LEGACY, bricked_levels, check, layout, lib
 
-_TORCH_DT = {DVC_F32: torch.float32, DVC_BF16: torch.bfloat16}
+
+class _DtypeMap(dict):
+    """dtype code -> torch dtype; a DVC_BRICKED layout flag ORed into the code is ignored."""
+
+    def __getitem__(self, code):
+        return super().__getitem__(int(code) & ~DVC_BRICKED)
+
+
+_TORCH_DT = _DtypeMap({DVC_F32: torch.float32, DVC_BF16: torch.bfloat16})
 
 
 def dtype_code(precision: str) -> int:
@@ -65,6 +73,8 @@ def pack_queries(fmap1_slab: torch.Tensor, dtype: int) -> torch.Tensor:
 
 
 def pack_targets(fmap2: torch.Tensor, num_levels: int, dtype: int, out: torch.Tensor = None) -> torch.Tensor:
+    """fmap2 -> packed targets of every level; dtype | DVC_BRICKED stores the bricked levels in brick order
+    (the materialised build then writes a bricked pyramid, which only the tile lookups read)."""
     _need_cuda(fmap2)
     f = _f32c(fmap2)
     B, C, H, W, D = f.shape
@@ -300,4 +310,4 @@ def flow_step(coords1: torch.Tensor, delta_flow, target_shape):
 __all__ = ["pack_queries", "pack_targets", "build", "pool", "lookup", "lookup_fused", "lookup_fused_proj", "corr_backward", "sample3d",
            "proj_pack", "proj_pack_cached", "lookup_proj",
            "coords_grid", "upflow", "flow_step",
-           "fused_workspace", "dtype_code", "layout", "_lib"]
+           "fused_workspace", "dtype_code", "layout", "bricked_levels", "DVC_BRICKED", "_lib"]

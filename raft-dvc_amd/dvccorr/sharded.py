@@ -114,8 +114,12 @@ class HipRows:
         self.dims = (C, H, W, D)
         self.L, self.R, self.legacy, self.impl = num_levels, radius, legacy, impl
         self.dt = ops.dtype_code(precision)
+        # materialised rows: wide levels in (1, 8, 8) bricks, read by the tile lookups (corr_block.brick_flag)
+        from .corr_block import brick_flag
+        lay = layout(H, W, D, num_levels, C)
+        self.ldt = self.dt | (brick_flag(lay, radius, legacy, True) if impl == "materialised" else 0)
         self.q = ops.pack_queries(q_flat, self.dt)
-        self.t = ops.pack_targets(fmap2, num_levels, self.dt)
+        self.t = ops.pack_targets(fmap2, num_levels, self.ldt)
         if impl == "materialised":
             self.corr = ops.build(self.q, self.t, C, H, W, D, num_levels, self.dt, self.dt)
         elif impl == "fused":
@@ -126,7 +130,7 @@ class HipRows:
     def lookup(self, coords_flat: torch.Tensor) -> torch.Tensor:
         C, H, W, D = self.dims
         if self.impl == "materialised":
-            return ops.lookup(self.corr, coords_flat, H, W, D, self.L, self.R, self.legacy, self.dt)
+            return ops.lookup(self.corr, coords_flat, H, W, D, self.L, self.R, self.legacy, self.ldt)
         return ops.lookup_fused(self.q, self.t, coords_flat, C, H, W, D, self.L, self.R, self.legacy, self.dt,
                                 workspace=self.ws)
 
@@ -147,7 +151,7 @@ class HipRows:
         packed = ops.proj_pack_cached(weight, self.L, self.R, self.legacy)
         if self.impl == "materialised":
             return ops.lookup_proj(self.corr, coords_flat, packed, bias, H, W, D, self.L, self.R, self.legacy,
-                                   self.dt)
+                                   self.ldt)
         if getattr(self, "pws", None) is None:   # sort keys + [B][N][96] rows, reused across lookups
             B, _, N = coords_flat.shape
             self.pws = torch.empty((max(ops.lib().dvc_lookup_fused_proj_workspace_bytes(B, N), 256),),

@@ -160,3 +160,38 @@ def test_precision_policy_host_logic(monkeypatch):
     assert dvccorr.resolve_precision(b16, "fp32") == "fp32"
     with pytest.raises(ValueError):
         dvccorr.resolve_precision(f32, "fp8")
+
+
+@pytest.mark.parametrize("shape,L,expect", [
+    ((32, 32, 32), 4, 0b0001),     # level 0 (Dp 32, W 32): bricked; level 1 (16^3): 32-byte z-rows, linear
+    ((64, 64, 64), 4, 0b0011),     # levels 0 and 1
+    ((64, 36, 64), 4, 0b0000),     # W % 8 != 0 at level 0; level 1 W = 18
+    ((16, 16, 16), 4, 0b0000),     # no level with a 64-byte z-row
+    ((32, 40, 33), 3, 0b0001),     # Dp 40 >= 32 (D 33 padded)
+])
+def test_bricked_levels(shape, L, expect):
+    """DVC_BRICKED stores exactly the levels with Dp >= 32 and W % 8 == 0 in (1, 8, 8) bricks (host function),
+    and the brick slots of such a level are a permutation of its linear slots."""
+    from dvccorr import _lib
+    from dvccorr.corr_block import brick_index
+    lay = _lib.layout(*shape, L, 32)
+    assert _lib.bricked_levels(lay) == expect
+    for l, (h, w, d) in enumerate(lay.levels()):
+        if (expect >> l) & 1:
+            idx = brick_index(h, w, lay.Dp[l], torch.device("cpu"))
+            assert torch.equal(torch.sort(idx).values, torch.arange(h * w * lay.Dp[l]))
+
+
+def test_brick_flag_policy(monkeypatch):
+    """The materialised block bricks its wide levels only for the tile kernel's cases."""
+    from dvccorr import _lib
+    from dvccorr.corr_block import brick_flag
+    lay = _lib.layout(32, 32, 32, 4, 128)
+    assert brick_flag(lay, 4, False, True) == _lib.DVC_BRICKED
+    assert brick_flag(lay, 4, False, False) == 0          # pooled build / gradients: linear
+    assert brick_flag(lay, 4, False, True, bricked=False) == 0
+    assert brick_flag(lay, 7, False, True) == 0           # radius outside the tile kernel: the walk
+    assert brick_flag(_lib.layout(32, 32, 32, 5, 128), 4, False, True) == 0   # > 4 levels: per-level pack
+    assert brick_flag(_lib.layout(32, 32, 40, 4, 128), 4, True, True) == 0    # legacy W != D on a bricked level
+    monkeypatch.setenv("DVCCORR_BRICKED", "0")
+    assert brick_flag(lay, 4, False, True) == 0

@@ -262,7 +262,8 @@ def test_lookup_variants(variant):
                                        ((30, 28, 40), 2, 6), ((40, 36, 33), 3, 4), ((16, 12, 20), 4, 4)])
 def test_tile_kernel_matches_walk(shape, L, r):
     """The LDS-staged tile kernel (variant 2) is bit-identical to the lane-per-query walk (variant 0):
-    same per-axis weights, same separable summation order.  Ragged tiles (Nq % 64 != 0), non-cubic and
+    same per-axis weights, same separable summation order; on the default block (wide levels in
+    DVC_BRICKED bricks where the shape allows: the 32^3 case) and on a linear one.  Ragged tiles (Nq % 64 != 0), non-cubic and
     odd sizes, D padding, every radius the kernel is instantiated for, both conventions, both store
     dtypes, wide flows that leave the volume, and NaN / huge coordinates."""
     import dvccorr
@@ -280,18 +281,22 @@ def test_tile_kernel_matches_walk(shape, L, r):
     try:
         for prec in ("bf16", "fp32"):
             for legacy in (False, True):
+                # the walk reads the linear layout; the default block may store wide levels in bricks
+                lin = dvccorr.CorrBlock(f1, f2, L, r, legacy_wd_swap=legacy, precision=prec, bricked=False)
                 blk = dvccorr.CorrBlock(f1, f2, L, r, legacy_wd_swap=legacy, precision=prec)
                 outs = []
-                for v in (0, 2):
+                for v, b in ((0, lin), (2, blk)):
                     _lib.set_tuning("lookup_variant", v)
-                    outs.append(blk(c))
+                    outs.append(b(c))
+                _lib.set_tuning("lookup_variant", 2)
+                outs.append(lin(c))   # the tile kernel on the linear layout too
                 if r == 4:   # three 3-column waves (lookup_waves 0) vs the default four balanced waves
                     _lib.set_tuning("lookup_waves", 0)
                     outs.append(blk(c))
                     _lib.set_tuning("lookup_waves", 4)
                 torch.cuda.synchronize()
-                for o in outs[2:]:
-                    assert torch.equal(outs[0], o), (shape, L, r, prec, legacy, "lookup_waves 0")
+                for k, o in enumerate(outs[2:]):
+                    assert torch.equal(outs[0], o), (shape, L, r, prec, legacy, ("tile, linear", "lookup_waves 0")[k])
                 assert torch.isfinite(outs[1]).all(), (prec, legacy)
                 assert torch.equal(outs[0], outs[1]), (shape, L, r, prec, legacy,
                                                         float((outs[0] - outs[1]).abs().max()))

@@ -35,7 +35,8 @@ f2 = torch.randn(1, 128, S, S, S, generator=g).to(dev)
 c = (dvccorr.coords_grid_3d(1, S, S, S, torch.device("cpu")) + (torch.rand(1, 3, S, S, S, generator=g) * 4 - 2)).to(dev)
 with torch.no_grad():
     cls = dvccorr.CorrBlock if a.impl == "materialised" else dvccorr.CorrBlockFused
-    kw = {"build": a.build} if a.impl == "materialised" else {}
+    # (the walk variants read the linear layout only)
+    kw = {"build": a.build, "bricked": None if a.variant == 2 else False} if a.impl == "materialised" else {}
     blk = cls(f1, f2, a.levels, 4, precision=a.precision, **kw)
     K = a.levels * 729
     w = ((torch.rand(96, K, generator=g) * 2 - 1) / K ** 0.5).to(dev)
