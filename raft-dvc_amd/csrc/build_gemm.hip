@@ -495,6 +495,35 @@ __global__ __launch_bounds__(256, 1) void k_build_f32(const float *__restrict__ 
     const long long ncol_tiles = (col_end - col_begin + kFP - 1) / kFP;
     const int h = lane >> 5, r32 = lane & 31;
 
+    // Resident queries (Cp <= 128): the next column tile's targets are loaded into registers (16-byte
+    // loads, Cp / 8 per thread) right after this tile's image is in LDS, so they fly under this tile's
+    // MFMAs, epilogue and stores instead of stalling the block before every tile (round 2: the exposed
+    // staging made the f32 build ~6x its MFMA time).
+    constexpr int kPF = 16;                // 128 rows x 128 channels / 4 floats / 256 threads
+    u32x4 pf[kPF];
+    const int npf = Cp / 8;                // pieces per thread (Cp is a multiple of 32 here)
+    auto load_t = [&](long long ctn) {
+        const long long pn = col_begin + ctn * kFP;
+        const int n16 = Cp / 4;            // 16-byte pieces per target row
+#pragma unroll
+        for (int i = 0; i < kPF; ++i)
+            if (i < npf) {
+                const int id = t + 256 * i, row = id / n16, pc = id - row * n16;
+                pf[i] = *reinterpret_cast<const u32x4 *>(Tb + (pn + row) * Cp + 4 * pc);
+            }
+    };
+    auto put_t = [&]() {
+        const int nsl = Cp / 2, msk = (nsl >= 32 ? 32 : nsl) - 1, n16 = Cp / 4;
+#pragma unroll
+        for (int i = 0; i < kPF; ++i)
+            if (i < npf) {
+                const int id = t + 256 * i, row = id / n16, pc = id - row * n16;
+                sT[row * nsl + ((2 * pc) ^ (row & msk))] = u32x2{pf[i][0], pf[i][1]};
+                sT[row * nsl + ((2 * pc + 1) ^ (row & msk))] = u32x2{pf[i][2], pf[i][3]};
+            }
+    };
+    if (resident && chunk < ncol_tiles) load_t(chunk);
+
     for (long long ct = chunk; ct < ncol_tiles; ct += nchunk) {
         const long long p0 = col_begin + ct * kFP;
         f32x16 acc[2];
@@ -507,13 +536,18 @@ __global__ __launch_bounds__(256, 1) void k_build_f32(const float *__restrict__ 
             const int nsl = kc / 2;
             const int msk = (nsl >= 32 ? 32 : nsl) - 1;
             __syncthreads();   // previous chunk / staging image fully read
-            if (!resident) stage_q(k0, nsl, msk);
-            for (int id = t; id < kFP * nsl; id += 256) {
-                const int row = id / nsl, s = id - row * nsl;
-                sT[row * nsl + (s ^ (row & msk))] =
-                    *reinterpret_cast<const u32x2 *>(Tb + (p0 + row) * Cp + k0 + 2 * s);
+            if (resident) {
+                put_t();
+            } else {
+                stage_q(k0, nsl, msk);
+                for (int id = t; id < kFP * nsl; id += 256) {
+                    const int row = id / nsl, s = id - row * nsl;
+                    sT[row * nsl + (s ^ (row & msk))] =
+                        *reinterpret_cast<const u32x2 *>(Tb + (p0 + row) * Cp + k0 + 2 * s);
+                }
             }
             __syncthreads();
+            if (resident && ct + nchunk < ncol_tiles) load_t(ct + nchunk);   // under this tile's MFMAs
             const int arow = 32 * w + r32;
             for (int kt = 0; kt < kc / 4; ++kt) {
                 const int s = 2 * kt + h;
