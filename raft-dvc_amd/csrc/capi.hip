@@ -74,7 +74,9 @@ static thread_local int g_lookup_nt = 1;          // nontemporal output stores i
 static thread_local int g_lookup_order = 1;       // tile kernel level order (LookupArgs::order)
 static thread_local int g_lookup_ldpol = 0;       // tile kernel load cache policy (LookupArgs::ldpol)
 static thread_local int g_build_ablate = 0;       // diagnostics only: k_build_bf16 ablation instance
-static thread_local int g_build_stpol = 0;        // cache-policy bits of the build's output stores
+// build output stores: 1 = nontemporal (default; round 2 A/B, bench n1 twice each: build 0.545 -> 0.506 ms,
+// step 2.20 -> 2.11 ms -- the 2.46 GB pyramid never fits the caches it would otherwise sweep), 0 = default policy
+static thread_local int g_build_stpol = 1;
 static thread_local int g_build_variant = 1;      // 1 = two-barrier bf16-store kernel (k_build_bf16_2b), 0 = k_build_bf16
 // fused lookup kernel where the MFMA path applies: 2 = k_fused_box 2x2x16, 8 waves (default),
 // 3 = k_fused_box 4x4x4 cubes, 8 waves, 4 = k_fused_box 2x2x16, 4 waves, 1 = k_fused_tile, 0 = two-stage VALU
