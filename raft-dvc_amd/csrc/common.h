@@ -11,6 +11,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned short bf16_t;   // storage type of one bf16 value
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 namespace dvc {
 
@@ -24,6 +25,16 @@ struct Geo {
     long long off[DVC_MAX_LEVELS];
     long long row_stride;
 };
+
+// {p, p} in two registers.  A packed-FP32 op whose low lane reads the high element of a source (op_sel
+// [1, ..], the compiler's way to broadcast the high half of a pair) returned wrong low-lane values in
+// lanes 48-63 now and then while another wave of the same workgroup ran MFMAs (k_fused_proj, round 2,
+// tools/dbg_poison4.py).  The empty asm hides that the halves are equal, so no such broadcast is formed.
+__device__ __forceinline__ f32x2 splat2(float p) {
+    f32x2 v = {p, p};
+    asm volatile("" : "+v"(v));
+    return v;
+}
 
 __device__ __forceinline__ float bf16_bits_to_f32(unsigned int h) { return __uint_as_float(h << 16); }
 

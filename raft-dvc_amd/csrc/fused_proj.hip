@@ -376,7 +376,8 @@ __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict_
                 for (int uu = 0; uu < NU; ++uu) {
                     const float p00 = wx0[uu] * wy0, p10 = wx1[uu] * wy0;
                     const float p01 = wx0[uu] * wy1, p11 = wx1[uu] * wy1;
-                    const f32x2 P00 = {p00, p00}, P10 = {p10, p10}, P01 = {p01, p01}, P11 = {p11, p11};
+                    // broadcasts materialised (splat2): the consumer waves run MFMAs meanwhile
+                    const f32x2 P00 = splat2(p00), P10 = splat2(p10), P01 = splat2(p01), P11 = splat2(p11);
 #pragma unroll
                     for (int i = 0; i < NP; ++i) {
                         f32x2 v = P00 * zp[uu].p[i];

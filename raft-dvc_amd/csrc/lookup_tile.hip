@@ -417,7 +417,9 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
                     const int uu = k - 1;
                     const float p00 = wx0[uu] * wy0, p10 = wx1[uu] * wy0;
                     const float p01 = wx0[uu] * wy1, p11 = wx1[uu] * wy1;
-                    const f32x2 P00 = {p00, p00}, P10 = {p10, p10}, P01 = {p01, p01}, P11 = {p11, p11};
+                    // PROJ (MFMA consumer wave alongside): broadcasts materialised, see splat2
+                    const auto bc = [](float p) { if constexpr (PROJ) return splat2(p); else return f32x2{p, p}; };
+                    const f32x2 P00 = bc(p00), P10 = bc(p10), P01 = bc(p01), P11 = bc(p11);
                     const __amdgpu_buffer_rsrc_t rs = out_rsrc(obase, a, u0 + uu);
                     [[maybe_unused]] float wide[2 * NP + 1];
 #pragma unroll

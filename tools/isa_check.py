@@ -1,0 +1,93 @@
+"""Scan the gfx950 assembly of the HIP sources for two instruction patterns kept out of every kernel:
+
+  * packed-FP32 ops (v_pk_fma/mul/add_f32) whose LOW lane reads the HIGH element of a VGPR source
+    (an op_sel bit set) in a kernel that also runs MFMAs.  Such ops returned wrong low-lane values in lanes 48-63 now and then while
+    another wave of the workgroup ran MFMAs (k_fused_proj, round 2: tools/dbg_poison4.py found the
+    corrupted X values, all from `v_pk_fma_f32 ... op_sel:[1,0,0]`; with the broadcasts materialised
+    by splat2() 0 of 220 poisoned runs differ, against ~4 % before);
+  * MFMAs whose destination overlaps their own A or B source registers (reported, not fatal).
+
+    python tools/isa_check.py [file.hip ...]      exit status 1 if such an op_sel read is found"""
+import concurrent.futures as cf
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "raft-dvc_amd", "csrc")
+MF = re.compile(r'v_mfma\S+\s+v\[(\d+):(\d+)\],\s+v\[(\d+):(\d+)\],\s+v\[(\d+):(\d+)\]')
+PK = re.compile(r'v_pk_(?:fma|mul|add)_f32\b.*\bop_sel:\[([01,]+)\]')
+
+
+def extra_flags(src):
+    """Per-object flags of the Makefile ('obj/X.o: EXTRA := ...')."""
+    obj = "obj/" + os.path.splitext(os.path.basename(src))[0] + ".o"
+    for line in open(os.path.join(CSRC, "Makefile")):
+        m = re.match(r'^(\S+):\s*EXTRA\s*:=\s*(.*)$', line)
+        if m and m.group(1) == obj:
+            return m.group(2).split()
+    return []
+
+
+def assemble(src, tmp):
+    out = os.path.join(tmp, os.path.basename(src) + ".s")
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-I" + os.path.join(ROOT, "include"),
+                    "-I" + CSRC, "--cuda-device-only", "-S", src, "-o", out] + extra_flags(src), check=True,
+                   stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    return out
+
+
+def vgpr_opsel(line, bits):
+    """True if a source whose op_sel bit is set is a VGPR pair (SGPR-pair broadcasts, e.g. the scale
+    factor of the k_build_bf16 epilogues, are uniform operands and have run bit-exact in every test)."""
+    ops = [o.strip() for o in line.split(None, 1)[1].split(" op_sel")[0].split(",")]
+    srcs = ops[1:]   # ops[0] is the destination
+    return any(b == "1" and i < len(srcs) and srcs[i].startswith("v") for i, b in enumerate(bits.split(",")))
+
+
+def scan(asm):
+    """(op_sel reads in kernels that also run MFMAs, MFMA overlaps, op_sel reads in MFMA-free kernels)"""
+    pk, mf, has_mfma = {}, {}, set()
+    cur = None
+    for line in open(asm):
+        m = re.match(r'^(_Z\S+):', line)
+        if m:
+            cur = m.group(1)
+            continue
+        if "v_mfma" in line:
+            has_mfma.add(cur)
+        m = PK.search(line)
+        if m and "1" in m.group(1) and vgpr_opsel(line, m.group(1)):
+            pk.setdefault(cur, []).append(line.strip())
+        m = MF.search(line)
+        if m:
+            r = [int(g) for g in m.groups()]
+            d = set(range(r[0], r[1] + 1))
+            if d & (set(range(r[2], r[3] + 1)) | set(range(r[4], r[5] + 1))):
+                mf.setdefault(cur, []).append(line.strip())
+    return ({k: v for k, v in pk.items() if k in has_mfma}, mf,
+            {k: v for k, v in pk.items() if k not in has_mfma})
+
+
+def check(files):
+    with tempfile.TemporaryDirectory() as tmp, cf.ThreadPoolExecutor(max_workers=8) as ex:
+        asms = list(ex.map(lambda f: assemble(f, tmp), files))
+        return {os.path.basename(f): scan(a) for f, a in zip(files, asms)}
+
+
+if __name__ == "__main__":
+    files = sys.argv[1:] or sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
+    res = check(files)
+    npk = 0
+    for f, (pk, mf, quiet) in res.items():
+        for k, v in pk.items():
+            npk += len(v)
+            print(f"{f}: {k[:70]}: {len(v)} packed-FP32 op_sel reads beside MFMAs, e.g. {v[0]}")
+        for k, v in quiet.items():
+            print(f"{f}: {k[:70]}: {len(v)} packed-FP32 op_sel reads, no MFMA in the kernel (informational)")
+        for k, v in mf.items():
+            print(f"{f}: {k[:70]}: {len(v)} MFMA dst/src overlaps (informational)")
+    print("packed-FP32 op_sel reads in kernels with MFMAs:", npk)
+    sys.exit(1 if npk else 0)

@@ -19,15 +19,15 @@ def pick(d, prefix):
 
 note = "HBM bytes per launch: 2 x FETCH_SIZE + WRITE_SIZE (KB x 1024), rocprofv3 --pmc, gfx950; source: {}"
 out = {}
-m = json.load(open(os.path.join(P, "r02_pmc_mat32_e.json")))
+m = json.load(open(os.path.join(P, "r02_pmc_mat32_f.json")))
 out["materialised_bf16_32_L4_r4_n1"] = {
     "build_hbm_bytes_per_launch": hbm(pick(m, "k_build_bf16_2b")),
     "lookup_hbm_bytes_per_launch": hbm(pick(m, "k_lookup_tile")),
-    "note": note.format("profiles/r02_pmc_mat32_e.json (DVC_BRICKED level 0)")}
-mp = json.load(open(os.path.join(P, "r02_pmc_mat32_convc1_e.json")))
+    "note": note.format("profiles/r02_pmc_mat32_f.json (DVC_BRICKED level 0)")}
+mp = json.load(open(os.path.join(P, "r02_pmc_mat32_convc1_f.json")))
 out["materialised_bf16_32_L4_r4_n1_convc1_fused"] = {
     "lookup_hbm_bytes_per_launch": hbm(pick(mp, "k_lookup_tile")),
-    "note": note.format("profiles/r02_pmc_mat32_convc1_e.json (k_lookup_tile<PROJ>, DVC_BRICKED level 0)")}
+    "note": note.format("profiles/r02_pmc_mat32_convc1_f.json (k_lookup_tile<PROJ>, DVC_BRICKED level 0)")}
 f = json.load(open(os.path.join(P, "r02_pmc_fused128.json")))
 out["fused_bf16_128_L2_r4_n1"] = {
     "lookup_hbm_bytes_per_launch": hbm(pick(f, "k_fused_box")),
