@@ -3,7 +3,6 @@ reads the high element of a VGPR source.  On gfx950 such ops returned wrong low-
 now and then while another wave of the workgroup ran MFMAs (k_fused_proj, round 2; tools/isa_check.py,
 splat2 in csrc/common.h)."""
 import os
-import shutil
 import sys
 
 import pytest
@@ -11,15 +10,21 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
-pytestmark = pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc") and shutil.which("hipcc") is None,
-                                reason="hipcc not available")
+LIB = os.path.join(ROOT, "raft-dvc_amd", "dvccorr", "libdvccorr.so")
+pytestmark = pytest.mark.skipif(not os.path.exists("/opt/rocm/llvm/bin/llvm-objdump") or not os.path.exists(LIB),
+                                reason="llvm tools or the built library not available")
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(300)
 def test_no_packed_fp32_opsel_beside_mfma():
+    """Disassembles the shipped library's gfx950 code objects (seconds)."""
     import isa_check
-    csrc = isa_check.CSRC
-    files = sorted(os.path.join(csrc, f) for f in os.listdir(csrc) if f.endswith(".hip"))
-    res = isa_check.check(files)
-    bad = {f"{f}:{k}": v[0] for f, (pk, _mf, _q) in res.items() for k, v in pk.items()}
+    res = isa_check.check_library(LIB)
+    mfma_kernels = set().union(*(v[3] for v in res.values()))
+    # the disassembly covers the kernels that matter, and the pattern is recognised in objdump syntax
+    # (the MFMA-free fp32 backward kernels keep such ops and are listed for information)
+    assert any("k_fused_proj" in k for k in mfma_kernels)
+    assert any("k_lookup_tile" in k for k in mfma_kernels)
+    assert any(v[2] for v in res.values())
+    bad = {f"{b}:{k}": v[0] for b, (pk, _mf, _q, _m) in res.items() for k, v in pk.items()}
     assert not bad, bad

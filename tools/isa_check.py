@@ -7,7 +7,10 @@
     by splat2() 0 of 220 poisoned runs differ, against ~4 % before);
   * MFMAs whose destination overlaps their own A or B source registers (reported, not fatal).
 
-    python tools/isa_check.py [file.hip ...]      exit status 1 if such an op_sel read is found"""
+    python tools/isa_check.py                 the shipped dvccorr/libdvccorr.so (seconds: its gfx950 code
+                                              objects are unbundled and disassembled)
+    python tools/isa_check.py file.hip ...    recompile those sources to assembly instead
+    exit status 1 if such an op_sel read is found"""
 import concurrent.futures as cf
 import os
 import re
@@ -42,17 +45,46 @@ def assemble(src, tmp):
 def vgpr_opsel(line, bits):
     """True if a source whose op_sel bit is set is a VGPR pair (SGPR-pair broadcasts, e.g. the scale
     factor of the k_build_bf16 epilogues, are uniform operands and have run bit-exact in every test)."""
-    ops = [o.strip() for o in line.split(None, 1)[1].split(" op_sel")[0].split(",")]
+    ops = [o.strip() for o in line.split("//")[0].split(None, 1)[1].split(" op_sel")[0].split(",")]
     srcs = ops[1:]   # ops[0] is the destination
     return any(b == "1" and i < len(srcs) and srcs[i].startswith("v") for i, b in enumerate(bits.split(",")))
 
 
+LLVM = "/opt/rocm/llvm/bin"
+LIB = os.path.join(ROOT, "raft-dvc_amd", "dvccorr", "libdvccorr.so")
+
+
+def disassemble_library(lib, tmp):
+    """One disassembly file per offload bundle of the library's .hip_fatbin (one bundle per source)."""
+    fb = os.path.join(tmp, "fatbin")
+    subprocess.run([LLVM + "/llvm-objcopy", "--dump-section", ".hip_fatbin=" + fb, lib, os.path.join(tmp, "lib.copy")],
+                   check=True)
+    data = open(fb, "rb").read()
+    offs = [m.start() for m in re.finditer(b"__CLANG_OFFLOAD_BUNDLE__", data)] + [len(data)]
+    outs = []
+    for i in range(len(offs) - 1):
+        b, co, dis = (os.path.join(tmp, f"b{i}.{x}") for x in ("bin", "co", "s"))
+        open(b, "wb").write(data[offs[i]:offs[i + 1]])
+        subprocess.run([LLVM + "/clang-offload-bundler", "--unbundle", "--type=o", "--input=" + b,
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--output=" + co], check=True)
+        with open(dis, "w") as f:
+            subprocess.run([LLVM + "/llvm-objdump", "-d", "--mcpu=gfx950", co], check=True, stdout=f)
+        outs.append(dis)
+    return outs
+
+
+def check_library(lib=LIB):
+    with tempfile.TemporaryDirectory() as tmp:
+        return {f"bundle{i}": scan(d) for i, d in enumerate(disassemble_library(lib, tmp))}
+
+
 def scan(asm):
-    """(op_sel reads in kernels that also run MFMAs, MFMA overlaps, op_sel reads in MFMA-free kernels)"""
+    """(op_sel reads in kernels that also run MFMAs, MFMA overlaps, op_sel reads in MFMA-free kernels,
+    names of the kernels that run MFMAs)"""
     pk, mf, has_mfma = {}, {}, set()
     cur = None
     for line in open(asm):
-        m = re.match(r'^(_Z\S+):', line)
+        m = re.match(r'^(_Z\S+):', line) or re.match(r'^[0-9a-f]+ <(_Z\S+)>:', line)
         if m:
             cur = m.group(1)
             continue
@@ -68,7 +100,7 @@ def scan(asm):
             if d & (set(range(r[2], r[3] + 1)) | set(range(r[4], r[5] + 1))):
                 mf.setdefault(cur, []).append(line.strip())
     return ({k: v for k, v in pk.items() if k in has_mfma}, mf,
-            {k: v for k, v in pk.items() if k not in has_mfma})
+            {k: v for k, v in pk.items() if k not in has_mfma}, has_mfma)
 
 
 def check(files):
@@ -78,10 +110,9 @@ def check(files):
 
 
 if __name__ == "__main__":
-    files = sys.argv[1:] or sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
-    res = check(files)
+    res = check(sys.argv[1:]) if sys.argv[1:] else check_library()
     npk = 0
-    for f, (pk, mf, quiet) in res.items():
+    for f, (pk, mf, quiet, _) in res.items():
         for k, v in pk.items():
             npk += len(v)
             print(f"{f}: {k[:70]}: {len(v)} packed-FP32 op_sel reads beside MFMAs, e.g. {v[0]}")
