@@ -74,12 +74,18 @@ def parse(argv=None):
                     help="each lookup also applies MotionEncoder.convc1 + ReLU: fused into the lookup "
                          "(dvc_corr_lookup_proj) or unfused (lookup, then torch conv3d + relu on the GPU)")
     ap.add_argument("--gather-output", action="store_true", help="strong scaling: all-gather every lookup output")
-    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm); gloo only for rehearsals")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm); gloo only with --rehearsal")
+    ap.add_argument("--rehearsal", action="store_true",
+                    help="allow a non-RCCL backend (gloo) for N>1: a rehearsal of the call sites on one device, "
+                         "labelled as such; its numbers are not RCCL numbers")
     ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
                     help="N>1: strong = one pair's query voxels sharded by H slabs (default); weak = one volume "
                          "pair per rank (global batch N)")
-    ap.add_argument("--no-overlap", dest="overlap", action="store_false", default=True,
-                    help="N>1 strong: do not overlap the next step's fmap2 all-gather with this step's compute")
+    ap.add_argument("--overlap", dest="overlap", action="store_true", default=False,
+                    help="N>1 strong: overlap the next step's fmap2 all-gather with this step's compute in the "
+                         "headline (default: the collective on the critical path; the overlapped figure is "
+                         "reported in scaling_detail)")
+    ap.add_argument("--no-overlap", dest="overlap", action="store_false")
     ap.add_argument("--graph", dest="graph", action="store_true", default=True,
                     help="replay each rank's post-collective step as a HIP graph (default)")
     ap.add_argument("--no-graph", dest="graph", action="store_false")
@@ -368,6 +374,9 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     dist = world > 1
+    if dist and args.dist_backend != "nccl" and not args.rehearsal:
+        raise SystemExit(f"bench.py: --dist-backend {args.dist_backend} is a rehearsal backend; pass --rehearsal "
+                         f"to run it (the line is then labelled as a rehearsal, not RCCL)")
     if os.environ.get("DVCCORR_BENCH_ONE_DEVICE") == "1":   # rehearsal of N ranks on a 1-GPU box
         local = 0
     torch.cuda.set_device(local)
@@ -493,14 +502,33 @@ def main():
                 roof.update({"bound": "mfma", "achieved": roof["mfma"]["achieved"], "peak": peak,
                              "unit": "TFLOP/s", "frac": roof["mfma"]["frac"], "traffic": None, "hbm": hbm})
     else:
-        achieved = bd_bytes / (bd_avg * 1e-3) / 1e9
-        roof = {"kernel": "build (pack + k_build_bf16/f32)", "bound": "hbm", "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "algorithmic_bytes_per_launch": bd_bytes, "avg_launch_ms": round(bd_avg, 4),
-                "lookup": {"achieved": round(lk_roof, 1), "frac": round(lk_roof / HBM_PEAK_GBS, 4),
-                           "algorithmic_bytes_per_launch": lk_bytes, "avg_launch_ms": round(lk_avg, 4)}}
+        # the bf16 build (C = 128) is HBM-write-bound (~112 FLOP/B < ridge ~312); the exact-f32
+        # build is bound by the f32 matrix cores (~56 FLOP/B > ridge ~20): report each against its own roof
+        gbs = bd_bytes / (bd_avg * 1e-3) / 1e9
+        tfs = bd_flops / (bd_avg * 1e-3) / 1e12
+        lk = {"achieved": round(lk_roof, 1), "frac": round(lk_roof / HBM_PEAK_GBS, 4),
+              "algorithmic_bytes_per_launch": lk_bytes, "avg_launch_ms": round(lk_avg, 4)}
+        if args.precision == "fp32":
+            roof = {"kernel": "build (pack + k_build_f32, exact-f32 MFMA v_mfma_f32_32x32x2_f32)", "bound": "mfma",
+                    "achieved": round(tfs, 1), "peak": F32_PEAK_TFS, "unit": "TFLOP/s",
+                    "frac": round(tfs / F32_PEAK_TFS, 4), "traffic": None, "flops_per_launch": bd_flops,
+                    "avg_launch_ms": round(bd_avg, 4),
+                    "hbm": {"achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                            "algorithmic_bytes_per_launch": bd_bytes},
+                    "lookup": lk}
+        else:
+            roof = {"kernel": "build (pack + k_build_bf16_2b)", "bound": "hbm", "achieved": round(gbs, 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                    "algorithmic_bytes_per_launch": bd_bytes, "avg_launch_ms": round(bd_avg, 4),
+                    "mfma": {"achieved": round(tfs, 1), "peak": BF16_PEAK_TFS,
+                             "frac": round(tfs / BF16_PEAK_TFS, 4), "flops_per_launch": bd_flops},
+                    "lookup": lk}
     build_info = {"avg_ms": round(bd_avg, 4), "GB/s": round(bd_bytes / (bd_avg * 1e-3) / 1e9, 1) if bd_avg else None,
                   "TFLOP/s": round(bd_flops / (bd_avg * 1e-3) / 1e12, 1) if bd_avg and bd_flops else None}
+    if bd_avg and bd_flops:   # each build against its binding roof
+        build_info["roof"] = ("f32 mfma" if args.precision == "fp32" else "hbm write")
+        build_info["frac"] = round(bd_flops / (bd_avg * 1e-3) / 1e12 / F32_PEAK_TFS, 4) if args.precision == "fp32" \
+            else round(bd_bytes / (bd_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
 
     tail = flow_tail(args, coords_slab, S, B, dev, stream, _lib, dvccorr)
     bwd = backward_timing(args, f1_slab, f2_slab, coords_slab, dims, dev, stream) \
@@ -515,7 +543,8 @@ def main():
         cpu = cpu_baseline(args, f1, f2, coords_list)
 
     if rank == 0:
-        par = (f"query-voxel H-slabs x{world}, RCCL all-gather of fmap2 per step" if (strong and dist) else
+        coll = "RCCL" if args.dist_backend == "nccl" else f"{args.dist_backend} (REHEARSAL, not RCCL)"
+        par = (f"query-voxel H-slabs x{world}, {coll} all-gather of fmap2 per step" if (strong and dist) else
                f"one volume pair per rank x{world} (no data-path collective)" if dist else "single GPU")
         if shard_diag:
             par = f"diagnostic: rank {args.shard_rank}'s slab of a {args.shard_of}-way split alone (no collective)"
@@ -635,14 +664,16 @@ def scaling_detail(args, f1, f2, coords_list, ms_strong, world, rank, dev, dist,
     torch.cuda.empty_cache()
     out["cfg3_t1_ms"] = round(t1, 4)
     out["cfg3_strong_resident"] = {"ms_per_step": round(ms_strong, 4), "E": round(t1 / (world * ms_strong), 4)}
-    if args.overlap:   # the same layout with the collective on the critical path
-        h0, h1 = slab_bounds(S, world, rank)
-        rs = Runner(f1[:, :, h0:h1].contiguous().to(dev), f2[:, :, h0:h1].contiguous().to(dev),
-                    [c[:, :, h0:h1].contiguous().to(dev) for c in coords_list], S, args, group, world,
-                    graph=args.graph, proj=proj, overlap=False)
-        ts = timed(rs, steps, warm, dist, dev) * 1e3 / steps
-        rs.release()
-        out["cfg3_strong_resident_serial_collective"] = {"ms_per_step": round(ts, 4), "E": round(t1 / (world * ts), 4)}
+    # the same layout with the other collective placement than the headline's: serial (collective on the
+    # critical path, the headline default) <-> overlapped (next step's all-gather under this step's compute)
+    h0, h1 = slab_bounds(S, world, rank)
+    rs = Runner(f1[:, :, h0:h1].contiguous().to(dev), f2[:, :, h0:h1].contiguous().to(dev),
+                [c[:, :, h0:h1].contiguous().to(dev) for c in coords_list], S, args, group, world,
+                graph=args.graph, proj=proj, overlap=not args.overlap)
+    ts = timed(rs, steps, warm, dist, dev) * 1e3 / steps
+    rs.release()
+    key = "cfg3_strong_resident_serial_collective" if args.overlap else "cfg3_strong_resident_overlapped_collective"
+    out[key] = {"ms_per_step": round(ts, 4), "E": round(t1 / (world * ts), 4)}
     h0, h1 = slab_bounds(S, world, rank)
     f1s, f2s = f1[:, :, h0:h1].contiguous().to(dev), f2[:, :, h0:h1].contiguous().to(dev)
     cs = [c[:, :, h0:h1].contiguous().to(dev) for c in coords_list]

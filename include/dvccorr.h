@@ -82,7 +82,12 @@ typedef enum { DVC_F32 = 0, DVC_BF16 = 1 } dvc_dtype;
  * instead of 2 columns x 32 z -- fewer HBM lines per query (the lookup is bound by its bytes).
  * Only the tile lookup kernels read it: radius 1..6, no legacy W != D bricked level, and
  * num_levels <= 4 for the pack; other uses return DVC_ERR_UNSUPPORTED (dvc_corr_pool, the
- * on-the-fly and backward paths and dvc_corr_build take the plain dtype). */
+ * on-the-fly and backward paths and dvc_corr_build take the plain dtype).
+ * A bricked buffer carries no tag of its own: the CALLER keeps track of it and passes it, with the
+ * DVC_BRICKED flag, only to dvc_corr_lookup / dvc_corr_lookup_proj.  Passed with the plain dtype to
+ * any entry point (dvc_corr_lookup_fused, dvc_corr_backward, dvc_corr_pool, a walk lookup) it would
+ * be read as the linear layout -- wrong values, no error.  (dvccorr's Python layer records the flag
+ * next to every packed buffer and checks it, dvccorr/ops.py.) */
 #define DVC_BRICKED 0x100
 
 /* corr_sampler_version 2 = fixed, 1 = legacy W<->D swap (raft_dvc.py:71-77, corr.py:49-52). */
@@ -156,7 +161,8 @@ int dvc_corr_lookup_fused(const void *packed_q, const void *packed_t, const floa
  *   grad_fmap2 (B, C, H, W, D) float32       overwritten (these Nq queries' contribution)
  * packed_q / packed_t are the forward's packed operands (dtype).  No atomics: every
  * sum runs in a fixed order, so results are bitwise reproducible.  Supported:
- * radius 1..6, c_pad <= 128, Nq a multiple of W*D (DVC_ERR_UNSUPPORTED otherwise);
+ * radius 1..6, any C (the gradient sums run per 128-channel group), Nq a multiple of W*D
+ * (DVC_ERR_UNSUPPORTED otherwise);
  * both conventions on every level shape (legacy levels with W != D use a stretched
  * window box).  The workspace size covers either convention. */
 size_t dvc_corr_backward_workspace_bytes(int B, int64_t Nq, int C, int H, int W, int D, int num_levels, int radius);

@@ -54,6 +54,7 @@ struct BwdArgs {
     int nwh[DVC_MAX_LEVELS], nwu[DVC_MAX_LEVELS], nwv[DVC_MAX_LEVELS];   // window box per level (2r+2 each if not generic)
     long long off[DVC_MAX_LEVELS], goff[DVC_MAX_LEVELS];
     float scale;
+    int cbase;   // first channel of this launch's 128-channel group (C_pad > 128: one launch per group)
 };
 
 __device__ __forceinline__ long long bw_nw3(const BwdArgs &A, int l) {
@@ -347,7 +348,7 @@ __global__ __launch_bounds__(256) void k_grad_q(const TT *__restrict__ Tt, float
     const long long q = active ? ((long long)qy * A.Wq + qx) * A.Dq + qz : 0;
     float cy = 0.0f, cx = 0.0f, cz = 0.0f;
     if (active) load_coords(A.coords, b, A.Nq, q, cy, cx, cz);
-    const int c0 = 2 * lane;
+    const int c0 = A.cbase + 2 * lane;
     const bool cok = c0 < A.Cp;
     f32x2 acc[64];
 #pragma unroll
@@ -421,8 +422,9 @@ __global__ __launch_bounds__(256) void k_transpose_targets(const bf16_t *__restr
     __shared__ __attribute__((aligned(16))) bf16_t tile[64][128 + 8];
     const int b = blockIdx.y;
     const long long r0 = (long long)blockIdx.x * 64;
-    const int nch = Cp / 8;
-    const bf16_t *src = Tt + (long long)b * rows * Cp;
+    const int cb = 128 * (int)blockIdx.z, cg = min(128, Cp - cb);   // this block's channel group
+    const int nch = cg / 8;
+    const bf16_t *src = Tt + (long long)b * rows * Cp + cb;
     for (int id = threadIdx.x; id < 64 * nch; id += 256) {
         const int r = id / nch, ch = id - r * nch;
         u32x4 v = {0u, 0u, 0u, 0u};
@@ -430,8 +432,8 @@ __global__ __launch_bounds__(256) void k_transpose_targets(const bf16_t *__restr
         *reinterpret_cast<u32x4 *>(&tile[r][ch * 8]) = v;
     }
     __syncthreads();
-    bf16_t *dst = Ttr + (long long)b * Cp * rows_pad;
-    for (int id = threadIdx.x; id < Cp * 32; id += 256) {
+    bf16_t *dst = Ttr + ((long long)b * Cp + cb) * rows_pad;
+    for (int id = threadIdx.x; id < cg * 32; id += 256) {
         const int c = id >> 5, rp = id & 31;
         if (r0 + 2 * rp < rows_pad) {
             const unsigned lo = tile[2 * rp][c], hi = tile[2 * rp + 1][c];
@@ -467,7 +469,7 @@ __global__ __launch_bounds__(256) void k_grad_q_mfma(const bf16_t *__restrict__ 
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[T][ct][i] = 0.0f;
     const int BIG = 1 << 29;
-    const bf16_t *tb = Ttr + (long long)b * A.Cp * rows_pad;
+    const bf16_t *tb = Ttr + ((long long)b * A.Cp + A.cbase) * rows_pad;   // this launch's channel group
     for (int l = 0; l < A.L; ++l) {
         if (A.zero[l]) continue;
         const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
@@ -577,7 +579,7 @@ __global__ __launch_bounds__(256) void k_grad_q_mfma(const bf16_t *__restrict__ 
             const int qi = 32 * T + 8 * (i >> 2) + 4 * h + (i & 3);
             const int y = by * 4 + (qi >> 4), x = bx * 4 + ((qi >> 2) & 3), z = bz * 4 + (qi & 3);
             if (y < A.Hq && x < A.Wq && z < A.Dq) {
-                float *dst = dQ + ((long long)b * A.Nq + ((long long)y * A.Wq + x) * A.Dq + z) * A.Cp + m;
+                float *dst = dQ + ((long long)b * A.Nq + ((long long)y * A.Wq + x) * A.Dq + z) * A.Cp + A.cbase + m;
 #pragma unroll
                 for (int ct = 0; ct < NCT; ++ct) dst[32 * ct] = acc[T][ct][i] * A.scale;
             }
@@ -657,7 +659,7 @@ __global__ __launch_bounds__(256) void k_grad_t(const TT *__restrict__ Qp, const
     const int ox0 = bx * 4, ox1 = min(bx * 4 + 3, Wl - 1) + nu - 1;
     const int oz0 = bz * 4, oz1 = min(bz * 4 + 3, Dl - 1) + nv - 1;
     const int nox = ox1 - ox0 + 1, nrows = (oy1 - oy0 + 1) * nox;
-    const int c0 = 2 * lane;
+    const int c0 = A.cbase + 2 * lane;
     const bool cok = c0 < A.Cp;
     const float *gl = A.gwin + A.goff[l] + (long long)b * A.Nq * nw3;
     const TT *qb = Qp + (long long)b * A.Nq * A.Cp + c0;
@@ -747,21 +749,22 @@ __global__ __launch_bounds__(256) void k_qt_sorted(const bf16_t *__restrict__ Q,
                                                    int b) {
     __shared__ __attribute__((aligned(16))) bf16_t tile[64][128 + 8];
     const long long i0 = (long long)blockIdx.x * 64;
-    const int nch = Cp / 8;
+    const int cb = 128 * (int)blockIdx.y, cg = min(128, Cp - cb);   // this block's channel group
+    const int nch = cg / 8;
     for (int id = threadIdx.x; id < 64 * nch; id += 256) {
         const int r = id / nch, ch = id - r * nch;
         u32x4 v = {0u, 0u, 0u, 0u};
         if (i0 + r < Nq) {
             const long long q = (long long)(keys[i0 + r] & 0xffffffffull);
-            v = *reinterpret_cast<const u32x4 *>(Q + ((long long)b * Nq + q) * Cp + ch * 8);
+            v = *reinterpret_cast<const u32x4 *>(Q + ((long long)b * Nq + q) * Cp + cb + ch * 8);
         }
         *reinterpret_cast<u32x4 *>(&tile[r][ch * 8]) = v;
     }
     __syncthreads();
-    for (int id = threadIdx.x; id < Cp * 32; id += 256) {
+    for (int id = threadIdx.x; id < cg * 32; id += 256) {
         const int c = id >> 5, qp = id & 31;
         const unsigned lo = tile[2 * qp][c], hi = tile[2 * qp + 1][c];
-        *reinterpret_cast<unsigned *>(Qt + (long long)c * NqPad + i0 + 2 * qp) = lo | (hi << 16);
+        *reinterpret_cast<unsigned *>(Qt + (long long)(cb + c) * NqPad + i0 + 2 * qp) = lo | (hi << 16);
     }
 }
 
@@ -829,7 +832,7 @@ __global__ __launch_bounds__(256) void k_grad_t_mfma(const bf16_t *__restrict__ 
                 bf16x8 qb[NCT];
 #pragma unroll
                 for (int ct = 0; ct < NCT; ++ct) {
-                    const bf16_t *src = Qt + (long long)(32 * ct + m) * NqPad + base + k0;
+                    const bf16_t *src = Qt + (long long)(A.cbase + 32 * ct + m) * NqPad + base + k0;
                     u32x4 v;
                     __builtin_memcpy(&v, src, 16);   // 2-byte aligned 16-byte load
                     qb[ct] = __builtin_bit_cast(bf16x8, v);
@@ -901,11 +904,12 @@ __global__ __launch_bounds__(256) void k_grad_t_mfma(const bf16_t *__restrict__ 
             const int ti = 32 * T + 8 * (i >> 2) + 4 * h + (i & 3);
             const int y = by * 4 + (ti >> 4), x = bx * 4 + ((ti >> 2) & 3), z = bz * 4 + (ti & 3);
             if (nsplit > 1) {
-                float *pp = dTp + (((long long)split * gridDim.x / nsplit + brick) * 64 + ti) * A.Cp + m;
+                float *pp = dTp + (((long long)split * gridDim.x / nsplit + brick) * 64 + ti) * A.Cp + A.cbase + m;
 #pragma unroll
                 for (int ct = 0; ct < NCT; ++ct) pp[32 * ct] = acc[T][ct][i];
             } else if (y < Hl && x < Wl && z < Dl) {
-                float *dst = dT + ((long long)b * A.row_stride + A.off[l] + ((long long)y * Wl + x) * Dpl + z) * A.Cp + m;
+                float *dst = dT + ((long long)b * A.row_stride + A.off[l] + ((long long)y * Wl + x) * Dpl + z) * A.Cp +
+                             A.cbase + m;
 #pragma unroll
                 for (int ct = 0; ct < NCT; ++ct) dst[32 * ct] = acc[T][ct][i] * sc;
             }
@@ -1086,6 +1090,7 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
         return true;
     };
     const long long nqb = (A.Nq + 63) / 64;
+    const int ngroups = (A.Cp + 127) / 128;   // 128-channel groups: one launch of each gradient kernel per group
     k_win_grad<R><<<(unsigned)((A.B * A.L * nqb + 3) / 4), 256, 0, s>>>(A);
     if (!launched("win_grad")) return DVC_ERR_LAUNCH;
     bool any_generic = false;
@@ -1096,16 +1101,25 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     }
     const long long boxes = (long long)A.B * ((A.Hq + 3) / 4) * ((A.Wq + 3) / 4) * ((A.Dq + 3) / 4);
     if constexpr (std::is_same<TT, bf16_t>::value) {
-        dim3 tg((unsigned)((P.rows_pad + 63) / 64), (unsigned)A.B);
+        dim3 tg((unsigned)((P.rows_pad + 63) / 64), (unsigned)A.B, (unsigned)ngroups);
         k_transpose_targets<<<tg, 256, 0, s>>>(Tt, ttr, A.row_stride, P.rows_pad, A.Cp);
         if (!launched("transpose_targets")) return DVC_ERR_LAUNCH;
-        switch (A.Cp / 32) {
-        case 1: k_grad_q_mfma<1><<<(unsigned)boxes, 256, 0, s>>>(ttr, P.rows_pad, dq, A); break;
-        case 2: k_grad_q_mfma<2><<<(unsigned)boxes, 256, 0, s>>>(ttr, P.rows_pad, dq, A); break;
-        default: k_grad_q_mfma<4><<<(unsigned)boxes, 256, 0, s>>>(ttr, P.rows_pad, dq, A); break;
+        for (int g = 0; g < ngroups; ++g) {
+            BwdArgs Ag = A;
+            Ag.cbase = 128 * g;
+            switch (std::min(128, A.Cp - Ag.cbase) / 32) {
+            case 1: k_grad_q_mfma<1><<<(unsigned)boxes, 256, 0, s>>>(ttr, P.rows_pad, dq, Ag); break;
+            case 2: k_grad_q_mfma<2><<<(unsigned)boxes, 256, 0, s>>>(ttr, P.rows_pad, dq, Ag); break;
+            case 3: k_grad_q_mfma<3><<<(unsigned)boxes, 256, 0, s>>>(ttr, P.rows_pad, dq, Ag); break;
+            default: k_grad_q_mfma<4><<<(unsigned)boxes, 256, 0, s>>>(ttr, P.rows_pad, dq, Ag); break;
+            }
         }
     } else {
-        k_grad_q<TT, R><<<(unsigned)boxes, 256, 0, s>>>(Tt, dq, A);
+        for (int g = 0; g < ngroups; ++g) {
+            BwdArgs Ag = A;
+            Ag.cbase = 128 * g;
+            k_grad_q<TT, R><<<(unsigned)boxes, 256, 0, s>>>(Tt, dq, Ag);
+        }
     }
     if (!launched("grad_q")) return DVC_ERR_LAUNCH;
     for (int b = 0; b < A.B; ++b)
@@ -1127,16 +1141,26 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
             const int sp = grad_t_splits(lay, l, P.nw[l]);
             if constexpr (std::is_same<TT, bf16_t>::value) {
                 // matrix-core path: sorted + transposed query rows, then 16-query MFMA batches
-                k_qt_sorted<<<(unsigned)(P.nq_pad / 64), 256, 0, s>>>(Q, kout, qt, A.Nq, P.nq_pad, A.Cp, b);
+                k_qt_sorted<<<dim3((unsigned)(P.nq_pad / 64), (unsigned)ngroups), 256, 0, s>>>(Q, kout, qt, A.Nq,
+                                                                                           P.nq_pad, A.Cp, b);
                 if (!launched("qt_sorted")) return DVC_ERR_LAUNCH;
                 const unsigned g = (unsigned)(bricks * sp);
-                switch (A.Cp / 32) {
-                case 1: k_grad_t_mfma<1><<<g, 256, 0, s>>>(qt, P.nq_pad, kout, starts, dt, dtp, sp, A, b, l); break;
-                case 2: k_grad_t_mfma<2><<<g, 256, 0, s>>>(qt, P.nq_pad, kout, starts, dt, dtp, sp, A, b, l); break;
-                default: k_grad_t_mfma<4><<<g, 256, 0, s>>>(qt, P.nq_pad, kout, starts, dt, dtp, sp, A, b, l); break;
+                for (int cg = 0; cg < ngroups; ++cg) {
+                    BwdArgs Ag = A;
+                    Ag.cbase = 128 * cg;
+                    switch (std::min(128, A.Cp - Ag.cbase) / 32) {
+                    case 1: k_grad_t_mfma<1><<<g, 256, 0, s>>>(qt, P.nq_pad, kout, starts, dt, dtp, sp, Ag, b, l); break;
+                    case 2: k_grad_t_mfma<2><<<g, 256, 0, s>>>(qt, P.nq_pad, kout, starts, dt, dtp, sp, Ag, b, l); break;
+                    case 3: k_grad_t_mfma<3><<<g, 256, 0, s>>>(qt, P.nq_pad, kout, starts, dt, dtp, sp, Ag, b, l); break;
+                    default: k_grad_t_mfma<4><<<g, 256, 0, s>>>(qt, P.nq_pad, kout, starts, dt, dtp, sp, Ag, b, l); break;
+                    }
                 }
             } else {
-                k_grad_t<TT, R><<<(unsigned)(bricks * sp), 256, 0, s>>>(Q, kout, starts, dt, dtp, sp, A, b, l);
+                for (int cg = 0; cg < ngroups; ++cg) {
+                    BwdArgs Ag = A;
+                    Ag.cbase = 128 * cg;
+                    k_grad_t<TT, R><<<(unsigned)(bricks * sp), 256, 0, s>>>(Q, kout, starts, dt, dtp, sp, Ag, b, l);
+                }
             }
             if (!launched("grad_t")) return DVC_ERR_LAUNCH;
             if (sp > 1) {
@@ -1177,10 +1201,6 @@ int corr_backward(const void *packed_q, const void *packed_t, const float *coord
                   size_t errlen) {
     if (radius < 1 || radius > 6) {
         snprintf(err, errlen, "corr_backward: radius %d outside [1, 6]", radius);
-        return DVC_ERR_UNSUPPORTED;
-    }
-    if (lay.c_pad > 128) {
-        snprintf(err, errlen, "corr_backward: C=%d > 128 not supported", C);
         return DVC_ERR_UNSUPPORTED;
     }
     const long long plane = (long long)lay.W[0] * lay.D[0];

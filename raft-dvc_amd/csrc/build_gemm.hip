@@ -125,6 +125,8 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict_
             bq[j][ks] = __builtin_bit_cast(bf16x8, sQ[row * nch + (c ^ (row & msk))]);
         }
 
+    // epilogue scale as a register pair (no op_sel broadcast of an SGPR pair beside MFMAs: common.h splat2)
+    const f32x2 sc2 = splat2(scale);
     // register prefetch of the next target tile: its global loads fly while the
     // current tile's MFMAs and epilogue run
     static_assert(PF == 4 || PF == 8 || PF == 16 || PF == 2, "prefetch depth");
@@ -209,11 +211,11 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict_
                     for (int g = 0; g < 4; ++g) {
                         const int q = 64 * wq + 32 * j + r32;
                         const int pch = 8 * wp + 4 * i + g;     // column chunk (8 columns)
+                        const f32x2 lo = f32x2{acc[i][j][4 * g + 0], acc[i][j][4 * g + 1]} * sc2;
+                        const f32x2 hi = f32x2{acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]} * sc2;
                         u32x2 v;
-                        v[0] = (unsigned)f32_to_bf16(acc[i][j][4 * g + 0] * scale) |
-                               ((unsigned)f32_to_bf16(acc[i][j][4 * g + 1] * scale) << 16);
-                        v[1] = (unsigned)f32_to_bf16(acc[i][j][4 * g + 2] * scale) |
-                               ((unsigned)f32_to_bf16(acc[i][j][4 * g + 3] * scale) << 16);
+                        v[0] = (unsigned)f32_to_bf16(lo[0]) | ((unsigned)f32_to_bf16(lo[1]) << 16);
+                        v[1] = (unsigned)f32_to_bf16(hi[0]) | ((unsigned)f32_to_bf16(hi[1]) << 16);
                         st[(q * 16 + (pch ^ (q & 15))) * 2 + h] = v;
                     }
             __syncthreads();
@@ -248,11 +250,10 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict_
                             for (int g = 0; g < 4; ++g) {
                                 const int q = 32 * j + r32;                 // local in this pass
                                 const int pch = 16 * wp + 8 * i + 2 * g + h;  // 4-column chunk
-                                u32x4 v;
-                                v[0] = __float_as_uint(acc[i][j][4 * g + 0] * scale);
-                                v[1] = __float_as_uint(acc[i][j][4 * g + 1] * scale);
-                                v[2] = __float_as_uint(acc[i][j][4 * g + 2] * scale);
-                                v[3] = __float_as_uint(acc[i][j][4 * g + 3] * scale);
+                                const f32x2 lo = f32x2{acc[i][j][4 * g + 0], acc[i][j][4 * g + 1]} * sc2;
+                                const f32x2 hi = f32x2{acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]} * sc2;
+                                const u32x4 v = {__float_as_uint(lo[0]), __float_as_uint(lo[1]),
+                                                 __float_as_uint(hi[0]), __float_as_uint(hi[1])};
                                 sT[q * 32 + (pch ^ (q & 31))] = v;
                             }
                 }
@@ -362,7 +363,7 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16_2b(const bf16_t *__restri
     issue(pfa, chunk + 2 * nchunk);
     const long long nrow = Nq - q0 < kBQ ? Nq - q0 : kBQ;
     u32x2 *st = reinterpret_cast<u32x2 *>(sS);
-    const f32x2 sc2 = {scale, scale};
+    const f32x2 sc2 = splat2(scale);   // materialised: no op_sel broadcast beside MFMAs (common.h)
     int soff[NSTORE];   // byte offset of this thread's store it inside the tile's rows
 #pragma unroll
     for (int it = 0; it < NSTORE; ++it) {

@@ -39,7 +39,8 @@ template <typename T>
 __global__ void k_corr_pool(T *, long long, long long, long long, int, int, long long, int, int, int, int);
 template <typename T, int R, bool WINBUF, bool ALIGNED> __global__ void k_lookup_win(LookupArgs);
 template <typename T> __global__ void k_lookup_generic(LookupArgs);
-template <typename T, int R, bool NT, int ABL, bool PROJ, int ACH, int NWV = 0> __global__ void k_lookup_tile(LookupArgs);
+template <typename T, int R, bool NT, int ABL, bool PROJ, int ACH, int NWV = 0, int SPOL = -1>
+__global__ void k_lookup_tile(LookupArgs);
 __global__ void k_proj_pack(const float *, bf16_t *, int, int, int, long long);
 __global__ void k_sample3d(const float *, const float *, float *, int, int, int, int, int, long long, int);
 int fused_lookup(const void *packed_q, const void *packed_t, const float *coords, float *out, void *workspace, int B,
@@ -160,6 +161,9 @@ static thread_local int g_split_ach = 5;          // rows per chunk of the row s
 // of 40 calls): config #3 bf16 151.8 -> 150.0 us, fp32 220.7 -> 213.9; one rank's slab of an 8 / 4 / 2-way
 // split 26.7 / 39.0 / 78.2 -> 26.2 / 38.9 / 77.4 us (bf16).
 static thread_local int g_lookup_waves = 4;
+// diagnostics: cache-policy bits of the tile kernel's output stores on the default bf16 r = 4 path
+// (-1 = the product's nontemporal stores; 0 plain, 16 sc1, 17 sc0 sc1, 18 nt sc1)
+static thread_local int g_lookup_stpol = -1;
 
 template <typename T, bool NT, int ACH>
 static void launch_tile_r(const LookupArgs &A, dim3 blocks, unsigned threads, hipStream_t s) {
@@ -198,8 +202,20 @@ static void launch_tile_nt(const LookupArgs &A0, hipStream_t s) {
     }
     if constexpr (NT) {
         if (bal) {
-            if (split_rows) k_lookup_tile<T, 4, true, 0, false, 5, 4><<<blocks, threads, 0, s>>>(A);
-            else k_lookup_tile<T, 4, true, 0, false, 0, 4><<<blocks, threads, 0, s>>>(A);
+            if (split_rows) {
+                k_lookup_tile<T, 4, true, 0, false, 5, 4><<<blocks, threads, 0, s>>>(A);
+                return;
+            }
+            if constexpr (std::is_same<T, bf16_t>::value) {
+                switch (g_lookup_stpol) {   // diagnostics only
+                case 0: k_lookup_tile<T, 4, true, 0, false, 0, 4, 0><<<blocks, threads, 0, s>>>(A); return;
+                case 16: k_lookup_tile<T, 4, true, 0, false, 0, 4, 16><<<blocks, threads, 0, s>>>(A); return;
+                case 17: k_lookup_tile<T, 4, true, 0, false, 0, 4, 17><<<blocks, threads, 0, s>>>(A); return;
+                case 18: k_lookup_tile<T, 4, true, 0, false, 0, 4, 18><<<blocks, threads, 0, s>>>(A); return;
+                default: break;
+                }
+            }
+            k_lookup_tile<T, 4, true, 0, false, 0, 4><<<blocks, threads, 0, s>>>(A);
             return;
         }
         if (split_rows) {
@@ -265,6 +281,12 @@ int dvc_set_tuning(const char *key, int value) {
     if (!strcmp(key, "lookup_waves")) {
         if (value != 0 && value != 4) return fail(DVC_ERR_INVALID, "set_tuning: lookup_waves %d (0 or 4)", value);
         g_lookup_waves = value;
+        return DVC_OK;
+    }
+    if (!strcmp(key, "lookup_stpol")) {
+        if (value != -1 && value != 0 && value != 16 && value != 17 && value != 18)
+            return fail(DVC_ERR_INVALID, "set_tuning: lookup_stpol %d (-1, 0, 16, 17 or 18)", value);
+        g_lookup_stpol = value;
         return DVC_OK;
     }
     if (!strcmp(key, "split_ach")) {

@@ -29,7 +29,9 @@ struct Geo {
 // {p, p} in two registers.  A packed-FP32 op whose low lane reads the high element of a source (op_sel
 // [1, ..], the compiler's way to broadcast the high half of a pair) returned wrong low-lane values in
 // lanes 48-63 now and then while another wave of the same workgroup ran MFMAs (k_fused_proj, round 2,
-// tools/dbg_poison4.py).  The empty asm hides that the halves are equal, so no such broadcast is formed.
+// found with dump instances of the kernel; tests/test_gpu_proj_fused.py::test_repeatable_under_poisoned_memory guards it).  The empty asm hides that the
+// halves are equal, so no such broadcast is formed.  Used for every broadcast pair (VGPR or SGPR source) in a
+// kernel that issues MFMAs; tools/isa_check.py fails the build check on any that is left.
 __device__ __forceinline__ f32x2 splat2(float p) {
     f32x2 v = {p, p};
     asm volatile("" : "+v"(v));

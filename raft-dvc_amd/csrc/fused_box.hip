@@ -133,7 +133,7 @@ __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__re
     const int q4 = active ? (int)(qg * 4) : 0x7ffffff0;
     const int vstep = buni((int)(chstep_v * Nq * 4));
     const int out_bytes = buni((int)(n * n * Nq * 4));
-    const f32x2 sc2 = {scale, scale};
+    const f32x2 sc2 = splat2(scale);   // materialised: no op_sel broadcast beside MFMAs (common.h)
     const int trash = C::TRASH + lane * 4;
     unsigned sink = 0;
     const int u0 = wave * C::COLS;
@@ -355,7 +355,7 @@ __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__re
                     const int uu = k - 1;
                     const float p00 = wx0[uu] * wy0, p10 = wx1[uu] * wy0;
                     const float p01 = wx0[uu] * wy1, p11 = wx1[uu] * wy1;
-                    const f32x2 P00 = {p00, p00}, P10 = {p10, p10}, P01 = {p01, p01}, P11 = {p11, p11};
+                    const f32x2 P00 = splat2(p00), P10 = splat2(p10), P01 = splat2(p01), P11 = splat2(p11);
                     const __amdgpu_buffer_rsrc_t rs = out_rsrc(obase, a, u0 + uu);
 #pragma unroll
                     for (int i = 0; i < NP; ++i) {

@@ -143,7 +143,7 @@ __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict_
 
     const int legacy = buni(A.legacy);
     unsigned sink = 0;
-    const f32x2 sc2 = {scale, scale};
+    const f32x2 sc2 = splat2(scale);   // materialised: no op_sel broadcast beside MFMAs (common.h)
     const int trash = C::TRASH + lane * 4;
     const int u0 = wave * 3;                                   // producer: output columns u0 .. u0 + NU - 1
     const bool cons = wave >= C::CONS0;                        // consumer: output tile ot = wave - CONS0

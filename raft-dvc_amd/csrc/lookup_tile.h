@@ -1,0 +1,523 @@
+// lookup_tile.h -- radius-r trilinear lookup of the correlation pyramid with
+// LDS-staged windows (reference src/core/corr.py:169-208, sampler :17-68).
+//
+// Why this kernel: in the lane-per-query walk (lookup.hip) every load
+// instruction touches 64 different pyramid rows, so the address path (TA) and
+// the fabric see 64 scattered 64-byte requests per instruction and the
+// re-touched lines of small levels fall out of L2 before their next use.  Here a
+// workgroup owns a tile of 64 consecutive query rows and streams their windows
+// plane by plane through LDS with coalesced 16-byte loads:
+//
+//   * plane strip of query j at window plane wp: level plane y = ih_j + wp,
+//     window columns [cs_j, cs_j + NC) (NC = min(2r+2, W_l)), and along the
+//     contiguous D axis the 16-byte chunks [za_j, za_j + ZW) that cover the
+//     query's z-run (ZW = D_l padded when it is small, else ceil(2r+2+7) to
+//     the chunk size).  Consecutive threads load consecutive chunks, so a wave
+//     instruction reads whole runs of 48..64-byte pieces of a few rows;
+//   * planes out of range and queries past the tile's end come back as zeros
+//     from the buffer descriptor's range check (no branch, no traffic);
+//   * compute is lane = query: each wave owns 3 output columns (u) and keeps
+//     the z-lerped runs of the previous plane in registers, so one new plane
+//     per output row is read from LDS; outputs leave as coalesced 256-byte wave
+//     stores into the channel-major output, as in lookup.hip.
+//
+// The arithmetic is exactly lookup.hip's (per-axis float32 weights of the
+// reference, zero padding folded into the weights, z-lerp then the four (y, x)
+// bilinear terms in the same order), so the two kernels agree bit for bit.
+// LDS: two plane slots (one being read, one being filled from registers
+// loaded a whole output row earlier) -- 63 KB for bf16 r=4, two workgroups/CU.
+#pragma once
+
+#include "common.h"
+#include "lookup_common.h"
+
+#include <type_traits>
+
+namespace dvc {
+
+// NWV = 0: ceil(n / 3) waves of 3 output columns (the last one takes the rest); NWV > 0: NWV waves
+// with the columns dealt as evenly as possible (n = 9, NWV = 4: 3 + 2 + 2 + 2), so that two workgroups
+// put exactly two waves on each SIMD.
+template <typename T, int R, int NWV = 0> struct TileCfg {
+    static constexpr int n = 2 * R + 1;
+    static constexpr int NW = 2 * R + 2;                        // window planes / columns / run length
+    static constexpr int ES = (int)sizeof(T);
+    static constexpr int CE = 16 / ES;                          // elements per 16-byte chunk
+    static constexpr int ZWMAX = (NW + CE - 1 + CE - 1) / CE * CE;   // z-chunk span covering any run
+    static constexpr int NWAVES = NWV > 0 ? NWV : (n + 2) / 3;
+    static constexpr int COLS = NWV > 0 ? (n + NWV - 1) / NWV : 3;   // output columns of the widest wave
+    static constexpr int THREADS = 64 * NWAVES;
+    static constexpr int SQMAX = NW * ZWMAX * ES + 8;           // bytes per query strip (+8: bank spread)
+    static constexpr int SLOT = 64 * SQMAX;
+    static constexpr int GUARD = 64;                            // >= NW*ES + 4 bytes either side
+    static constexpr int MAXCH = (64 * NW * (ZWMAX / CE) + THREADS - 1) / THREADS;
+    static constexpr int LDS = GUARD + 2 * SLOT + GUARD;
+    static_assert(SLOT / 8 < 0xffff, "chunk LDS offsets are packed as 16-bit multiples of 8 bytes");
+    static_assert(SQMAX % 8 == 0, "strips must stay 8-byte aligned");
+};
+
+// One z-run of NW elements at LDS byte address `addr` (any 2-byte alignment for
+// bf16), returned as floats.
+template <int NW>
+__device__ __forceinline__ void lds_run(const unsigned char *base, int addr, const bf16_t *, float (&v)[NW]) {
+    constexpr int K = NW / 2;
+    const unsigned *p = reinterpret_cast<const unsigned *>(base + (addr & ~3));
+    unsigned d[K + 1];
+#pragma unroll
+    for (int i = 0; i <= K; ++i) d[i] = p[i];
+    const unsigned sh = (unsigned)(addr & 2);
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const unsigned w = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+        v[2 * i] = __uint_as_float(w << 16);
+        v[2 * i + 1] = __uint_as_float(w & 0xffff0000u);
+    }
+}
+
+template <int NW>
+__device__ __forceinline__ void lds_run(const unsigned char *base, int addr, const float *, float (&v)[NW]) {
+    const float *p = reinterpret_cast<const float *>(base + addr);
+#pragma unroll
+    for (int i = 0; i < NW; ++i) v[i] = p[i];
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// z-lerped run of one window column: zl[v] = fma(R[v+1], w1[v], R[v] * w0[v]), v < n,
+// kept as n/2 pairs (packed-f32 math, same per-element rounding) plus a tail.
+template <int n> struct ZRun {
+    f32x2 p[n / 2];
+    float t;
+};
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// convc1 fusion (PROJ): the motion encoder's first layer, relu(conv1x1(corr, W) + b)
+// with 96 output channels (reference src/core/update.py:219-222, 246), applied to the
+// lookup's L*(2r+1)^3 channels without writing them to HBM.
+//   * the NWAVES lookup waves (producers) write each output row a (their (2r+1) x 3
+//     values per query) as fp16 into a [64 query][NWAVES x 32 k] LDS tile X instead of
+//     storing them; within a wave's 32-k slice, k = 2 (uu NP + i) + {0, 1} holds the
+//     pair (column uu, v = 2i, 2i + 1) and k = 2 NU NP + uu the tail v = n - 1.
+//   * one extra wave (consumer) multiplies X by the row's 96 x (NWAVES x 32) weight
+//     block on v_mfma_f32_16x16x32_f16 (A = weights, 16 output channels; B = X, 16
+//     queries), accumulating D[96][64] over every row of every level in 96 VGPRs, and
+//     stores relu(D + b) once per tile.  The weights are pre-permuted into that k order
+//     and the MFMA A-operand lane layout (dvc_proj_pack), so any sampler convention is
+//     just a different permutation.
+//   * X is single-buffered: a barrier before the producers overwrite it (the consumer
+//     has read the previous row) plus the row barrier the lookup already has.
+struct ProjCfg {
+    static constexpr int COUT = 96, OT = COUT / 16, KW = 32;
+};
+
+// ABL (diagnostics only, never the product path): 1 = skip output stores, 2 = skip loads, 4 = the same
+// output bytes as 16-byte stores (a column's 9 values leave as 2 x dwordx4 + 1 dword per lane, at
+// query-major addresses -- wrong layout, a third of the store instructions).
+// ACH > 0: row split -- the workgroup computes output rows [ACH * blockIdx.z, + ACH) of its level only
+// (ACH + 1 window planes), for launches whose (tile, level) pairs alone cannot fill the chip.
+// SPOL >= 0 (diagnostics, tuning "lookup_stpol"): the output stores' cache-policy bits instead of NT's
+// (16 = sc1: the line is not kept in the XCD's L2, which the plane loads then have to themselves).
+template <typename T, int R, bool NT, int ABL, bool PROJ, int ACH, int NWV = 0, int SPOL = -1>
+__global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)), 2) void k_lookup_tile(LookupArgs A) {
+    using C = TileCfg<T, R, NWV>;
+    static_assert(!PROJ || NWV == 0, "the convc1 weight packing assumes the 3-column waves");
+    constexpr bool BAL = NWV > 0;
+    constexpr int FLO = BAL ? C::n / C::NWAVES : 0, REM = BAL ? C::n % C::NWAVES : 0;
+    constexpr int n = C::n, NW = C::NW, ES = C::ES, CE = C::CE, NP = n / 2;
+    constexpr long long n3 = (long long)n * n * n;
+    constexpr int NU_LAST = n - C::COLS * (C::NWAVES - 1);   // output columns of the last wave
+    constexpr int XROW = C::NWAVES * ProjCfg::KW * 2 + 16;    // bytes per query row of X (+16: bank spread)
+    static_assert(!PROJ || C::COLS * n <= ProjCfg::KW, "PROJ: one wave's row values must fit a 32-k slice");
+    __shared__ __attribute__((aligned(16))) unsigned char smem[C::LDS];
+    __shared__ int tab[5][64];   // per query of the tile: ih, cs, za, iv, iu (element units)
+    __shared__ __attribute__((aligned(16))) unsigned char xs[PROJ ? 64 * XROW : 16];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int b = blockIdx.x / (int)A.nqb;
+    const long long qb = blockIdx.x - (long long)b * A.nqb;
+    const long long qt = qb * 64;                     // first query of the tile, relative to A.q0
+    const int nvalid = (int)min(64LL, A.nq - qt);     // valid queries in the tile
+    const long long q = A.q0 + qt + lane;
+    const bool active = lane < nvalid;
+    const long long Nq = A.Nq;
+    const bool rev = A.order && !A.split_levels && (blockIdx.x & 1);   // level order (see the level loop)
+
+    if constexpr (PROJ) {
+        if (wave == C::NWAVES) {   // the convc1 consumer wave
+            constexpr int OT = ProjCfg::OT, NWP = C::NWAVES;
+            const int m16 = lane & 15, h4 = lane >> 4;
+            f32x4 acc[OT][4];   // acc[ot][j][i] = D[o = 16 ot + 4 h4 + i][query 16 j + m16]
+#pragma unroll
+            for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[ot][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            const f16x8 *wp = reinterpret_cast<const f16x8 *>(A.proj_w) + lane;
+            for (int li = 0; li < A.nl; ++li) {
+                const int l = A.l0 + (rev ? A.nl - 1 - li : li);
+                if (A.zero[l] || A.generic[l]) continue;   // (the producers skip the same levels)
+                __syncthreads();
+                __syncthreads();   // level preamble: window table
+                __syncthreads();
+                __syncthreads();   // planes 0 and 1 staged
+                for (int a = 0; a < n; ++a) {
+                    // this row's weight block, [wave slice ks][16-channel tile ot][lane] x 8 fp16
+                    const f16x8 *wr = wp + (long long)(l * n + a) * NWP * OT * 64;
+                    f16x8 wa[NWP][OT];
+#pragma unroll
+                    for (int ks = 0; ks < NWP; ++ks)
+#pragma unroll
+                        for (int ot = 0; ot < OT; ++ot) wa[ks][ot] = wr[(ks * OT + ot) * 64];
+                    __syncthreads();   // the producers may overwrite X: row a-1 has been read
+                    __syncthreads();   // row a complete in X
+#pragma unroll
+                    for (int ks = 0; ks < NWP; ++ks) {
+                        f16x8 xb[4];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            xb[j] = *reinterpret_cast<const f16x8 *>(xs + (16 * j + m16) * XROW + ks * 64 + h4 * 16);
+#pragma unroll
+                        for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+                            for (int j = 0; j < 4; ++j)
+                                acc[ot][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[ks][ot], xb[j], acc[ot][j], 0,
+                                                                                     0, 0);
+                    }
+                }
+            }
+            // relu(D + b) -> out (B, 96, Nq); a wave store covers 16 consecutive queries of 4 channels
+            float *ob = A.proj_out + (long long)b * ProjCfg::COUT * Nq + A.q0 + qt;
+#pragma unroll
+            for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int o = 16 * ot + 4 * h4 + i;
+                    const float bo = A.proj_b[o];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int qq = 16 * j + m16;
+                        const float v = acc[ot][j][i] + bo;
+                        if (qq < nvalid) ob[(long long)o * Nq + qq] = v < 0.f ? 0.f : v;   // relu (NaN kept)
+                    }
+                }
+            return;
+        }
+    }
+
+    // zero the LDS once: guards and strip padding are read (with zero weight) and must be finite
+    for (int i = tid * 16; i < C::LDS; i += C::THREADS * 16) *reinterpret_cast<u32x4 *>(smem + i) = u32x4{0, 0, 0, 0};
+
+    float cy = 0.f, cx = 0.f, cz = 0.f;
+    if (active) load_coords(A.coords, b, Nq, q, cy, cx, cz);
+
+    // the tile's rows as one buffer: offsets past its valid rows (or negative) read 0
+    const T *tile_rows = reinterpret_cast<const T *>(A.corr) + ((long long)b * Nq + A.q0 + qt) * A.row_stride;
+    // (readfirstlane: keep the descriptor in SGPRs, no waterfall loops around the loads)
+    const unsigned long long trp = (unsigned long long)tile_rows;
+    const unsigned trlo = __builtin_amdgcn_readfirstlane((unsigned)trp);
+    const unsigned trhi = __builtin_amdgcn_readfirstlane((unsigned)(trp >> 32));
+    const int nrec = __builtin_amdgcn_readfirstlane((int)((long long)nvalid * A.row_stride * ES));
+    const __amdgpu_buffer_rsrc_t rs_in = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(((unsigned long long)trhi << 32) | trlo), (short)0, nrec, 0x00020000);
+    // output lane offset; lanes past the tile's end store out of the descriptor's range (dropped)
+    const int q4 = active ? (int)(q * 4) : 0x7ffffff0;
+    const int chstep_u = A.legacy ? 1 : n;       // output-channel step per U (W-axis) offset
+    const int chstep_v = A.legacy ? n : 1;       // ... per V (D-axis) offset
+    const int u0 = BAL ? wave * FLO + min(wave, REM) : wave * C::COLS;   // this wave's columns u0 .. u0 + NU - 1
+    const int ldpol = A.ldpol;
+
+    // store of output (row a, column u, offset v) of this lane's query
+    auto out_rsrc = [&](float *obase, int a, int u) {
+        return __builtin_amdgcn_make_buffer_rsrc(obase + ((long long)a * n * n + (long long)u * chstep_u) * Nq,
+                                                 (short)0, (int)(n * n * Nq * 4), 0x00020000);
+    };
+    auto store = [&](__amdgpu_buffer_rsrc_t rs, int v, float val) {
+        if constexpr ((ABL & 1) != 0) asm volatile("" ::"v"(val));
+        else __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val), rs, q4, (int)(v * chstep_v * Nq * 4),
+                                                   SPOL >= 0 ? SPOL : (NT ? 2 : 0));
+    };
+
+    static_assert(!PROJ || ACH == 0, "the convc1 consumer accumulates every row of the tile");
+    // output rows [a0, a0 + NA) of level l; planes a0 .. a0 + NA of the window
+    auto level = [&](int l, auto nu_c, auto na_c, int a0) {
+        constexpr int NU = decltype(nu_c)::value;
+        constexpr int NA = decltype(na_c)::value;
+        float *obase = A.out + ((long long)b * A.Ltot + l) * n3 * Nq;   // wave-uniform
+        if (A.zero[l]) {
+            if constexpr (PROJ) return;   // zero outputs add nothing to convc1
+            for (int a = a0; a < a0 + NA; ++a)
+#pragma unroll
+                for (int uu = 0; uu < NU; ++uu) {
+                    const __amdgpu_buffer_rsrc_t rs = out_rsrc(obase, a, u0 + uu);
+#pragma unroll
+                    for (int v = 0; v < n; ++v) store(rs, v, 0.0f);
+                }
+            return;
+        }
+        const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
+        const float sc = (float)(1 << l);
+        WinAxes ax;
+        window_axes(cy / sc, cx / sc, cz / sc, Hl, Wl, Dl, A.legacy, ax);
+        // (a NaN / huge coordinate moves the window far outside the level: every
+        //  weight below is then folded to 0 and the output is 0, as the reference's)
+        const int ih = (int)ax.kh - R, iu = (int)ax.ku - R, iv = (int)ax.kv - R;
+        const int NC = min(NW, Wl);
+        const int ZW = min(Dpl, C::ZWMAX);
+        const int cs = min(max(iu, 0), Wl - NC);
+        const int za = min(max(iv & ~(CE - 1), 0), Dpl - ZW);
+        const int SQ = NC * ZW * ES + 8;
+        const int ZC = ZW / CE;                          // chunks per column
+        const int nch = 64 * NC * ZC;                    // chunks per plane slot
+        const int plane_bytes = Wl * Dpl * ES;
+
+        // per-axis weights (reference float32 arithmetic), zero padding folded in
+        float wv0[n], wv1[n];
+#pragma unroll
+        for (int t = 0; t < n; ++t) {
+            axis_weights(ax.pv, ax.kv, t - R, ax.vn, ax.vu, wv0[t], wv1[t]);
+            wv0[t] = (unsigned)(iv + t) < (unsigned)Dl ? wv0[t] : 0.0f;
+            wv1[t] = (unsigned)(iv + t + 1) < (unsigned)Dl ? wv1[t] : 0.0f;
+        }
+        f32x2 w0p[NP], w1p[NP];
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+            w0p[i] = f32x2{wv0[2 * i], wv0[2 * i + 1]};
+            w1p[i] = f32x2{wv1[2 * i], wv1[2 * i + 1]};
+        }
+        float wx0[NU], wx1[NU];
+#pragma unroll
+        for (int uu = 0; uu < NU; ++uu) {
+            const int u = u0 + uu;
+            axis_weights(ax.pu, ax.ku, u - R, ax.un, ax.uu, wx0[uu], wx1[uu]);
+            wx0[uu] = (unsigned)(iu + u) < (unsigned)Wl ? wx0[uu] : 0.0f;
+            wx1[uu] = (unsigned)(iu + u + 1) < (unsigned)Wl ? wx1[uu] : 0.0f;
+        }
+        // LDS read offsets (bytes, relative to a slot) of this lane's window columns
+        const int rz = min(max(iv - za, -NW), ZW);
+        int coff[NU + 1];
+#pragma unroll
+        for (int k = 0; k <= NU; ++k) {
+            const int cl = min(max(iu + u0 + k - cs, 0), NC - 1);
+            coff[k] = lane * SQ + (cl * ZW + rz) * ES;
+        }
+
+        __syncthreads();   // previous level's LDS reads are done; table free
+        if (wave == 0) {
+            tab[0][lane] = min(max(ih, -2 * NW), Hl);
+            tab[1][lane] = cs;
+            tab[2][lane] = za;
+            tab[3][lane] = iv;
+            tab[4][lane] = iu;
+        }
+        __syncthreads();
+        // a bricked level (DVC_BRICKED, bit l of A.brick): voxel (y, x, z) at
+        // ((y * W/8 + x/8) * Dp/8 + z/8) * 64 + (x%8) * 8 + z%8, i.e. (1, 8, 8) bricks of one 128-byte
+        // line, so the strip of a window plane touches lines of 8 columns x 8 z instead of 2 x 32
+        // (Dp = 32) or 1 x 64; the strip's z-chunk that the query's run never reaches is not loaded.
+        const bool bk8 = (A.brick >> l) & 1;
+
+        // this thread's chunks of every plane: (query j, column c, z-chunk k).  voff =
+        // byte offset of the chunk in window plane 0; window plane wp adds wp * plane_bytes.
+        // pk = LDS offset / 8 (low 16 bits; 0xffff: no chunk) | mask of the window planes
+        // inside the level (high 16 bits).  Planes outside it are not loaded: their LDS
+        // slots keep earlier, finite data, and their weights are 0.
+        int voff[C::MAXCH];
+        unsigned pk[C::MAXCH];
+#pragma unroll
+        for (int k = 0; k < C::MAXCH; ++k) {
+            const int idx = tid + k * C::THREADS;
+            const int j = idx / (NC * ZC);
+            const int rem = idx - j * (NC * ZC);
+            const int c = rem / ZC;
+            const int zc = rem - c * ZC;
+            const bool ok = idx < nch;
+            const int jj = ok ? j : 0;
+            const int ihj = tab[0][jj];
+            const int plo = min(max(-ihj, 0), NW), phi = min(max(Hl - ihj, 0), NW);
+            unsigned mask = ok && jj < nvalid ? ((1u << phi) - 1u) & ~((1u << plo) - 1u) : 0u;
+            // only chunks the window reads: its columns [iu, iu + NW) (the strip is clamped into the level, so
+            // at a border it holds columns outside the window) and the z-chunks its run [iv, iv + NW) reaches.
+            // Every other chunk is read with weight 0 or not at all (coff clamps into the window's columns).
+            {
+                const int zs = tab[2][jj] + zc * CE, ivj = tab[3][jj], xw = tab[1][jj] + c - tab[4][jj];
+                if (!(zs < ivj + NW && zs + CE > ivj) || (unsigned)xw >= (unsigned)NW) mask = 0u;
+            }
+            if (bk8) {
+                const int zs = tab[2][jj] + zc * CE, x = tab[1][jj] + c;
+                pk[k] = (ok ? (unsigned)(jj * SQ + (c * ZW + zc * CE) * ES) >> 3 : 0xffffu) | (mask << 16);
+                voff[k] = (int)(((long long)jj * A.row_stride + A.off[l] + (long long)ihj * Wl * Dpl +
+                                 ((long long)(x >> 3) * (Dpl >> 3) + (zs >> 3)) * 64 + (x & 7) * 8 + (zs & 7)) * ES);
+            } else {
+                pk[k] = (ok ? (unsigned)(jj * SQ + (c * ZW + zc * CE) * ES) >> 3 : 0xffffu) | (mask << 16);
+                voff[k] = (int)(((long long)jj * A.row_stride + A.off[l] + (long long)ihj * Wl * Dpl +
+                                 (long long)(tab[1][jj] + c) * Dpl + tab[2][jj] + zc * CE) * ES);
+            }
+        }
+        auto load_plane = [&](int wp, u32x4 (&st)[C::MAXCH]) {
+#pragma unroll
+            for (int k = 0; k < C::MAXCH; ++k) {
+                if constexpr ((ABL & 2) != 0) st[k] = u32x4{(unsigned)k, 0, 0, 0};
+                else if (pk[k] & (1u << (16 + wp))) {
+                    const int o = voff[k] + wp * plane_bytes;   // (bricks keep whole planes: same plane stride)
+                    if (ldpol == 2)
+                        st[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, o, 0, 2));
+                    else
+                        st[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, o, 0, 0));
+                }
+            }
+        };
+        auto write_plane = [&](int slot, int wp, const u32x4 (&st)[C::MAXCH]) {
+            unsigned char *sb = smem + C::GUARD + slot * C::SLOT;
+#pragma unroll
+            for (int k = 0; k < C::MAXCH; ++k) {
+                if (pk[k] & (1u << (16 + wp))) {
+                    const unsigned o = (pk[k] & 0xffffu) * 8;
+                    u32x2 lo = {st[k][0], st[k][1]}, hi = {st[k][2], st[k][3]};
+                    *reinterpret_cast<u32x2 *>(sb + o) = lo;
+                    *reinterpret_cast<u32x2 *>(sb + o + 8) = hi;
+                }
+            }
+        };
+        auto lerp_col = [&](int slot, int k, ZRun<n> &z) {
+            float r[NW];
+            lds_run<NW>(smem + C::GUARD + slot * C::SLOT, coff[k], (const T *)nullptr, r);
+#pragma unroll
+            for (int i = 0; i < NP; ++i)
+                z.p[i] = __builtin_elementwise_fma(f32x2{r[2 * i + 1], r[2 * i + 2]}, w1p[i],
+                                                   f32x2{r[2 * i], r[2 * i + 1]} * w0p[i]);
+            z.t = __builtin_fmaf(r[n], wv1[n - 1], r[n - 1] * wv0[n - 1]);
+        };
+
+        // staged planes (relative index p = plane - a0): plane p + 2 is loaded into st[p & 1]
+        // two rows before it is written
+        constexpr int NPL = NA + 1;   // window planes this workgroup reads
+        u32x4 st[2][C::MAXCH];
+        ZRun<n> zp[NU + 1];       // z-lerped columns of the lower plane of the current row
+        load_plane(a0, st[0]);
+        load_plane(a0 + 1, st[1]);
+        write_plane(0, a0, st[0]);
+        if (2 < NPL) load_plane(a0 + 2, st[0]);
+        __syncthreads();          // plane a0 in slot 0
+#pragma unroll
+        for (int k = 0; k <= NU; ++k) lerp_col(0, k, zp[k]);
+        write_plane(1, a0 + 1, st[1]);
+        __syncthreads();          // plane a0 + 1 in slot 1
+#pragma unroll
+        for (int ia = 0; ia < NA; ++ia) {
+            const int a = a0 + ia;
+            if (ia + 3 < NPL) load_plane(a + 3, st[(ia + 1) & 1]);   // in flight for two rows
+            float wy0, wy1;
+            axis_weights(ax.ph, ax.kh, a - R, ax.hs, ax.hs, wy0, wy1);
+            wy0 = (unsigned)(ih + a) < (unsigned)Hl ? wy0 : 0.0f;
+            wy1 = (unsigned)(ih + a + 1) < (unsigned)Hl ? wy1 : 0.0f;
+            // column by column: once window column k of plane a+1 is lerped, output
+            // column k-1 is complete and plane a's column k-1 retires
+            ZRun<n> zprev;
+            unsigned xr[NU * NP];   // PROJ: this row's value pairs as f16x2
+            float xt[NU];           // PROJ: tails (v = n - 1)
+#pragma unroll
+            for (int k = 0; k <= NU; ++k) {
+                ZRun<n> zcur;
+                lerp_col((ia + 1) & 1, k, zcur);
+                if (k >= 1) {
+                    const int uu = k - 1;
+                    const float p00 = wx0[uu] * wy0, p10 = wx1[uu] * wy0;
+                    const float p01 = wx0[uu] * wy1, p11 = wx1[uu] * wy1;
+                    // PROJ (MFMA consumer wave alongside): broadcasts materialised, see splat2
+                    const auto bc = [](float p) { if constexpr (PROJ) return splat2(p); else return f32x2{p, p}; };
+                    const f32x2 P00 = bc(p00), P10 = bc(p10), P01 = bc(p01), P11 = bc(p11);
+                    const __amdgpu_buffer_rsrc_t rs = out_rsrc(obase, a, u0 + uu);
+                    [[maybe_unused]] float wide[2 * NP + 1];
+#pragma unroll
+                    for (int i = 0; i < NP; ++i) {
+                        f32x2 acc = P00 * zp[uu].p[i];
+                        acc = __builtin_elementwise_fma(P10, zp[uu + 1].p[i], acc);
+                        acc = __builtin_elementwise_fma(P01, zprev.p[i], acc);
+                        acc = __builtin_elementwise_fma(P11, zcur.p[i], acc);
+                        if constexpr (PROJ) {
+                            xr[uu * NP + i] = __builtin_bit_cast(unsigned, __builtin_convertvector(acc, f16x2));
+                        } else if constexpr ((ABL & 4) != 0) {
+                            wide[2 * i] = acc[0];
+                            wide[2 * i + 1] = acc[1];
+                        } else {
+                            store(rs, 2 * i, acc[0]);
+                            store(rs, 2 * i + 1, acc[1]);
+                        }
+                    }
+                    float acc = p00 * zp[uu].t;
+                    acc = __builtin_fmaf(p10, zp[uu + 1].t, acc);
+                    acc = __builtin_fmaf(p01, zprev.t, acc);
+                    acc = __builtin_fmaf(p11, zcur.t, acc);
+                    if constexpr (PROJ) {
+                        xt[uu] = acc;
+                    } else if constexpr ((ABL & 4) != 0) {   // diagnostics: same bytes, 16-byte stores
+                        wide[n - 1] = acc;
+#pragma unroll
+                        for (int g4 = 0; g4 + 4 <= n - 1; g4 += 4)
+                            __builtin_amdgcn_raw_buffer_store_b128(
+                                u32x4{__float_as_uint(wide[g4]), __float_as_uint(wide[g4 + 1]),
+                                      __float_as_uint(wide[g4 + 2]), __float_as_uint(wide[g4 + 3])},
+                                rs, q4 * 4, (int)(g4 * Nq * 4), 2);
+                        store(rs, n - 1, acc);
+                    } else {
+                        store(rs, n - 1, acc);
+                    }
+                    zp[uu] = zprev;
+                }
+                zprev = zcur;
+                if (k == NU) zp[k] = zcur;
+            }
+            if constexpr (PROJ) {
+                // this wave's 32-k slice of the row: pairs, then the tails, then zeros
+                constexpr int T0 = NU * NP;
+                unsigned xw[ProjCfg::KW / 2];
+#pragma unroll
+                for (int d = 0; d < ProjCfg::KW / 2; ++d) xw[d] = d < T0 ? xr[d < T0 ? d : 0] : 0u;
+#pragma unroll
+                for (int p = 0; 2 * p < NU; ++p) {
+                    const f32x2 t2 = {xt[2 * p], 2 * p + 1 < NU ? xt[2 * p + 1 < NU ? 2 * p + 1 : 0] : 0.0f};
+                    xw[T0 + p] = __builtin_bit_cast(unsigned, __builtin_convertvector(t2, f16x2));
+                }
+                __syncthreads();   // the consumer has read the previous row of X
+                u32x4 *dst = reinterpret_cast<u32x4 *>(xs + lane * XROW + wave * (ProjCfg::KW * 2));
+#pragma unroll
+                for (int j = 0; j < ProjCfg::KW / 8; ++j)
+                    dst[j] = u32x4{xw[4 * j], xw[4 * j + 1], xw[4 * j + 2], xw[4 * j + 3]};
+            }
+            if (ia + 2 < NPL) write_plane(ia & 1, a + 2, st[ia & 1]);   // plane a+2 into the slot of plane a (read in row a-1)
+            __syncthreads();
+        }
+    };
+
+    // odd tiles walk the levels coarse-to-fine, so the two tiles sharing a CU mix the
+    // gather-heavy fine levels with the store-heavy coarse ones
+    const int li0 = A.split_levels ? (int)blockIdx.y : 0;
+    const int li1 = A.split_levels ? li0 + 1 : A.nl;
+    constexpr int NCH_A = ACH > 0 ? (n + ACH - 1) / ACH : 1;       // row chunks
+    constexpr int NA_FULL = ACH > 0 ? ACH : n;
+    constexpr int NA_TAIL = ACH > 0 ? n - ACH * (NCH_A - 1) : n;    // rows of the last chunk
+    const int a0 = ACH > 0 ? (int)blockIdx.z * ACH : 0;
+    auto rows = [&](int l, auto nu_c) {
+        if (NA_TAIL == NA_FULL || a0 + NA_FULL <= n) level(l, nu_c, std::integral_constant<int, NA_FULL>{}, a0);
+        else level(l, nu_c, std::integral_constant<int, NA_TAIL>{}, a0);
+    };
+    for (int li = li0; li < li1; ++li) {
+        const int l = A.l0 + (rev ? A.nl - 1 - li : li);
+        if (A.generic[l] && !A.zero[l]) continue;   // legacy level with W != D: k_lookup_generic
+        if constexpr (BAL) {
+            if (REM > 0 && wave < REM) rows(l, std::integral_constant<int, FLO + 1>{});
+            else rows(l, std::integral_constant<int, FLO>{});
+        } else if (NU_LAST == C::COLS || wave < C::NWAVES - 1) {
+            rows(l, std::integral_constant<int, C::COLS>{});
+        } else {
+            rows(l, std::integral_constant<int, NU_LAST>{});
+        }
+    }
+}
+
+}  // namespace dvc

@@ -2,19 +2,17 @@
 
 namespace dvc {
 
-// instances of k_lookup_tile (lookup_tile.h), split over translation units so they compile in parallel:
-// this file float32 pyramids, lookup_tile_bf16.hip bf16, lookup_tile_proj.hip the convc1-fused ones,
-// lookup_tile_diag.hip the diagnostics-only ablation / store-policy instances.
+// bf16 instances of k_lookup_tile (lookup_tile.h); see lookup_tile.hip
 #define DVC_TILE_INST(T, R)                                                      \
     template __global__ void k_lookup_tile<T, R, false, 0, false, 0>(LookupArgs); \
     template __global__ void k_lookup_tile<T, R, true, 0, false, 0>(LookupArgs);  \
     template __global__ void k_lookup_tile<T, R, true, 0, false, 2>(LookupArgs);  \
     template __global__ void k_lookup_tile<T, R, true, 0, false, 3>(LookupArgs);  \
     template __global__ void k_lookup_tile<T, R, true, 0, false, 5>(LookupArgs);
-DVC_TILE_INST(float, 1) DVC_TILE_INST(float, 2) DVC_TILE_INST(float, 3)
-DVC_TILE_INST(float, 4) DVC_TILE_INST(float, 5) DVC_TILE_INST(float, 6)
+DVC_TILE_INST(bf16_t, 1) DVC_TILE_INST(bf16_t, 2) DVC_TILE_INST(bf16_t, 3)
+DVC_TILE_INST(bf16_t, 4) DVC_TILE_INST(bf16_t, 5) DVC_TILE_INST(bf16_t, 6)
 // balanced four-wave instances (tuning "lookup_waves" = 4)
-template __global__ void k_lookup_tile<float, 4, true, 0, false, 0, 4>(LookupArgs);
-template __global__ void k_lookup_tile<float, 4, true, 0, false, 5, 4>(LookupArgs);
+template __global__ void k_lookup_tile<bf16_t, 4, true, 0, false, 0, 4>(LookupArgs);
+template __global__ void k_lookup_tile<bf16_t, 4, true, 0, false, 5, 4>(LookupArgs);
 
 }  // namespace dvc

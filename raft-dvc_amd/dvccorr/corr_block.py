@@ -81,11 +81,11 @@ def _wants_grad(*ts: torch.Tensor) -> bool:
 
 def _check_backward_support(lay, C: int, radius: int, legacy: bool) -> None:
     """Raise at construction (not after twelve forward lookups) when dvc_corr_backward cannot
-    differentiate this block (include/dvccorr.h: radius 1..6, C <= 128)."""
+    differentiate this block (include/dvccorr.h: radius 1..6; any C -- the gradient kernels run per
+    128-channel group, as the reference's CUDA backward is templated for C in {16, 64, 128, 256},
+    corr_otf_cuda.cu:537-541)."""
     if not 1 <= radius <= 6:
         raise NotImplementedError(f"dvccorr backward supports radius 1..6, got {radius}")
-    if lay.c_pad > 128:
-        raise NotImplementedError(f"dvccorr backward supports C <= 128 feature channels, got {C}")
 
 
 def pyramid_bytes(B: int, C: int, H: int, W: int, D: int, num_levels: int, precision: str = "fp32") -> int:
@@ -428,6 +428,10 @@ def flow_step(coords1: torch.Tensor, delta_flow: Optional[torch.Tensor], target_
     return ops.flow_step(coords1, delta_flow, target_shape)
 
 
+# CorrBlock keywords with no meaning for the on-the-fly block (no pyramid is stored)
+_MATERIALISED_ONLY_KW = ("build", "bricked")
+
+
 def make_corr_block(impl: str, fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int = 4, radius: int = 4,
                     sampler_version: int = 2, **kw):
     """The dispatch RAFTDVC.forward performs on config.corr_impl (raft_dvc.py:369-420), for the new impls.
@@ -451,6 +455,6 @@ def make_corr_block(impl: str, fmap1: torch.Tensor, fmap2: torch.Tensor, num_lev
         prec = resolve_precision(fmap1, kw.get("precision"))
         fits = pyramid_bytes(B, C, H, W, D, num_levels, prec) <= 0.9 * hbm_available(fmap1.device)
         cls = CorrBlock if fits else CorrBlockFused
-        kw = {k: v for k, v in kw.items() if cls is CorrBlock or k != "build"}
+        kw = {k: v for k, v in kw.items() if cls is CorrBlock or k not in _MATERIALISED_ONLY_KW}
         return cls(fmap1, fmap2, num_levels, radius, legacy_wd_swap=legacy, **kw)
     raise ValueError(f"Invalid corr_impl for dvccorr: {impl!r}. Must be 'mi355x', 'mi355x_fused' or 'mi355x_auto'")

@@ -58,6 +58,20 @@ def _need_cuda(*ts: torch.Tensor) -> None:
             raise RuntimeError("dvccorr runs on the MI355X only: got a CPU tensor (no CPU fallback)")
 
 
+def _mark(t: torch.Tensor, dtype: int) -> torch.Tensor:
+    """Record the DVC_BRICKED layout flag next to a packed-target / pyramid buffer (the C ABI cannot tell)."""
+    t._dvc_bricked = bool(int(dtype) & DVC_BRICKED)
+    return t
+
+
+def _expect_layout(t: torch.Tensor, dtype: int, what: str) -> None:
+    """A buffer packed bricked must be read with DVC_BRICKED, and only by the entry points that take it."""
+    rec = getattr(t, "_dvc_bricked", None)
+    if rec is not None and rec != bool(int(dtype) & DVC_BRICKED):
+        raise ValueError(f"{what}: the buffer was packed {'bricked' if rec else 'linear'} but is passed as "
+                         f"{'bricked' if int(dtype) & DVC_BRICKED else 'linear'} (include/dvccorr.h, DVC_BRICKED)")
+
+
 def _f32c(t: torch.Tensor) -> torch.Tensor:
     return t.to(torch.float32).contiguous()
 
@@ -85,7 +99,7 @@ def pack_targets(fmap2: torch.Tensor, num_levels: int, dtype: int, out: torch.Te
     ws = torch.empty((max(nws, 4) // 4,), dtype=torch.float32, device=f.device)
     check(lib().dvc_pack_targets(_ptr(f), _ptr(out), _ptr(ws), B, C, H, W, D, num_levels, dtype, _stream(f)),
           "pack_targets")
-    return out
+    return _mark(out, dtype)
 
 
 GUARD_BYTES = 256   # DVC_CORR_GUARD_BYTES
@@ -112,11 +126,14 @@ def build(packed_q: torch.Tensor, packed_t: torch.Tensor, C: int, H: int, W: int
         out = alloc_corr(B, Nq, lay.row_stride, store_dtype, packed_q.device)
     check(lib().dvc_corr_build(_ptr(packed_q), _ptr(packed_t), _ptr(out), B, Nq, C, H, W, D, num_levels, in_dtype,
                                store_dtype, col_begin, col_end, _stream(packed_q)), "corr_build")
+    # the build is layout-blind: bricked packed targets give a bricked pyramid
+    out._dvc_bricked = getattr(packed_t, "_dvc_bricked", False)
     return out
 
 
 def pool(corr: torch.Tensor, H: int, W: int, D: int, num_levels: int, src_level: int, store_dtype: int) -> None:
     _need_cuda(corr)
+    _expect_layout(corr, store_dtype, "corr_pool")
     B, Nq, _ = corr.shape
     check(lib().dvc_corr_pool(_ptr(corr), B, Nq, H, W, D, num_levels, src_level, store_dtype, _stream(corr)),
           "corr_pool")
@@ -125,6 +142,7 @@ def pool(corr: torch.Tensor, H: int, W: int, D: int, num_levels: int, src_level:
 def lookup(corr: torch.Tensor, coords: torch.Tensor, H: int, W: int, D: int, num_levels: int, radius: int,
            legacy: bool, store_dtype: int, out: torch.Tensor = None) -> torch.Tensor:
     _need_cuda(corr, coords)
+    _expect_layout(corr, store_dtype, "corr_lookup")
     B, Nq, _ = corr.shape
     c = _f32c(coords)
     n3 = (2 * radius + 1) ** 3
@@ -177,6 +195,7 @@ def lookup_proj(corr: torch.Tensor, coords: torch.Tensor, packed_w: torch.Tensor
                 out: torch.Tensor = None) -> torch.Tensor:
     """relu(convc1(lookup(coords))) -> (B, 96, Nq) f32, the lookup never written (dvc_corr_lookup_proj)."""
     _need_cuda(corr, coords, packed_w, bias)
+    _expect_layout(corr, store_dtype, "corr_lookup_proj")
     B, Nq, _ = corr.shape
     c = _f32c(coords)
     b = _f32c(bias)
@@ -196,6 +215,7 @@ def lookup_fused_proj(packed_q: torch.Tensor, packed_t: torch.Tensor, coords: to
     """relu(convc1(lookup_fused(coords))) -> (B, 96, Nq) f32 on the on-the-fly path, the lookup never written
     (dvc_corr_lookup_fused_proj: queries grouped by window origin, convc1 on MFMA)."""
     _need_cuda(packed_q, packed_t, coords, packed_w, bias)
+    _expect_layout(packed_t, dtype, "corr_lookup_fused_proj")
     B, Nq, _ = packed_q.shape
     c = _f32c(coords)
     b = _f32c(bias)
@@ -217,6 +237,7 @@ def lookup_fused(packed_q: torch.Tensor, packed_t: torch.Tensor, coords: torch.T
                  D: int, num_levels: int, radius: int, legacy: bool, dtype: int, out: torch.Tensor = None,
                  workspace: torch.Tensor = None) -> torch.Tensor:
     _need_cuda(packed_q, packed_t, coords)
+    _expect_layout(packed_t, dtype, "corr_lookup_fused")
     B, Nq, _ = packed_q.shape
     c = _f32c(coords)
     n3 = (2 * radius + 1) ** 3
@@ -241,6 +262,7 @@ def corr_backward(packed_q: torch.Tensor, packed_t: torch.Tensor, coords: torch.
     """d loss / d fmap1 (B, C, Nq) and d loss / d fmap2 (B, C, H, W, D), both float32, from the gradient of
     a lookup output (B, L*(2r+1)^3, Nq) (dvc_corr_backward)."""
     _need_cuda(packed_q, packed_t, coords, grad_out)
+    _expect_layout(packed_t, dtype, "corr_backward")
     B, Nq, _ = packed_q.shape
     c = _f32c(coords)
     g = _f32c(grad_out)

@@ -15,12 +15,25 @@ to the whole-volume one:
 
   * halo planes: before every convolution with a spatial extent along H, each
     rank receives the planes the kernel reaches across its slab boundaries
-    from its neighbours (zeros beyond the volume, as the reference's zero
-    padding); one all-gather of every rank's boundary planes per convolution;
+    from its two neighbours (zeros beyond the volume, as the reference's zero
+    padding): one batched point-to-point exchange with rank - 1 and rank + 1
+    per convolution (dist.batch_isend_irecv), so a rank's halo traffic does not
+    grow with the number of ranks;
   * normalisation statistics: InstanceNorm3d / GroupNorm / training-mode
     BatchNorm3d normalise over the whole volume, so their per-channel sums are
     all-reduced (two passes: mean, then the centred sum of squares, as the
     reference's biased variance).
+
+Scope (forward only): the collectives above carry no autograd, so the encoder
+is run for inference -- a call that would need gradients (grad mode on and
+the input or any encoder parameter requiring grad) raises, as ShardedCorrBlock
+does.  Only encoders whose forward is the reference's conv1 -> norm1 -> relu ->
+layers -> conv2 sequence are accepted: BasicEncoder, MediumEncoder and
+ShallowEncoder (and subclasses that keep their forward, e.g. LateStrideEncoder,
+extractor.py:526); a subclass that overrides forward (ShallowUpEncoder adds a
+trilinear x2 upsample, extractor.py:549-566) is refused unless its class sets
+`sharded_forward_equivalent = True` itself.  Training-mode norms that track running
+statistics are refused (the slab pass would not update them).
 
 Slabs follow sharded.slab_bounds on the feature-map H axis; rank r's input
 slab is planes [s * h0, s * h1) of the volume (s = the encoder's total
@@ -73,47 +86,81 @@ def encoder_stride(encoder: nn.Module) -> int:
 class ShardedEncoder:
     """Run `encoder` on this rank's H-slab.  __call__(volume_slab | [vol0_slab, vol1_slab], H) -> feature slab(s)."""
 
+    #: classes whose forward is the sequence interpreted here (extractor.py:218-256, :386-412, :497-523)
+    KNOWN_FORWARDS = ("BasicEncoder", "MediumEncoder", "ShallowEncoder")
+
     def __init__(self, encoder: nn.Module, group=None):
         for name in ("conv1", "norm1", "conv2"):
             if not hasattr(encoder, name):
                 raise TypeError(f"ShardedEncoder: encoder has no {name!r} (expected a RAFT-DVC feature encoder)")
+        owner = next((k for k in type(encoder).__mro__ if "forward" in vars(k)), None)
+        if not (owner is not None and (owner.__name__ in self.KNOWN_FORWARDS
+                                       or vars(owner).get("sharded_forward_equivalent", False))):
+            raise NotImplementedError(
+                f"ShardedEncoder: {type(encoder).__name__}.forward is defined by "
+                f"{getattr(owner, '__name__', None)}, not by one of {self.KNOWN_FORWARDS}; a forward that adds "
+                f"steps (e.g. ShallowUpEncoder's x2 upsample) would be skipped by the slab interpreter")
         if getattr(encoder, "training", False) and getattr(encoder, "dropout", None) is not None:
             raise NotImplementedError("ShardedEncoder: dropout in training mode is not supported")
+        for m in encoder.modules():
+            if isinstance(m, nn.modules.batchnorm._NormBase) and m.training and m.track_running_stats:
+                raise NotImplementedError(
+                    f"ShardedEncoder: training-mode {type(m).__name__} with track_running_stats would not update "
+                    f"its running statistics on the slab pass; call encoder.eval() or disable tracking")
         self.enc = encoder
         self.group = group
         self.world, self.rank = _world(group), _rank(group)
         self.stride = encoder_stride(encoder)
+        self._thin = 1.0   # (thinnest rank's slab) / (this rank's slab), set per call
 
     # ---------------------------------------------------------------- collectives
-    def _all_gather(self, t: torch.Tensor) -> torch.Tensor:
-        buf = t.new_empty((self.world,) + tuple(t.shape))
-        if dist.get_backend(self.group) == "nccl":
-            dist.all_gather_into_tensor(buf, t.contiguous(), group=self.group)
-        else:
-            dist.all_gather(list(buf.unbind(0)), t.contiguous(), group=self.group)
-        return buf
-
     def _all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         if self.world > 1:
             dist.all_reduce(t, group=self.group)
         return t
 
+    def _peer(self, r: int) -> int:
+        """Global rank of group rank r (point-to-point ops address global ranks)."""
+        return r if self.group is None else dist.get_global_rank(self.group, r)
+
     def _halo(self, x: torch.Tensor, lo: int, hi: int) -> torch.Tensor:
-        """x with `lo` planes of the previous slab prepended and `hi` of the next appended (zeros at the ends)."""
+        """x with `lo` planes of the previous slab prepended and `hi` of the next appended (zeros at the ends).
+
+        Neighbour exchange: this rank sends its last `lo` planes to rank + 1 and its first `hi` planes to
+        rank - 1, and receives the matching planes from them -- four point-to-point ops at most, whatever
+        the number of ranks."""
         if lo == 0 and hi == 0:
             return x
         m = max(lo, hi)
-        if self.world == 1:
-            parts_lo = x.new_zeros(x.shape[:2] + (lo,) + x.shape[3:])
-            parts_hi = x.new_zeros(x.shape[:2] + (hi,) + x.shape[3:])
-            return torch.cat([parts_lo, x, parts_hi], dim=2)
-        if x.shape[2] < m:
-            raise ValueError(f"ShardedEncoder: a slab of {x.shape[2]} planes is thinner than the {m}-plane halo; "
-                             f"use fewer ranks for this volume")
-        edges = self._all_gather(torch.cat([x[:, :, :m], x[:, :, -m:]], dim=2))   # [world, B, C, 2m, W, D]
-        r = self.rank
-        below = edges[r - 1][:, :, 2 * m - lo:] if r > 0 else x.new_zeros(x.shape[:2] + (lo,) + x.shape[3:])
-        above = edges[r + 1][:, :, :hi] if r < self.world - 1 else x.new_zeros(x.shape[:2] + (hi,) + x.shape[3:])
+        below = x.new_zeros(x.shape[:2] + (lo,) + x.shape[3:])
+        above = x.new_zeros(x.shape[:2] + (hi,) + x.shape[3:])
+        if self.world > 1:
+            # every rank applies the same test (the thinnest slab scales like this one): all raise together
+            if x.shape[2] * self._thin < m:
+                raise ValueError(f"ShardedEncoder: a slab of {int(x.shape[2] * self._thin)} planes is thinner than "
+                                 f"the {m}-plane halo; use fewer ranks for this volume")
+            # gloo moves host memory only: device tensors are staged through the host (rehearsals)
+            host = x.is_cuda and dist.get_backend(self.group) != "nccl"
+            stage = (lambda t: t.cpu()) if host else (lambda t: t.contiguous())
+            bl, ab = stage(below), stage(above)
+            r, ops = self.rank, []
+            if r > 0:
+                if hi:
+                    ops.append(dist.P2POp(dist.isend, stage(x[:, :, :hi]), self._peer(r - 1), self.group))
+                if lo:
+                    ops.append(dist.P2POp(dist.irecv, bl, self._peer(r - 1), self.group))
+            if r < self.world - 1:
+                if lo:
+                    ops.append(dist.P2POp(dist.isend, stage(x[:, :, x.shape[2] - lo:]), self._peer(r + 1),
+                                          self.group))
+                if hi:
+                    ops.append(dist.P2POp(dist.irecv, ab, self._peer(r + 1), self.group))
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+            if host:
+                below, above = bl.to(x.device), ab.to(x.device)
+            else:
+                below, above = bl, ab
         return torch.cat([below, x, above], dim=2)
 
     # ---------------------------------------------------------------- layers
@@ -191,6 +238,14 @@ class ShardedEncoder:
         extractor.py:397-410: both volumes through one pass, split after).  H: full input H (checks the slab)."""
         is_list = isinstance(x, (list, tuple))
         xs = torch.cat(list(x), dim=0) if is_list else x
+        if torch.is_grad_enabled() and (xs.requires_grad or any(p.requires_grad for p in self.enc.parameters())):
+            raise NotImplementedError(
+                "ShardedEncoder is forward-only (its halo and statistics exchanges carry no autograd): run it "
+                "under torch.no_grad() / inference_mode, or use the whole-volume encoder for training")
+        if self.world > 1:   # the thinnest slab, for the halo check every rank makes alike
+            t = torch.tensor([xs.shape[2]], dtype=torch.float64, device=xs.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+            self._thin = float(t.item()) / xs.shape[2]
         if H is not None:
             i0, i1 = self.input_bounds(H)
             if xs.shape[2] != i1 - i0:

@@ -42,6 +42,9 @@ class Bottleneck(nn.Module):
 
 
 class Encoder(nn.Module):
+    # forward is extractor.py's conv1 -> norm1 -> relu -> layers -> conv2 (the sequence ShardedEncoder interprets)
+    sharded_forward_equivalent = True
+
     def __init__(self, kind="1/4", input_dim=1, output_dim=128):
         super().__init__()
         s1, s2, s3 = STRIDES[kind]

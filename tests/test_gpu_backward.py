@@ -80,6 +80,25 @@ def test_grad_matches_oracle(shape, C, L, r, legacy):
         assert e1 <= GRAD_TOL and e2 <= GRAD_TOL, (shape, r, legacy, kind, e1, e2)
 
 
+@pytest.mark.parametrize("precision,tol", [("fp32", GRAD_TOL), ("bf16", BF16_TOL)])
+def test_grad_wide_features_c256(precision, tol):
+    """C = 256 (C_pad 256, two 128-channel groups per gradient kernel; the reference's CUDA backward is
+    templated for C in {16, 64, 128, 256}, corr_otf_cuda.cu:537-541) and C = 160 (a partial second group),
+    against autograd through oracle/torch_cpu.py; tolerance test_corr_equivalence.py:189-217 style."""
+    for C, shape, L, r in ((256, (10, 9, 12), 3, 4), (160, (8, 12, 10), 2, 3)):
+        H, W, D = shape
+        seed = 2560 + C + r
+        f1 = prng.normal(seed, (1, C, H, W, D))
+        f2 = prng.normal(seed + 1, (1, C, H, W, D))
+        coords = prng.flow_coords(seed + 2, 1, H, W, D, 3.0)
+        G = prng.normal(seed + 3, (1, L * (2 * r + 1) ** 3, H, W, D))
+        ref1, ref2 = oracle_grads(f1, f2, coords, G, L, r, False)
+        for kind in ("gemm", "fused"):
+            d1, d2 = _gpu_grads(kind, f1, f2, coords, G, L, r, False, precision=precision)
+            e1, e2 = orc.rel_err(d1, ref1), orc.rel_err(d2, ref2)
+            assert e1 <= tol and e2 <= tol, (C, precision, kind, e1, e2)
+
+
 def test_grad_bf16_build():
     g = load_golden("grad_equiv_L2_r4_rand.npz")
     f1, f2, coords, G, L, r, legacy = grad_inputs(g)

@@ -119,4 +119,11 @@ def test_bricked_refused_where_linear():
         ops.lookup(corr, cf, S, S, S, L, 7, False, dt | ops.DVC_BRICKED)
     with pytest.raises(NotImplementedError, match="single-pass"):
         ops.pack_targets(torch.randn(1, C, S, S, S, device=DEV), 5, dt | ops.DVC_BRICKED)
+    # the C ABI cannot tell a bricked buffer from a linear one; the Python layer records the flag
+    with pytest.raises(ValueError, match="packed bricked"):
+        ops.lookup(corr, cf, S, S, S, L, 4, False, dt)
+    with pytest.raises(ValueError, match="packed bricked"):
+        ops.lookup_fused(q, t, cf, C, S, S, S, L, 4, False, dt)
+    with pytest.raises(ValueError, match="packed bricked"):
+        ops.corr_backward(q, t, cf, torch.zeros(1, L * 729, S ** 3, device=DEV), C, S, S, S, L, 4, False, dt)
     torch.cuda.synchronize()

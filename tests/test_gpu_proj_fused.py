@@ -177,3 +177,38 @@ def test_fp32_block_takes_exact_composition():
     t1, t2, tc, tw, tb = _gpu(f1, f2, coords, w, b)
     out = dvccorr.CorrBlockFused(t1, t2, L, r, precision="fp32").lookup_convc1(tc, tw, tb)
     assert orc.rel_err(out.cpu().numpy(), ref) < FP32_TOL
+
+
+def test_repeatable_under_poisoned_memory():
+    """Regression check of the round-2 packed-FP32 hazard: the caching allocator is
+    filled with -7 / 3e4 / NaN between calls, so every workspace the kernels get holds stale values; 30
+    calls of the case that failed then (12x10x16, C=64, L=3, r=2) must all equal the first, bit for bit.
+    Before the fix 3-5 % of such calls differed in lanes 48-63 of a few chunks (tools/dbg_poison3.py)."""
+    import dvccorr
+    from dvccorr import ops
+    H, W, D = 12, 10, 16
+    C, L, r, B = 64, 3, 2, 1
+    seed = 1900 + H + 3 * W + 7 * D + r
+    f1 = prng.normal(seed, (2, C, H, W, D))[1:]
+    f2 = prng.normal(seed + 1, (2, C, H, W, D))[1:]
+    coords = prng.flow_coords(seed + 2, 2, H, W, D, 2.5)[1:]
+    w, b = _conv_inputs(seed + 3, L, r)
+    t1, t2, tc, tw, tb = _gpu(f1, f2, coords, w, b)
+    nws = ops.lib().dvc_lookup_fused_proj_workspace_bytes(B, H * W * D)
+    blk = dvccorr.CorrBlockFused(t1, t2, L, r, precision="bf16")
+    pw = ops.proj_pack(tw, L, r, False)
+
+    def call(ws):
+        return ops.lookup_fused_proj(blk._q, blk._t, tc.reshape(B, 3, -1), pw, tb, C, H, W, D, L, r, False,
+                                     blk._dt, workspace=ws).clone()
+
+    ref = call(torch.zeros((nws,), dtype=torch.uint8, device=DEV))
+    ora = orc.motion_convc1(orc.corr_lookup(f1, f2, coords, L, r, False), w, b)
+    assert orc.rel_err(ref.reshape(ora.shape).cpu().numpy(), ora) < PROJ_TOL
+    differ = 0
+    for it in range(30):
+        bufs = [torch.full((mb * (1 << 20) // 4,), (-7.0, 3.0e4, float("nan"))[it % 3], device=DEV)
+                for mb in (1, 3, 7, 16, 40) for _ in range(3)]
+        del bufs
+        differ += not torch.equal(call(torch.empty((nws,), dtype=torch.uint8, device=DEV)), ref)
+    assert differ == 0, f"{differ} of 30 calls differ"

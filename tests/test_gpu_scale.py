@@ -105,6 +105,36 @@ def test_cfg5_fused_rows():
     assert torch.equal(part, out[:, :, 48 * S * S:64 * S * S])
 
 
+def test_cfg5_fused_convc1_rows():
+    """Config #5 with MotionEncoder.convc1 fused (dvc_corr_lookup_fused_proj: k_otf_keys + radix sort +
+    k_fused_proj + k_rows_to_channels) at full size, 128^3 x 128 fmaps, L=2, r=4, bf16: sampled query
+    rows of relu(convc1(lookup)) against the f64 oracle at the bf16 tolerance (update.py:222, 246;
+    corr_otf.py:198-237), and two calls bitwise equal (the kernel whose packed-FP32 broadcasts once
+    corrupted lanes 48-63 intermittently)."""
+    import dvccorr
+    S, C, L, r = 128, 128, 2, 4
+    f1, f2, c = _inputs(515, C, S)
+    K = L * (2 * r + 1) ** 3
+    g = torch.Generator(device="cpu").manual_seed(516)
+    w = ((torch.rand(96, K, generator=g) * 2 - 1) / K ** 0.5).to(DEV)
+    b = ((torch.rand(96, generator=g) * 2 - 1) / K ** 0.5).to(DEV)
+    with torch.no_grad():
+        blk = dvccorr.CorrBlockFused(f1, f2, L, r, precision="bf16")
+        out = blk.lookup_convc1(c, w, b).reshape(1, 96, -1)
+        out2 = blk.lookup_convc1(c, w, b).reshape(1, 96, -1)
+        torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    assert torch.equal(out, out2)
+    N = S ** 3
+    rows = np.sort(np.random.default_rng(515).choice(N, 32, replace=False))
+    # plus the volume's corners/edges and rows inside one 64-query chunk's lanes 48-63
+    rows = np.unique(np.concatenate([rows, [0, N - 1, S - 1, S * S * 64 + S * 3 + 127, 4096 + 48, 4096 + 63]]))
+    rows = rows.astype(np.int64)
+    look = _oracle_rows(f1, f2, c, L, r, rows)                                   # [rows, K] f64
+    ref = np.maximum(look @ w.cpu().double().numpy().T + b.cpu().double().numpy()[None], 0.0)
+    assert orc.rel_err(_rows(out, rows), ref) <= BF16_TOL
+
+
 @pytest.mark.parametrize("precision,tol", [("bf16", BF16_TOL), ("fp32", FP32_TOL)])
 def test_wide_features_c256(precision, tol):
     """C = 256 (C_pad 256): the bf16 build instances whose spilled prefetch registers faulted in round 1
@@ -134,6 +164,9 @@ def test_capacity_check_and_auto_impl():
         dvccorr.CorrBlock(f, f, 1, 4, precision="bf16")
     assert torch.cuda.memory_allocated(DEV) == before
     blk = dvccorr.make_corr_block("mi355x_auto", f, f, 1, 4, precision="bf16")
+    assert isinstance(blk, dvccorr.CorrBlockFused)
+    # CorrBlock-only keywords are dropped on the fallback (they raised TypeError exactly there)
+    blk = dvccorr.make_corr_block("mi355x_auto", f, f, 1, 4, precision="bf16", build="gemm", bricked=True)
     assert isinstance(blk, dvccorr.CorrBlockFused)
     small = torch.randn(1, 32, 8, 8, 8, device=DEV)
     assert type(dvccorr.make_corr_block("mi355x_auto", small, small, 2, 2)) is dvccorr.CorrBlock

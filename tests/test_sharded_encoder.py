@@ -110,5 +110,42 @@ def test_thin_slab_raises():
     from dvccorr.sharded_encoder import ShardedEncoder
     enc, x, _ = _encoder("1_8")
     se = ShardedEncoder(enc, group="local")
-    with pytest.raises(ValueError, match="multiple of the encoder stride"):
+    with torch.no_grad(), pytest.raises(ValueError, match="multiple of the encoder stride"):
         se(x[:, :, :12], 12)
+
+
+def test_forward_only_guard():
+    """The halo / statistics exchanges carry no autograd: a call that would need gradients raises."""
+    from dvccorr.sharded_encoder import ShardedEncoder
+    enc, x, _ = _encoder("1_4")
+    se = ShardedEncoder(enc, group="local")
+    with pytest.raises(NotImplementedError, match="forward-only"):
+        se(x, x.shape[2])                       # encoder parameters require grad
+    with torch.no_grad():
+        se(x, x.shape[2])
+
+
+def test_refuses_overridden_forward_and_tracked_training_norms():
+    """A subclass that changes forward (the reference's ShallowUpEncoder upsamples x2, extractor.py:549-566)
+    is refused; one that keeps it (LateStrideEncoder, extractor.py:526) is accepted; training-mode norms
+    tracking running statistics are refused."""
+    from dvccorr.sharded_encoder import ShardedEncoder
+    enc, _, _ = _encoder("1_2")
+
+    class UpEncoder(type(enc)):
+        def forward(self, x):
+            return torch.nn.functional.interpolate(super().forward(x), scale_factor=2.0, mode="trilinear")
+
+    class SameForward(type(enc)):
+        pass
+
+    up = UpEncoder("1/2")
+    with pytest.raises(NotImplementedError, match="forward is defined by UpEncoder"):
+        ShardedEncoder(up, group="local")
+    ShardedEncoder(SameForward("1/2"), group="local")
+    bn = renc.Encoder("1/4")
+    bn.norm1 = torch.nn.BatchNorm3d(32)
+    bn.train()
+    with pytest.raises(NotImplementedError, match="running statistics"):
+        ShardedEncoder(bn, group="local")
+    ShardedEncoder(bn.eval(), group="local")
