@@ -96,7 +96,7 @@ typedef enum { DVC_FIXED = 0, DVC_LEGACY = 1 } dvc_convention;
 typedef struct {
     int32_t num_levels;
     int32_t channels;                 /* C */
-    int32_t c_pad;                    /* C rounded up to 32 (packed-row length) */
+    int32_t c_pad;                    /* packed-row length: 32, 64, 128, then multiples of 128 */
     int32_t H[DVC_MAX_LEVELS];
     int32_t W[DVC_MAX_LEVELS];
     int32_t D[DVC_MAX_LEVELS];

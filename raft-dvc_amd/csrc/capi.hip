@@ -347,6 +347,11 @@ int dvc_set_tuning(const char *key, int value) {
 const char *dvc_version(void) { return "dvccorr 0.1.0 (gfx950)"; }
 int dvc_abi_version(void) { return DVC_ABI_VERSION; }
 
+// Channel padding of the packed rows: 32, 64 or 128 up to C = 128, then multiples of 128 -- the channel
+// widths the bf16 MFMA build instantiates (C_pad / 8 in {4, 8, 16, 32}) and the backward's 128-channel
+// groups, so any C <= 256 builds on either path (C = 96 -> 128, C = 160 -> 256; the pad is zeros).
+static int pad_channels(int C) { return C <= 32 ? 32 : C <= 64 ? 64 : (int)round_up(C, 128); }
+
 int dvc_layout_init(int H, int W, int D, int num_levels, int C, dvc_layout *out) {
     if (!out) return fail(DVC_ERR_INVALID, "layout: null output");
     if (H < 1 || W < 1 || D < 1 || C < 1)
@@ -356,7 +361,7 @@ int dvc_layout_init(int H, int W, int D, int num_levels, int C, dvc_layout *out)
     memset(out, 0, sizeof(*out));
     out->num_levels = num_levels;
     out->channels = C;
-    out->c_pad = (int)round_up(C, 32);
+    out->c_pad = pad_channels(C);
     int h = H, w = W, d = D;
     long long off = 0;
     for (int l = 0; l < num_levels; ++l) {
@@ -400,7 +405,7 @@ int dvc_pack_queries(const float *fmap1, void *packed, int B, int C, int64_t Nq,
     if (!fmap1 || !packed) return fail(DVC_ERR_INVALID, "pack_queries: null pointer");
     if (B < 1 || C < 1 || Nq < 1) return fail(DVC_ERR_INVALID, "pack_queries: bad shape B=%d C=%d Nq=%lld", B, C,
                                                (long long)Nq);
-    const int Cp = (int)round_up(C, 32);
+    const int Cp = pad_channels(C);
     hipStream_t s = (hipStream_t)stream;
     dim3 grid((unsigned)ceil_div(Nq, 64), (unsigned)ceil_div(Cp, 32), (unsigned)B);
     if (dtype == DVC_BF16)

@@ -80,7 +80,7 @@ def pack_queries(fmap1_slab: torch.Tensor, dtype: int) -> torch.Tensor:
     _need_cuda(fmap1_slab)
     f = _f32c(fmap1_slab)
     B, C, Nq = f.shape
-    Cp = (C + 31) // 32 * 32
+    Cp = 32 if C <= 32 else 64 if C <= 64 else (C + 127) // 128 * 128   # dvc_layout_init's c_pad
     out = torch.empty((B, Nq, Cp), dtype=_TORCH_DT[dtype], device=f.device)
     check(lib().dvc_pack_queries(_ptr(f), _ptr(out), B, C, Nq, dtype, _stream(f)), "pack_queries")
     return out

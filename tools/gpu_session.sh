@@ -34,7 +34,7 @@ EOF
 for s in ${STEPS:-tests bench}; do
   case $s in
   tests)
-    timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+    timeout -k 10 900 python -u -m pytest tests -m gpu --maxfail=${MAXFAIL:-1} -v --timeout 300 --timeout-method thread \
         ${PYTEST_ARGS:-} > "$OUT/pytest.log" 2>&1
     rc=$?; echo "pytest rc=$rc"; tail -3 "$OUT/pytest.log"; grep -E "^FAILED|^ERROR" "$OUT/pytest.log" | head
     if [ $rc -ne 0 ] || fault "$OUT/pytest.log"; then echo "STOP after pytest"; exit 3; fi

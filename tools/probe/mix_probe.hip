@@ -1,0 +1,94 @@
+// mix_probe.hip -- calibration (not product code): the HBM ceiling of the lookup's traffic MIX.
+// k_lookup_tile at config #3 reads ~260 MB of scattered 128-byte lines of the pyramid (rows of
+// 75 KB, one per query) and writes 382 MB of fp32 output as dword-per-lane, 256-byte wave stores
+// into the channel-major (2916, 32768) output.  This kernel moves the same bytes in the same
+// shapes with no compute, no LDS and no barriers, so its time is the floor any lookup kernel with
+// that traffic can reach.  Variants: read bytes (line count per query), waves per CU, store policy.
+//   hipcc --offload-arch=gfx950 -O3 -o mix_probe mix_probe.hip && ./mix_probe
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// one workgroup = 64 queries (lane = query for the stores), NWV waves.  Per "row" step a wave
+// loads LPR lines per query-chunk group (8 lanes per 128-byte line, 16 B per lane) from the
+// tile's 64 rows and stores CPR channels (256 B each) of the output.
+template <int NWV, int POL>
+__global__ __launch_bounds__(64 * NWV) void k_mix(const unsigned char *pyr, float *out, long long rs, int nq, int nch,
+                                                  int rows, int lines_per_row, unsigned *sink) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const long long q0 = (long long)blockIdx.x * 64;
+    const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(pyr + q0 * rs), (short)0, (int)(64 * rs), 0x00020000);
+    const int chs = nch / rows;   // channels per row step
+    u32x4 acc = {0, 0, 0, 0};
+    unsigned h = blockIdx.x * 2654435761u + wave * 40503u;
+    for (int r = 0; r < rows; ++r) {
+        // loads: lines_per_row lines per wave per row; lane group g = lane / 8 takes lines g, g + 8, ...
+        for (int li = lane >> 3; li < lines_per_row; li += 8) {
+            h = h * 1664525u + 1013904223u;
+            const int qq = (h >> 8) & 63;
+            const int line = (h >> 16) % (int)(rs / 128);
+            acc ^= __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                rin, (int)(qq * rs + line * 128 + (lane & 7) * 16), 0, 0));
+        }
+        // stores: this wave's share of the row's channels
+        for (int c = wave; c < chs; c += NWV) {
+            const int ch = r * chs + c;
+            __builtin_amdgcn_raw_buffer_store_b32(
+                __float_as_uint((float)ch) ^ (acc[0] & 1u),
+                __builtin_amdgcn_make_buffer_rsrc(out + (long long)ch * nq, (short)0, nq * 4, 0x00020000),
+                (int)((q0 + lane) * 4), 0, POL);
+        }
+    }
+    if ((acc[0] ^ acc[1] ^ acc[2] ^ acc[3]) == 0x9e3779b9u) *sink = 1;
+}
+
+int main() {
+    const long long nq = 32768, rs = 37504LL * 2;   // config #3 bf16 rows
+    const int nch = 4 * 729, rows = 36;             // 4 levels x 9 output rows
+    unsigned char *pyr;
+    float *out;
+    unsigned *sink;
+    hipMalloc(&pyr, nq * rs);
+    hipMalloc(&out, (long long)nch * nq * 4);
+    hipMalloc(&sink, 4);
+    hipMemset(pyr, 0, nq * rs);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    auto timeit = [&](const char *name, double rd, double wr, auto launch) {
+        launch();
+        hipDeviceSynchronize();
+        float best = 1e9f;
+        for (int r = 0; r < 7; ++r) {
+            hipEventRecord(e0);
+            launch();
+            hipEventRecord(e1);
+            hipEventSynchronize(e1);
+            float ms;
+            hipEventElapsedTime(&ms, e0, e1);
+            if (ms < best) best = ms;
+        }
+        printf("%-46s %7.1f us  read %5.0f MB write %5.0f MB  %6.0f GB/s  (498 MB alg -> %.3f of 8 TB/s)\n", name,
+               best * 1e3, rd / 1e6, wr / 1e6, (rd + wr) / (best * 1e-3) / 1e9, 498e6 / (best * 1e-3) / 8e12);
+    };
+    const unsigned g = (unsigned)(nq / 64);
+    const double wr = (double)nch * nq * 4;
+    for (int lpq : {0, 50, 64, 80, 100, 124}) {   // lines per query over all rows: 124 ~ 7.9 KB (today), 100 ~ 6.4 KB
+        const int lpr = lpq * 64 / rows / 4;        // lines per wave per row (4 waves share a tile's loads)
+        const double rd = (double)lpr * 4 * rows * 128 * g;
+        char nm[96];
+        snprintf(nm, sizeof nm, "4 waves, %d lines/query", lpq);
+        timeit(nm, rd, wr, [&] { k_mix<4, 0><<<g, 256>>>(pyr, out, rs, (int)nq, nch, rows, lpr, sink); });
+        snprintf(nm, sizeof nm, "4 waves nt, %d lines/query", lpq);
+        timeit(nm, rd, wr, [&] { k_mix<4, 2><<<g, 256>>>(pyr, out, rs, (int)nq, nch, rows, lpr, sink); });
+        const int lpr8 = lpq * 64 / rows / 8;
+        snprintf(nm, sizeof nm, "8 waves nt, %d lines/query", lpq);
+        timeit(nm, (double)lpr8 * 8 * rows * 128 * g, wr,
+               [&] { k_mix<8, 2><<<g, 512>>>(pyr, out, rs, (int)nq, nch, rows, lpr8, sink); });
+    }
+    hipFree(pyr);
+    hipFree(out);
+    return 0;
+}
