@@ -74,6 +74,32 @@ __device__ __forceinline__ void lds_run(const unsigned char *base, int addr, con
     }
 }
 
+// Same values with one v_perm_b32 per element: the byte selectors pick the element's two bytes from the
+// dword pair (d[i], d[i+1]) into the high half of a zeroed dword (bf16 -> f32), so the 2-byte
+// misalignment and the conversion cost one instruction instead of alignbyte + shift/and.  sel_e / sel_o:
+// selectors of the even / odd element of a pair, from the run's parity (bf16_run_selectors).
+template <int NW>
+__device__ __forceinline__ void lds_run_perm(const unsigned char *base, int addr, unsigned sel_e, unsigned sel_o,
+                                             float (&v)[NW]) {
+    constexpr int K = NW / 2;
+    const unsigned *p = reinterpret_cast<const unsigned *>(base + (addr & ~3));
+    unsigned d[K + 1];
+#pragma unroll
+    for (int i = 0; i <= K; ++i) d[i] = p[i];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        v[2 * i] = __uint_as_float(__builtin_amdgcn_perm(d[i + 1], d[i], sel_e));
+        v[2 * i + 1] = __uint_as_float(__builtin_amdgcn_perm(d[i + 1], d[i], sel_o));
+    }
+}
+// v_perm_b32 byte order: selector values 0-3 = bytes of the second source (d[i]), 4-7 = the first
+// (d[i + 1]), 0x0c = 0x00.  Even run start (odd = 0): elements at bytes (0,1) and (2,3) of d[i]; odd start:
+// bytes (2,3) of d[i] and (0,1) of d[i + 1].
+__device__ __forceinline__ void bf16_run_selectors(bool odd, unsigned &sel_e, unsigned &sel_o) {
+    sel_e = odd ? 0x03020c0cu : 0x01000c0cu;
+    sel_o = odd ? 0x05040c0cu : 0x03020c0cu;
+}
+
 template <int NW>
 __device__ __forceinline__ void lds_run(const unsigned char *base, int addr, const float *, float (&v)[NW]) {
     const float *p = reinterpret_cast<const float *>(base + addr);
@@ -328,12 +354,18 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
         // slots keep earlier, finite data, and their weights are 0.
         int voff[C::MAXCH];
         unsigned pk[C::MAXCH];
+        // chunk index -> (query, column, z-chunk) by float reciprocals: idx < 2^12 and divisors <= 40, so
+        // (idx + 0.5) / d sits >= 1/80 from an integer while the float error is < 2^-11 (no integer divides)
+        const int NCZ = NC * ZC;
+        const float inv_ncz = 1.0f / (float)NCZ, inv_zc = 1.0f / (float)ZC;
+        // byte offsets fit 32 bits (the buffer covers one tile's rows: 64 x row_stride x ES < 2^31)
+        const int rs_b = (int)A.row_stride * ES, lev_b = (int)A.off[l] * ES;
 #pragma unroll
         for (int k = 0; k < C::MAXCH; ++k) {
             const int idx = tid + k * C::THREADS;
-            const int j = idx / (NC * ZC);
-            const int rem = idx - j * (NC * ZC);
-            const int c = rem / ZC;
+            const int j = (int)(((float)idx + 0.5f) * inv_ncz);
+            const int rem = idx - j * NCZ;
+            const int c = (int)(((float)rem + 0.5f) * inv_zc);
             const int zc = rem - c * ZC;
             const bool ok = idx < nch;
             const int jj = ok ? j : 0;
@@ -347,16 +379,11 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
                 const int zs = tab[2][jj] + zc * CE, ivj = tab[3][jj], xw = tab[1][jj] + c - tab[4][jj];
                 if (!(zs < ivj + NW && zs + CE > ivj) || (unsigned)xw >= (unsigned)NW) mask = 0u;
             }
-            if (bk8) {
-                const int zs = tab[2][jj] + zc * CE, x = tab[1][jj] + c;
-                pk[k] = (ok ? (unsigned)(jj * SQ + (c * ZW + zc * CE) * ES) >> 3 : 0xffffu) | (mask << 16);
-                voff[k] = (int)(((long long)jj * A.row_stride + A.off[l] + (long long)ihj * Wl * Dpl +
-                                 ((long long)(x >> 3) * (Dpl >> 3) + (zs >> 3)) * 64 + (x & 7) * 8 + (zs & 7)) * ES);
-            } else {
-                pk[k] = (ok ? (unsigned)(jj * SQ + (c * ZW + zc * CE) * ES) >> 3 : 0xffffu) | (mask << 16);
-                voff[k] = (int)(((long long)jj * A.row_stride + A.off[l] + (long long)ihj * Wl * Dpl +
-                                 (long long)(tab[1][jj] + c) * Dpl + tab[2][jj] + zc * CE) * ES);
-            }
+            pk[k] = (ok ? (unsigned)(jj * SQ + (c * ZW + zc * CE) * ES) >> 3 : 0xffffu) | (mask << 16);
+            const int zs = tab[2][jj] + zc * CE, x = tab[1][jj] + c;
+            const int inplane = bk8 ? (((x >> 3) * (Dpl >> 3) + (zs >> 3)) * 64 + (x & 7) * 8 + (zs & 7))
+                                    : x * Dpl + zs;
+            voff[k] = jj * rs_b + lev_b + (ihj * Wl * Dpl + inplane) * ES;
         }
         auto load_plane = [&](int wp, u32x4 (&st)[C::MAXCH]) {
 #pragma unroll
@@ -383,9 +410,12 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
                 }
             }
         };
+        unsigned sel_e = 0, sel_o = 0;   // bf16: v_perm selectors of this lane's run parity (same for every column)
+        if constexpr (ES == 2) bf16_run_selectors((rz & 1) != 0, sel_e, sel_o);
         auto lerp_col = [&](int slot, int k, ZRun<n> &z) {
             float r[NW];
-            lds_run<NW>(smem + C::GUARD + slot * C::SLOT, coff[k], (const T *)nullptr, r);
+            if constexpr (ES == 2) lds_run_perm<NW>(smem + C::GUARD + slot * C::SLOT, coff[k], sel_e, sel_o, r);
+            else lds_run<NW>(smem + C::GUARD + slot * C::SLOT, coff[k], (const T *)nullptr, r);
 #pragma unroll
             for (int i = 0; i < NP; ++i)
                 z.p[i] = __builtin_elementwise_fma(f32x2{r[2 * i + 1], r[2 * i + 2]}, w1p[i],

@@ -22,11 +22,12 @@ __global__ __launch_bounds__(64 * NWV) void k_mix(const unsigned char *pyr, floa
         (void *)(pyr + q0 * rs), (short)0, (int)(64 * rs), 0x00020000);
     const int chs = nch / rows;   // channels per row step
     u32x4 acc = {0, 0, 0, 0};
-    unsigned h = blockIdx.x * 2654435761u + wave * 40503u;
     for (int r = 0; r < rows; ++r) {
         // loads: lines_per_row lines per wave per row; lane group g = lane / 8 takes lines g, g + 8, ...
         for (int li = lane >> 3; li < lines_per_row; li += 8) {
-            h = h * 1664525u + 1013904223u;
+            // a distinct pseudo-random (row, line) per (workgroup, wave, row step, line slot)
+            unsigned h = ((blockIdx.x * 64u + wave) * 64u + r) * 256u + li;
+            h ^= h >> 16; h *= 0x7feb352du; h ^= h >> 15; h *= 0x846ca68bu; h ^= h >> 16;
             const int qq = (h >> 8) & 63;
             const int line = (h >> 16) % (int)(rs / 128);
             acc ^= __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
