@@ -72,7 +72,10 @@ typedef enum {
     DVC_ERR_RUNTIME = 4       /* other HIP runtime failure */
 } dvc_status;
 
-typedef enum { DVC_F32 = 0, DVC_BF16 = 1 } dvc_dtype;
+/* DVC_F16: the reference's AMP pyramid (torch.amp.autocast('cuda') in its Trainer, trainer.py:249-252,
+ * makes CorrBlock's matmul and pyramid float16, corr.py:155-167): pack, build (v_mfma_f32_32x32x16_f16),
+ * pool, lookup (also convc1-fused) and backward; the on-the-fly entry points take F32 / BF16 only. */
+typedef enum { DVC_F32 = 0, DVC_BF16 = 1, DVC_F16 = 2 } dvc_dtype;
 
 /* Layout flag ORed into the dtype of dvc_pack_targets and the store_dtype of dvc_corr_lookup /
  * dvc_corr_lookup_proj (dvc_corr_build is layout-blind: it writes the columns in packed-target

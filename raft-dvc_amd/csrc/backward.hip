@@ -102,6 +102,12 @@ template <> __device__ __forceinline__ f32x2 load2<bf16_t>(const bf16_t *p) {
     const unsigned u = *reinterpret_cast<const unsigned *>(p);
     return f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
 }
+// fp16 operands (the AMP pyramid's packed rows) take the fp32 VALU gradient kernels: splitting the fp32
+// window gradients into fp16 hi + lo for the matrix cores would lose the small gradients to fp16's range
+template <> __device__ __forceinline__ f32x2 load2<f16_t>(const f16_t *p) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    return __builtin_convertvector(*reinterpret_cast<const h2 *>(p), f32x2);
+}
 
 // ---------------------------------------------------------------------------------
 // 1. window gradients.  Forward (lookup_tile.hip / lookup.hip): output (a, u, v) of a
@@ -1234,6 +1240,9 @@ int corr_backward(const void *packed_q, const void *packed_t, const float *coord
         return dtype == DVC_BF16                                                                                   \
                    ? backward_r<bf16_t, RR>((const bf16_t *)packed_q, (const bf16_t *)packed_t, A, lay, P, ws,     \
                                             grad_fmap1, grad_fmap2, C, s, err, errlen)                             \
+               : dtype == DVC_F16                                                                                  \
+                   ? backward_r<f16_t, RR>((const f16_t *)packed_q, (const f16_t *)packed_t, A, lay, P, ws,        \
+                                           grad_fmap1, grad_fmap2, C, s, err, errlen)                              \
                    : backward_r<float, RR>((const float *)packed_q, (const float *)packed_t, A, lay, P, ws,        \
                                            grad_fmap1, grad_fmap2, C, s, err, errlen);
     switch (radius) {

@@ -288,9 +288,27 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16(const bf16_t *__restrict_
 //   S -> global stores (t); prefetched registers -> T (tile t+1); issue loads (t+2)
 // The loads for tile t+2 are in flight for a whole tile; the stores of tile t
 // drain during tile t+1.
-template <int NCH>
-__global__ __launch_bounds__(256, 2) void k_build_bf16_2b(const bf16_t *__restrict__ Q, const bf16_t *__restrict__ T,
-                                                          bf16_t *__restrict__ corr, long long Nq, int Cp,
+// E = bf16_t (v_mfma_f32_32x32x16_bf16, bf16 store) or f16_t (v_mfma_f32_32x32x16_f16, fp16 store: the
+// reference's AMP pyramid, corr.py:155-167 under trainer.py:249-252's autocast): same tiles, same schedule.
+template <typename E> struct Mma16;
+template <> struct Mma16<bf16_t> {
+    typedef bf16x8 V;
+    typedef __bf16 P2 __attribute__((ext_vector_type(2)));
+    static __device__ __forceinline__ f32x16 mma(V a, V b, f32x16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+    }
+};
+template <> struct Mma16<f16_t> {
+    typedef _Float16 V __attribute__((ext_vector_type(8)));
+    typedef _Float16 P2 __attribute__((ext_vector_type(2)));
+    static __device__ __forceinline__ f32x16 mma(V a, V b, f32x16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+    }
+};
+
+template <int NCH, typename E>
+__global__ __launch_bounds__(256, 2) void k_build_bf16_2b(const E *__restrict__ Q, const E *__restrict__ T,
+                                                          E *__restrict__ corr, long long Nq, int Cp,
                                                           long long t_batch_rows, long long row_stride,
                                                           long long col_begin, long long col_end, int nchunk,
                                                           float scale, int stpol) {
@@ -306,8 +324,10 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16_2b(const bf16_t *__restri
     const long long qtile = blockIdx.x / nchunk;
     const int chunk = blockIdx.x % nchunk;
     const long long q0 = qtile * kBQ;
-    const bf16_t *Qb = Q + (long long)b * Nq * Cp;
-    const bf16_t *Tb = T + (long long)b * t_batch_rows * Cp;
+    using MM = Mma16<E>;
+    using V8 = typename MM::V;
+    const E *Qb = Q + (long long)b * Nq * Cp;
+    const E *Tb = T + (long long)b * t_batch_rows * Cp;
     const long long ncol_tiles = (col_end - col_begin + kBP - 1) / kBP;
     const int wp = w & 1, wq = w >> 1;
     const int h = lane >> 5, r32 = lane & 31;
@@ -330,7 +350,7 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16_2b(const bf16_t *__restri
     }
     auto issue = [&](u32x4 (&pf)[PF], long long ct) {   // clamped: past the end it re-reads the last tile
         const long long cc = ct < ncol_tiles ? ct : ncol_tiles - 1;
-        const bf16_t *tile = Tb + (col_begin + cc * kBP) * Cp;   // wave-uniform base
+        const E *tile = Tb + (col_begin + cc * kBP) * Cp;   // wave-uniform base
 #pragma unroll
         for (int i = 0; i < PF; ++i) asm_load16_s<Hidden<NCH>::value>(pf[i], tile, toff[i]);
     };
@@ -346,14 +366,14 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16_2b(const bf16_t *__restri
     issue(pfa, chunk);
     issue(pfb, chunk + nchunk);
     __syncthreads();   // query tile in LDS
-    bf16x8 bq[2][NCH / 2];
+    V8 bq[2][NCH / 2];
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int ks = 0; ks < NCH / 2; ++ks) {
             const int row = 64 * wq + 32 * j + r32;
             const int c = 2 * ks + h;
-            bq[j][ks] = __builtin_bit_cast(bf16x8, sS[row * nch + (c ^ (row & msk))]);
+            bq[j][ks] = __builtin_bit_cast(V8, sS[row * nch + (c ^ (row & msk))]);
         }
     constexpr int NSTORE = kBQ * 16 / 256;   // global stores per thread per tile
     asm volatile("s_waitcnt vmcnt(%c0)" ::"i"(PF) : "memory");   // tile 0 landed (tile 1 may fly)
@@ -385,17 +405,17 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16_2b(const bf16_t *__restri
 #pragma unroll
         for (int ks = 0; ks < NCH / 2; ++ks) {
             const int c = 2 * ks + h;
-            bf16x8 a[2];
+            V8 a[2];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 const int row = 64 * wp + 32 * i + r32;
-                a[i] = __builtin_bit_cast(bf16x8, sT[row * nch + (c ^ (row & msk))]);
+                a[i] = __builtin_bit_cast(V8, sT[row * nch + (c ^ (row & msk))]);
             }
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], bq[j][ks], acc[i][j], 0, 0, 0);
+                    acc[i][j] = MM::mma(a[i], bq[j][ks], acc[i][j]);
         }
         // staging [128 q][16 chunks of 8 cols] bf16, chunk' = chunk ^ (q & 15)
 #pragma unroll
@@ -410,14 +430,14 @@ __global__ __launch_bounds__(256, 2) void k_build_bf16_2b(const bf16_t *__restri
                     const f32x2 lo = f32x2{acc[i][j][4 * g + 0], acc[i][j][4 * g + 1]} * sc2;
                     const f32x2 hi = f32x2{acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]} * sc2;
                     u32x2 v;
-                    v[0] = __builtin_bit_cast(unsigned, __builtin_convertvector(lo, bf16x2));
-                    v[1] = __builtin_bit_cast(unsigned, __builtin_convertvector(hi, bf16x2));
+                    v[0] = __builtin_bit_cast(unsigned, __builtin_convertvector(lo, typename MM::P2));
+                    v[1] = __builtin_bit_cast(unsigned, __builtin_convertvector(hi, typename MM::P2));
                     st[(q * 16 + (pch ^ (q & 15))) * 2 + h] = v;
                 }
         __syncthreads();   // B: staging visible; every wave is done reading T(ct)
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             corr + ((long long)b * Nq + q0) * row_stride + p0, (short)0,
-            (int)(nrow * row_stride * (long long)sizeof(bf16_t)), 0x00020000);
+            (int)(nrow * row_stride * (long long)sizeof(E)), 0x00020000);
 #pragma unroll
         for (int it = 0; it < NSTORE; ++it) {
             const int id = it * 256 + t;
@@ -614,13 +634,21 @@ template __global__ void k_build_bf16<32, false, 0>(const bf16_t *, const bf16_t
 template __global__ void k_build_bf16<32, true, 0>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
                                                 long long, long long, long long, int, float);
 
-template __global__ void k_build_bf16_2b<4>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+template __global__ void k_build_bf16_2b<4, f16_t>(const f16_t *, const f16_t *, f16_t *, long long, int, long long,
                                             long long, long long, long long, int, float, int);
-template __global__ void k_build_bf16_2b<8>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+template __global__ void k_build_bf16_2b<4, bf16_t>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
                                             long long, long long, long long, int, float, int);
-template __global__ void k_build_bf16_2b<16>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+template __global__ void k_build_bf16_2b<8, f16_t>(const f16_t *, const f16_t *, f16_t *, long long, int, long long,
+                                            long long, long long, long long, int, float, int);
+template __global__ void k_build_bf16_2b<8, bf16_t>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+                                            long long, long long, long long, int, float, int);
+template __global__ void k_build_bf16_2b<16, f16_t>(const f16_t *, const f16_t *, f16_t *, long long, int, long long,
+                                            long long, long long, long long, int, float, int);
+template __global__ void k_build_bf16_2b<16, bf16_t>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
                                              long long, long long, long long, int, float, int);
-template __global__ void k_build_bf16_2b<32>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
+template __global__ void k_build_bf16_2b<32, f16_t>(const f16_t *, const f16_t *, f16_t *, long long, int, long long,
+                                            long long, long long, long long, int, float, int);
+template __global__ void k_build_bf16_2b<32, bf16_t>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
                                              long long, long long, long long, int, float, int);
 template __global__ void k_build_bf16<16, false, 1>(const bf16_t *, const bf16_t *, bf16_t *, long long, int,
                                                     long long, long long, long long, long long, int, float);

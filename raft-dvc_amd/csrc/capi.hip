@@ -30,8 +30,8 @@ template <typename T> __global__ void k_pack_queries(const float *, T *, int, in
 template <int NCH, bool STORE_F32, int ABL>
 __global__ void k_build_bf16(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long, long long, long long,
                              long long, int, float);
-template <int NCH>
-__global__ void k_build_bf16_2b(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long, long long,
+template <int NCH, typename E>
+__global__ void k_build_bf16_2b(const E *, const E *, E *, long long, int, long long, long long,
                                 long long, long long, int, float, int);
 __global__ void k_build_f32(const float *, const float *, float *, long long, int, long long, long long, long long,
                             long long, int, float);
@@ -410,6 +410,8 @@ int dvc_pack_queries(const float *fmap1, void *packed, int B, int C, int64_t Nq,
     dim3 grid((unsigned)ceil_div(Nq, 64), (unsigned)ceil_div(Cp, 32), (unsigned)B);
     if (dtype == DVC_BF16)
         k_pack_queries<bf16_t><<<grid, 256, 0, s>>>(fmap1, (bf16_t *)packed, C, Cp, Nq);
+    else if (dtype == DVC_F16)
+        k_pack_queries<f16_t><<<grid, 256, 0, s>>>(fmap1, (f16_t *)packed, C, Cp, Nq);
     else if (dtype == DVC_F32)
         k_pack_queries<float><<<grid, 256, 0, s>>>(fmap1, (float *)packed, C, Cp, Nq);
     else
@@ -429,10 +431,11 @@ int dvc_pack_targets(const float *fmap2, void *packed, float *workspace, int B, 
     if (!fmap2 || !packed || (dvc_pack_workspace_bytes(B, C, H, W, D, num_levels) > 0 && !workspace))
         return fail(DVC_ERR_INVALID, "pack_targets: null pointer");
     if (B < 1) return fail(DVC_ERR_INVALID, "pack_targets: B=%d", B);
-    if (dtype != DVC_BF16 && dtype != DVC_F32) return fail(DVC_ERR_INVALID, "pack_targets: bad dtype %d", dtype);
+    if (dtype != DVC_BF16 && dtype != DVC_F32 && dtype != DVC_F16)
+        return fail(DVC_ERR_INVALID, "pack_targets: bad dtype %d", dtype);
     hipStream_t s = (hipStream_t)stream;
     const int Cp = lay.c_pad;
-    const size_t esz = dtype == DVC_BF16 ? 2 : 4;
+    const size_t esz = dtype == DVC_F32 ? 4 : 2;
     if (num_levels <= 4 && g_pack_variant == 1) {   // one pass: every level of an 8^3 cell pooled in LDS (k_pack_pyramid,
                                                      // which also zeroes the z-padding and tail rows)
         PyrGeo g;
@@ -449,6 +452,9 @@ int dvc_pack_targets(const float *fmap2, void *packed, float *workspace, int B, 
         if (dtype == DVC_BF16) {
             if (cg32) k_pack_pyramid<bf16_t, 32><<<grid, 256, 0, s>>>(fmap2, (bf16_t *)packed, g);
             else k_pack_pyramid<bf16_t, 16><<<grid, 256, 0, s>>>(fmap2, (bf16_t *)packed, g);
+        } else if (dtype == DVC_F16) {
+            if (cg32) k_pack_pyramid<f16_t, 32><<<grid, 256, 0, s>>>(fmap2, (f16_t *)packed, g);
+            else k_pack_pyramid<f16_t, 16><<<grid, 256, 0, s>>>(fmap2, (f16_t *)packed, g);
         } else {
             if (cg32) k_pack_pyramid<float, 32><<<grid, 256, 0, s>>>(fmap2, (float *)packed, g);
             else k_pack_pyramid<float, 16><<<grid, 256, 0, s>>>(fmap2, (float *)packed, g);
@@ -476,6 +482,9 @@ int dvc_pack_targets(const float *fmap2, void *packed, float *workspace, int B, 
         if (dtype == DVC_BF16)
             k_pack_rows<bf16_t><<<grid, 256, 0, s>>>(src, (bf16_t *)packed, C, Cp, (long long)C * npos, nrows,
                                                      lay.D[l], lay.Dp[l], lay.offset[l], lay.row_stride);
+        else if (dtype == DVC_F16)
+            k_pack_rows<f16_t><<<grid, 256, 0, s>>>(src, (f16_t *)packed, C, Cp, (long long)C * npos, nrows,
+                                                    lay.D[l], lay.Dp[l], lay.offset[l], lay.row_stride);
         else
             k_pack_rows<float><<<grid, 256, 0, s>>>(src, (float *)packed, C, Cp, (long long)C * npos, nrows, lay.D[l],
                                                     lay.Dp[l], lay.offset[l], lay.row_stride);
@@ -499,7 +508,8 @@ int dvc_corr_build(const void *packed_q, const void *packed_t, void *corr, int B
     // bf16 tiles keep [128][Cp] query and target tiles in LDS: C_pad <= 256 (160 KB per CU).  The C_pad = 256
     // fault of round 1 was k_build_bf16_2b<32> spilling the destinations of its hidden prefetch loads; those
     // instances now use compiler-visible loads (build_gemm.hip, Hidden<NCH>).
-    if (in_dtype == DVC_BF16 && Cp > 256) return fail(DVC_ERR_UNSUPPORTED, "build: bf16 C=%d > 256 not supported", C);
+    if (in_dtype != DVC_F32 && Cp > 256)
+        return fail(DVC_ERR_UNSUPPORTED, "build: 16-bit C=%d > 256 not supported", C);
     if (Cp > 1024) return fail(DVC_ERR_UNSUPPORTED, "build: C=%d > 1024 not supported", C);
     const float scale = 1.0f / sqrtf((float)C);   // corr / sqrt(C) (corr.py:165)
     hipStream_t s = (hipStream_t)stream;
@@ -507,10 +517,29 @@ int dvc_corr_build(const void *packed_q, const void *packed_t, void *corr, int B
     // column chunks per query tile: 8 (one per XCD: blocks b, b + 8, ... share an XCD and stream the same
     // eighth of the targets through its L2), doubled while the grid is short of 4 workgroups per CU (one
     // rank's slab: 32 query tiles at config #3 / 8 GPUs) and every chunk keeps >= 2 column tiles
-    const long long qtiles = ceil_div(Nq, in_dtype == DVC_BF16 ? 128 : 64) * B;
+    const long long qtiles = ceil_div(Nq, in_dtype == DVC_F32 ? 64 : 128) * B;
     long long nch = 8;
     while (qtiles * nch < 1024 && nch * 4 <= ncol_tiles && nch < 64) nch *= 2;
     const int nchunk = (int)std::min<long long>(nch, ncol_tiles);
+    if (in_dtype == DVC_F16) {   // the AMP pyramid: fp16 operands on v_mfma_f32_32x32x16_f16, fp16 store
+        if (store_dtype != DVC_F16) return fail(DVC_ERR_UNSUPPORTED, "build: float16 inputs need a float16 store");
+        dim3 grid((unsigned)(ceil_div(Nq, 128) * nchunk), 1, (unsigned)B);
+        const size_t lds2 = (size_t)128 * std::max(Cp, 128) * 2 + (size_t)128 * Cp * 2;
+        auto launch2 = [&](auto kern) {
+            (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            kern<<<grid, 256, lds2, s>>>((const f16_t *)packed_q, (const f16_t *)packed_t, (f16_t *)corr, Nq, Cp,
+                                         lay.row_stride, lay.row_stride, col_begin, col_end, nchunk, scale,
+                                         g_build_stpol);
+        };
+        switch (Cp / 8) {
+        case 4: launch2(k_build_bf16_2b<4, f16_t>); break;
+        case 8: launch2(k_build_bf16_2b<8, f16_t>); break;
+        case 16: launch2(k_build_bf16_2b<16, f16_t>); break;
+        case 32: launch2(k_build_bf16_2b<32, f16_t>); break;
+        default: return fail(DVC_ERR_UNSUPPORTED, "build: C=%d not supported on the fp16 path", C);
+        }
+        return check_launch("corr_build");
+    }
     if (in_dtype == DVC_BF16) {
         if (store_dtype != DVC_BF16 && store_dtype != DVC_F32) return fail(DVC_ERR_INVALID, "build: bad store dtype");
         const size_t lds = (size_t)128 * Cp * 2 + std::max<size_t>((size_t)128 * Cp * 2, 32768);
@@ -530,10 +559,10 @@ int dvc_corr_build(const void *packed_q, const void *packed_t, void *corr, int B
                                              g_build_stpol);
             };
             switch (Cp / 8) {
-            case 4: launch2(k_build_bf16_2b<4>); break;
-            case 8: launch2(k_build_bf16_2b<8>); break;
-            case 16: launch2(k_build_bf16_2b<16>); break;
-            case 32: launch2(k_build_bf16_2b<32>); break;
+            case 4: launch2(k_build_bf16_2b<4, bf16_t>); break;
+            case 8: launch2(k_build_bf16_2b<8, bf16_t>); break;
+            case 16: launch2(k_build_bf16_2b<16, bf16_t>); break;
+            case 32: launch2(k_build_bf16_2b<32, bf16_t>); break;
             default: return fail(DVC_ERR_UNSUPPORTED, "build: C=%d not supported on the bf16 path", C);
             }
             return check_launch("corr_build");
@@ -586,6 +615,10 @@ int dvc_corr_pool(void *corr, int B, int64_t Nq, int H, int W, int D, int num_le
         k_corr_pool<bf16_t><<<blocks, 256, 0, s>>>((bf16_t *)corr, nrows, lay.row_stride, lay.offset[l], lay.W[l],
                                                    lay.Dp[l], lay.offset[l + 1], lay.H[l + 1], lay.W[l + 1],
                                                    lay.D[l + 1], lay.Dp[l + 1]);
+    else if (store_dtype == DVC_F16)
+        k_corr_pool<f16_t><<<blocks, 256, 0, s>>>((f16_t *)corr, nrows, lay.row_stride, lay.offset[l], lay.W[l],
+                                                  lay.Dp[l], lay.offset[l + 1], lay.H[l + 1], lay.W[l + 1],
+                                                  lay.D[l + 1], lay.Dp[l + 1]);
     else if (store_dtype == DVC_F32)
         k_corr_pool<float><<<blocks, 256, 0, s>>>((float *)corr, nrows, lay.row_stride, lay.offset[l], lay.W[l],
                                                   lay.Dp[l], lay.offset[l + 1], lay.H[l + 1], lay.W[l + 1],
@@ -611,12 +644,14 @@ int dvc_corr_lookup(const void *corr, const float *coords, float *out, int B, in
     store_dtype &= ~DVC_BRICKED;
     LookupArgs A;
     fill_lookup_args(A, lay, corr, coords, out, B, Nq, radius, convention);
-    if (store_dtype != DVC_BF16 && store_dtype != DVC_F32) return fail(DVC_ERR_INVALID, "lookup: bad dtype %d", store_dtype);
+    if (store_dtype != DVC_BF16 && store_dtype != DVC_F32 && store_dtype != DVC_F16)
+        return fail(DVC_ERR_INVALID, "lookup: bad dtype %d", store_dtype);
+    const size_t esz = store_dtype == DVC_F32 ? 4 : 2;
     if (bricked) {   // only the tile kernel reads bricked levels
         A.brick = dvc_bricked_levels(&lay);
         bool generic_brick = false;
         for (int l = 0; l < lay.num_levels; ++l) generic_brick |= ((A.brick >> l) & 1) && A.generic[l];
-        if (lookup_variant() != 2 || !tile_ok(A, store_dtype == DVC_BF16 ? 2 : 4) || generic_brick)
+        if (lookup_variant() != 2 || !tile_ok(A, esz) || generic_brick)
             return fail(DVC_ERR_UNSUPPORTED, "lookup: a DVC_BRICKED pyramid needs the tile kernel (radius 1..6, "
                                              "no legacy W != D bricked level, lookup_variant 2)");
     }
@@ -624,6 +659,7 @@ int dvc_corr_lookup(const void *corr, const float *coords, float *out, int B, in
     const unsigned blocks = (unsigned)ceil_div(items, 4);
     hipStream_t s = (hipStream_t)stream;
     if (store_dtype == DVC_BF16) launch_lookup<bf16_t>(A, blocks, s);
+    else if (store_dtype == DVC_F16) launch_lookup<f16_t>(A, blocks, s);
     else launch_lookup<float>(A, blocks, s);
     if ((rc = check_launch("corr_lookup"))) return rc;
     if (radius >= 1 && radius <= 6) {   // legacy levels with W != D: per-output kernel, one launch per level
@@ -633,6 +669,7 @@ int dvc_corr_lookup(const void *corr, const float *coords, float *out, int B, in
             G.l0 = l; G.nl = 1;
             const unsigned gb = (unsigned)ceil_div((long long)G.nach * B * G.nqb, 4);
             if (store_dtype == DVC_BF16) k_lookup_generic<bf16_t><<<gb, 256, 0, s>>>(G);
+            else if (store_dtype == DVC_F16) k_lookup_generic<f16_t><<<gb, 256, 0, s>>>(G);
             else k_lookup_generic<float><<<gb, 256, 0, s>>>(G);
             if ((rc = check_launch("corr_lookup_generic"))) return rc;
         }
@@ -677,7 +714,7 @@ int dvc_corr_lookup_proj(const void *corr, const float *coords, const void *pack
         return fail(DVC_ERR_INVALID, "lookup_proj: bad convention %d", convention);
     const bool bricked = (store_dtype & DVC_BRICKED) != 0;
     store_dtype &= ~DVC_BRICKED;
-    if (store_dtype != DVC_BF16 && store_dtype != DVC_F32)
+    if (store_dtype != DVC_BF16 && store_dtype != DVC_F32 && store_dtype != DVC_F16)
         return fail(DVC_ERR_INVALID, "lookup_proj: bad dtype %d", store_dtype);
     LookupArgs A;
     fill_lookup_args(A, lay, corr, coords, nullptr, B, Nq, radius, convention);
@@ -686,7 +723,7 @@ int dvc_corr_lookup_proj(const void *corr, const float *coords, const void *pack
         if (A.generic[l] && !A.zero[l])
             return fail(DVC_ERR_UNSUPPORTED, "lookup_proj: legacy level %d with W != D (%d, %d)", l, lay.W[l],
                         lay.D[l]);
-    if (!tile_ok(A, store_dtype == DVC_BF16 ? 2 : 4))
+    if (!tile_ok(A, store_dtype == DVC_F32 ? 4 : 2))
         return fail(DVC_ERR_UNSUPPORTED, "lookup_proj: rows of %lld elements too wide for the tile kernel",
                     (long long)lay.row_stride);
     A.proj_w = packed_w; A.proj_b = bias; A.proj_out = out;
@@ -702,6 +739,7 @@ int dvc_corr_lookup_proj(const void *corr, const float *coords, const void *pack
     default: k_lookup_tile<T, 4, true, 0, true, 0><<<blocks, threads, 0, s>>>(A); break;       \
     }
     if (store_dtype == DVC_BF16) { DVC_PROJ_LAUNCH(bf16_t) }
+    else if (store_dtype == DVC_F16) { DVC_PROJ_LAUNCH(f16_t) }
     else { DVC_PROJ_LAUNCH(float) }
 #undef DVC_PROJ_LAUNCH
     return check_launch("corr_lookup_proj");
@@ -745,7 +783,8 @@ int dvc_corr_backward(const void *packed_q, const void *packed_t, const float *c
     if (B < 1 || Nq < 1) return fail(DVC_ERR_INVALID, "corr_backward: B=%d Nq=%lld", B, (long long)Nq);
     if (convention != DVC_FIXED && convention != DVC_LEGACY)
         return fail(DVC_ERR_INVALID, "corr_backward: bad convention %d", convention);
-    if (dtype != DVC_BF16 && dtype != DVC_F32) return fail(DVC_ERR_INVALID, "corr_backward: bad dtype %d", dtype);
+    if (dtype != DVC_BF16 && dtype != DVC_F32 && dtype != DVC_F16)
+        return fail(DVC_ERR_INVALID, "corr_backward: bad dtype %d", dtype);
     return corr_backward(packed_q, packed_t, coords, grad_out, grad_fmap1, grad_fmap2, workspace, B, Nq, C, lay, radius,
                          convention, dtype, (hipStream_t)stream, g_err, sizeof(g_err));
 }

@@ -11,6 +11,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned short bf16_t;   // storage type of one bf16 value
+typedef _Float16 f16_t;          // storage type of one fp16 value (the AMP pyramid, trainer.py:249-252)
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 namespace dvc {
@@ -41,6 +42,22 @@ __device__ __forceinline__ f32x2 splat2(float p) {
 __device__ __forceinline__ float bf16_bits_to_f32(unsigned int h) { return __uint_as_float(h << 16); }
 
 __device__ __forceinline__ bf16_t f32_to_bf16(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+
+// 16-bit storage types (bf16_t, f16_t): two values (round to nearest even) packed into one dword, low first,
+// and one value's 16 bits (low half of h) widened to float.
+template <typename T> __device__ __forceinline__ unsigned pack2_16(float a, float b);
+template <> __device__ __forceinline__ unsigned pack2_16<bf16_t>(float a, float b) {
+    return (unsigned)f32_to_bf16(a) | ((unsigned)f32_to_bf16(b) << 16);
+}
+template <> __device__ __forceinline__ unsigned pack2_16<f16_t>(float a, float b) {
+    return (unsigned)__builtin_bit_cast(unsigned short, (f16_t)a) |
+           ((unsigned)__builtin_bit_cast(unsigned short, (f16_t)b) << 16);
+}
+template <typename T> __device__ __forceinline__ float bits16_to_f32(unsigned h);
+template <> __device__ __forceinline__ float bits16_to_f32<bf16_t>(unsigned h) { return __uint_as_float(h << 16); }
+template <> __device__ __forceinline__ float bits16_to_f32<f16_t>(unsigned h) {
+    return (float)__builtin_bit_cast(f16_t, (unsigned short)(h & 0xffffu));
+}
 
 // Arguments of the lookup kernels (materialised pyramid or fused window buffer).
 // A launch covers queries [q0, q0 + nq) of every batch element and levels
@@ -75,6 +92,10 @@ template <> struct StoreT<float> {
 template <> struct StoreT<bf16_t> {
     static __device__ __forceinline__ float load(const bf16_t *p) { return bf16_bits_to_f32(*p); }
     static __device__ __forceinline__ void store(bf16_t *p, float v) { *p = f32_to_bf16(v); }
+};
+template <> struct StoreT<f16_t> {
+    static __device__ __forceinline__ float load(const f16_t *p) { return (float)*p; }
+    static __device__ __forceinline__ void store(f16_t *p, float v) { *p = (f16_t)v; }
 };
 
 // ---------------------------------------------------------------------------

@@ -35,8 +35,8 @@ namespace dvc {
 // 16-byte loads (gfx950 global loads accept any 2-byte-aligned address).  The
 // caller guarantees the NW elements are readable (clamped addresses + the
 // DVC_CORR_GUARD_BYTES guards); out-of-range elements are cancelled by zero weights.
-template <int NW>
-__device__ __forceinline__ void load_run(const bf16_t *row, float (&v)[NW]) {
+template <int NW, typename T16>   // T16: a 16-bit storage type (bf16_t, f16_t)
+__device__ __forceinline__ void load_run(const T16 *row, float (&v)[NW]) {
     constexpr int ND = NW / 2;            // NW is even: 2R+2
     unsigned w[ND];
     int i = 0;
@@ -58,8 +58,8 @@ __device__ __forceinline__ void load_run(const bf16_t *row, float (&v)[NW]) {
     }
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
-        v[2 * j] = __uint_as_float(w[j] << 16);
-        v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+        v[2 * j] = bits16_to_f32<T16>(w[j]);
+        v[2 * j + 1] = bits16_to_f32<T16>(w[j] >> 16);
     }
 }
 
@@ -87,8 +87,8 @@ __device__ __forceinline__ unsigned sel_word(unsigned hi, unsigned lo, unsigned 
     return __builtin_amdgcn_perm(hi, lo, sel);
 }
 
-template <int NW>
-__device__ __forceinline__ void load_run_al(const bf16_t *row, int z0, float (&v)[NW]) {
+template <int NW, typename T16>
+__device__ __forceinline__ void load_run_al(const T16 *row, int z0, float (&v)[NW]) {
     constexpr int NCH = (7 + NW + 7) / 8;
     const int za = z0 & ~7;
     const unsigned s = (unsigned)(z0 - za);
@@ -109,8 +109,8 @@ __device__ __forceinline__ void load_run_al(const bf16_t *row, int z0, float (&v
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
         const unsigned o = __builtin_amdgcn_alignbyte(w[j + 1], w[j], bs);
-        v[2 * j] = __uint_as_float(o << 16);
-        v[2 * j + 1] = __uint_as_float(o & 0xffff0000u);
+        v[2 * j] = bits16_to_f32<T16>(o);
+        v[2 * j + 1] = bits16_to_f32<T16>(o >> 16);
     }
 }
 
@@ -137,11 +137,11 @@ __device__ __forceinline__ void load_run_al(const float *row, int z0, float (&v)
 
 // Raw run containers: the prefetched runs stay packed (bf16: NW/2 dwords) until the
 // z-lerp consumes them, halving the registers the prefetch needs.
-template <typename T, int NW> struct Raw;
-template <int NW> struct Raw<bf16_t, NW> {
+template <typename T, int NW, bool W16 = sizeof(T) == 2> struct Raw;
+template <typename T, int NW> struct Raw<T, NW, true> {   // 16-bit storage (bf16_t, f16_t)
     static constexpr int K = NW / 2;
     unsigned w[K];
-    __device__ __forceinline__ void load(const bf16_t *row) {
+    __device__ __forceinline__ void load(const T *row) {
         int i = 0;
 #pragma unroll
         for (; i + 4 <= K; i += 4) {
@@ -160,7 +160,7 @@ template <int NW> struct Raw<bf16_t, NW> {
             w[K - 1] = x;
         }
     }
-    __device__ __forceinline__ void load_al(const bf16_t *row, int z0) {
+    __device__ __forceinline__ void load_al(const T *row, int z0) {
         constexpr int NCH = (7 + NW + 7) / 8;
         const int za = z0 & ~7;
         const unsigned s = (unsigned)(z0 - za);
@@ -181,10 +181,10 @@ template <int NW> struct Raw<bf16_t, NW> {
         for (int j = 0; j < K; ++j) w[j] = __builtin_amdgcn_alignbyte(t[j + 1], t[j], bs);
     }
     __device__ __forceinline__ float get(int j) const {
-        return (j & 1) ? __uint_as_float(w[j >> 1] & 0xffff0000u) : __uint_as_float(w[j >> 1] << 16);
+        return (j & 1) ? bits16_to_f32<T>(w[j >> 1] >> 16) : bits16_to_f32<T>(w[j >> 1]);
     }
 };
-template <int NW> struct Raw<float, NW> {
+template <int NW> struct Raw<float, NW, false> {
     float w[NW];
     __device__ __forceinline__ void load(const float *row) { load_run<NW>(row, w); }
     __device__ __forceinline__ void load_al(const float *row, int z0) { load_run_al<NW>(row, z0, w); }
@@ -427,6 +427,8 @@ DVC_LOOKUP_INST(float, 1) DVC_LOOKUP_INST(float, 2) DVC_LOOKUP_INST(float, 3)
 DVC_LOOKUP_INST(float, 4) DVC_LOOKUP_INST(float, 5) DVC_LOOKUP_INST(float, 6)
 DVC_LOOKUP_INST(bf16_t, 1) DVC_LOOKUP_INST(bf16_t, 2) DVC_LOOKUP_INST(bf16_t, 3)
 DVC_LOOKUP_INST(bf16_t, 4) DVC_LOOKUP_INST(bf16_t, 5) DVC_LOOKUP_INST(bf16_t, 6)
+DVC_LOOKUP_INST(f16_t, 1) DVC_LOOKUP_INST(f16_t, 2) DVC_LOOKUP_INST(f16_t, 3)
+DVC_LOOKUP_INST(f16_t, 4) DVC_LOOKUP_INST(f16_t, 5) DVC_LOOKUP_INST(f16_t, 6)
 template __global__ void k_lookup_win<float, 1, true, false>(LookupArgs);
 template __global__ void k_lookup_win<float, 2, true, false>(LookupArgs);
 template __global__ void k_lookup_win<float, 3, true, false>(LookupArgs);
@@ -435,6 +437,7 @@ template __global__ void k_lookup_win<float, 5, true, false>(LookupArgs);
 template __global__ void k_lookup_win<float, 6, true, false>(LookupArgs);
 template __global__ void k_lookup_generic<float>(LookupArgs);
 template __global__ void k_lookup_generic<bf16_t>(LookupArgs);
+template __global__ void k_lookup_generic<f16_t>(LookupArgs);
 
 // --- bilinear_sampler_3d on a plain (B, C, Hv, Wv, Dv) float32 volume ---------------------
 __global__ __launch_bounds__(256) void k_sample3d(const float *__restrict__ vol, const float *__restrict__ pts,

@@ -100,6 +100,23 @@ __device__ __forceinline__ void bf16_run_selectors(bool odd, unsigned &sel_e, un
     sel_o = odd ? 0x05040c0cu : 0x03020c0cu;
 }
 
+// fp16 (the AMP pyramid): realign each dword, then v_cvt_f32_f16 per half.
+template <int NW>
+__device__ __forceinline__ void lds_run(const unsigned char *base, int addr, const f16_t *, float (&v)[NW]) {
+    constexpr int K = NW / 2;
+    const unsigned *p = reinterpret_cast<const unsigned *>(base + (addr & ~3));
+    unsigned d[K + 1];
+#pragma unroll
+    for (int i = 0; i <= K; ++i) d[i] = p[i];
+    const unsigned sh = (unsigned)(addr & 2);
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const unsigned w = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+        v[2 * i] = bits16_to_f32<f16_t>(w);
+        v[2 * i + 1] = bits16_to_f32<f16_t>(w >> 16);
+    }
+}
+
 template <int NW>
 __device__ __forceinline__ void lds_run(const unsigned char *base, int addr, const float *, float (&v)[NW]) {
     const float *p = reinterpret_cast<const float *>(base + addr);
@@ -410,11 +427,12 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
                 }
             }
         };
+        constexpr bool BF = std::is_same<T, bf16_t>::value;
         unsigned sel_e = 0, sel_o = 0;   // bf16: v_perm selectors of this lane's run parity (same for every column)
-        if constexpr (ES == 2) bf16_run_selectors((rz & 1) != 0, sel_e, sel_o);
+        if constexpr (BF) bf16_run_selectors((rz & 1) != 0, sel_e, sel_o);
         auto lerp_col = [&](int slot, int k, ZRun<n> &z) {
             float r[NW];
-            if constexpr (ES == 2) lds_run_perm<NW>(smem + C::GUARD + slot * C::SLOT, coff[k], sel_e, sel_o, r);
+            if constexpr (BF) lds_run_perm<NW>(smem + C::GUARD + slot * C::SLOT, coff[k], sel_e, sel_o, r);
             else lds_run<NW>(smem + C::GUARD + slot * C::SLOT, coff[k], (const T *)nullptr, r);
 #pragma unroll
             for (int i = 0; i < NP; ++i)

@@ -7,6 +7,7 @@ namespace dvc {
 #define DVC_TILE_PROJ(T, R) template __global__ void k_lookup_tile<T, R, true, 0, true, 0>(LookupArgs);
 DVC_TILE_PROJ(float, 1) DVC_TILE_PROJ(float, 2) DVC_TILE_PROJ(float, 3) DVC_TILE_PROJ(float, 4)
 DVC_TILE_PROJ(bf16_t, 1) DVC_TILE_PROJ(bf16_t, 2) DVC_TILE_PROJ(bf16_t, 3) DVC_TILE_PROJ(bf16_t, 4)
+DVC_TILE_PROJ(f16_t, 1) DVC_TILE_PROJ(f16_t, 2) DVC_TILE_PROJ(f16_t, 3) DVC_TILE_PROJ(f16_t, 4)
 
 // Weight re-layout for the PROJ instances: W (96, L (2r+1)^3) fp32, the reference's
 // convc1.weight viewed (96, L*(2r+1)^3) (update.py:222) -> fp16 in the consumer's

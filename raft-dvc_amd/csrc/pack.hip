@@ -40,10 +40,11 @@ __device__ __forceinline__ void store16(float *d, const float (&v)[16]) {
     for (int k = 0; k < 4; ++k)
         *reinterpret_cast<float4 *>(d + 4 * k) = float4{v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]};
 }
-__device__ __forceinline__ void store16(bf16_t *d, const float (&v)[16]) {
+template <typename T>
+__device__ __forceinline__ void store16(T *d, const float (&v)[16]) {   // T: a 16-bit type (bf16_t, f16_t)
     unsigned w[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) w[k] = (unsigned)f32_to_bf16(v[2 * k]) | ((unsigned)f32_to_bf16(v[2 * k + 1]) << 16);
+    for (int k = 0; k < 8; ++k) w[k] = pack2_16<T>(v[2 * k], v[2 * k + 1]);
     *reinterpret_cast<u32x4 *>(d) = u32x4{w[0], w[1], w[2], w[3]};
     *reinterpret_cast<u32x4 *>(d + 8) = u32x4{w[4], w[5], w[6], w[7]};
 }
@@ -227,8 +228,7 @@ __global__ __launch_bounds__(256) void k_pack_pyramid(const float *__restrict__ 
             } else {
                 unsigned u[4];
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    u[k] = (unsigned)f32_to_bf16(w[2 * k]) | ((unsigned)f32_to_bf16(w[2 * k + 1]) << 16);
+                for (int k = 0; k < 4; ++k) u[k] = pack2_16<T>(w[2 * k], w[2 * k + 1]);
                 *reinterpret_cast<u32x4 *>(d) = u32x4{u[0], u[1], u[2], u[3]};
             }
         }
@@ -315,22 +315,27 @@ __global__ __launch_bounds__(256) void k_pack_queries(const float *__restrict__ 
     } else {
         unsigned u[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) u[k] = (unsigned)f32_to_bf16(w[2 * k]) | ((unsigned)f32_to_bf16(w[2 * k + 1]) << 16);
+        for (int k = 0; k < 4; ++k) u[k] = pack2_16<T>(w[2 * k], w[2 * k + 1]);
         *reinterpret_cast<u32x4 *>(d) = u32x4{u[0], u[1], u[2], u[3]};
     }
 }
 
 template __global__ void k_pack_queries<float>(const float *, float *, int, int, long long);
 template __global__ void k_pack_queries<bf16_t>(const float *, bf16_t *, int, int, long long);
+template __global__ void k_pack_queries<f16_t>(const float *, f16_t *, int, int, long long);
 
 template __global__ void k_pack_pyramid<float, 16>(const float *, float *, PyrGeo);
 template __global__ void k_pack_pyramid<bf16_t, 16>(const float *, bf16_t *, PyrGeo);
 template __global__ void k_pack_pyramid<float, 32>(const float *, float *, PyrGeo);
 template __global__ void k_pack_pyramid<bf16_t, 32>(const float *, bf16_t *, PyrGeo);
+template __global__ void k_pack_pyramid<f16_t, 16>(const float *, f16_t *, PyrGeo);
+template __global__ void k_pack_pyramid<f16_t, 32>(const float *, f16_t *, PyrGeo);
 
 template __global__ void k_pack_rows<float>(const float *, float *, int, int, long long, long long, int, int,
                                             long long, long long);
 template __global__ void k_pack_rows<bf16_t>(const float *, bf16_t *, int, int, long long, long long, int, int,
                                              long long, long long);
+template __global__ void k_pack_rows<f16_t>(const float *, f16_t *, int, int, long long, long long, int, int,
+                                            long long, long long);
 
 }  // namespace dvc

@@ -55,5 +55,7 @@ template __global__ void k_corr_pool<float>(float *, long long, long long, long 
                                             int, int);
 template __global__ void k_corr_pool<bf16_t>(bf16_t *, long long, long long, long long, int, int, long long, int,
                                              int, int, int);
+template __global__ void k_corr_pool<f16_t>(f16_t *, long long, long long, long long, int, int, long long, int,
+                                            int, int, int);
 
 }  // namespace dvc

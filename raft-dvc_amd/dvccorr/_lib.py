@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DVCCORR_LIB") or os.path.join(_HERE, "libdvccorr.so")
 
 DVC_OK, DVC_ERR_INVALID, DVC_ERR_UNSUPPORTED, DVC_ERR_LAUNCH, DVC_ERR_RUNTIME = range(5)
-DVC_F32, DVC_BF16 = 0, 1
+DVC_F32, DVC_BF16, DVC_F16 = 0, 1, 2
 DVC_BRICKED = 0x100     # layout flag ORed into a dtype (include/dvccorr.h)
 DVC_FIXED, DVC_LEGACY = 0, 1
 MAX_LEVELS = 8

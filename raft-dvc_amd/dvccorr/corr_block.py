@@ -20,9 +20,11 @@ materialises the O(N^2) volume.
 
 Precision: fp32 feature maps build in exact f32 MFMA and store fp32
 (tolerance 1e-5 relative to the reference); `precision="bf16"` builds on
-bf16 MFMA and stores bf16 (tolerance 1e-2), halving the HBM traffic; the
-default follows the input dtype (fp16/bf16 inputs -> bf16), overridable with
-the DVCCORR_PRECISION environment variable.
+bf16 MFMA and stores bf16 (tolerance 1e-2), halving the HBM traffic;
+`precision="fp16"` builds on fp16 MFMA and stores fp16 -- the reference's
+pyramid under its Trainer's autocast, and the default inside an enabled CUDA
+autocast region; otherwise the default follows the input dtype (fp16 -> fp16,
+bf16 -> bf16), overridable with the DVCCORR_PRECISION environment variable.
 
 Backward: when a feature map requires grad, every call is the differentiable
 operator dvccorr::lookup_ad (library.py) whose registered autograd formula runs
@@ -54,7 +56,10 @@ __all__ = ["CorrBlock", "CorrBlockFused", "CorrBlockOnTheFly", "bilinear_sampler
            "upflow_3d", "flow_step", "make_corr_block", "resolve_precision", "pyramid_bytes", "hbm_available"]
 
 
-def resolve_precision(fmap: torch.Tensor, precision: Optional[str]) -> str:
+_CANON = {ops.DVC_F32: "fp32", ops.DVC_BF16: "bf16", ops.DVC_F16: "fp16"}
+
+
+def resolve_precision(fmap: torch.Tensor, precision: Optional[str], fp16_ok: bool = True) -> str:
     """Storage/MFMA precision of the pyramid.  Explicit argument > DVCCORR_PRECISION >
     AMP policy > input dtype.
 
@@ -62,17 +67,21 @@ def resolve_precision(fmap: torch.Tensor, precision: Optional[str]) -> str:
     torch.amp.autocast('cuda') (trainer.py:249-252), so its CorrBlock matmul and
     avg_pool3d produce an fp16 pyramid (corr.py:155-167) even though the fmaps are
     cast to float32 first (raft_dvc.py:366-367), while grid_sample autocasts back to
-    float32.  Inside an enabled CUDA autocast region this block likewise builds and
-    stores 16-bit (bf16: same 2 bytes per value, fp32 range) and returns float32
-    lookups; outside it, float32 fmaps build in exact f32."""
+    float32.  Inside an enabled CUDA autocast region (the float16 one: the reference's
+    trainer uses autocast's default dtype) this block likewise packs, builds and stores
+    fp16 (v_mfma_f32_32x32x16_f16) and returns float32 lookups; an autocast region set to
+    bfloat16 gives bf16.  Outside autocast, float32 fmaps build in exact f32.
+
+    fp16_ok=False (the on-the-fly block, whose kernels take fp32 / bf16 operands): an fp16
+    request or policy resolves to bf16 (same storage width, fp32's exponent range)."""
     if precision is None:
         precision = os.environ.get("DVCCORR_PRECISION") or None
     if precision is None and fmap.is_cuda and torch.is_autocast_enabled("cuda"):
-        precision = "bf16"
+        precision = "bf16" if torch.get_autocast_dtype("cuda") == torch.bfloat16 else "fp16"
     if precision is None:
-        precision = "fp32" if fmap.dtype == torch.float32 else "bf16"
-    ops.dtype_code(precision)
-    return "bf16" if precision in ("bf16", "bfloat16") else "fp32"
+        precision = {torch.float32: "fp32", torch.float16: "fp16"}.get(fmap.dtype, "bf16")
+    p = _CANON[ops.dtype_code(precision)]
+    return "bf16" if p == "fp16" and not fp16_ok else p
 
 
 def _wants_grad(*ts: torch.Tensor) -> bool:
@@ -91,7 +100,7 @@ def _check_backward_support(lay, C: int, radius: int, legacy: bool) -> None:
 def pyramid_bytes(B: int, C: int, H: int, W: int, D: int, num_levels: int, precision: str = "fp32") -> int:
     """HBM bytes of the materialised pyramid CorrBlock allocates (B x N rows of row_stride values)."""
     lay = layout(H, W, D, num_levels, C)
-    esz = 2 if precision == "bf16" else 4
+    esz = 4 if precision == "fp32" else 2
     return B * H * W * D * lay.row_stride * esz + 2 * ops.GUARD_BYTES
 
 
@@ -111,10 +120,10 @@ class _Block:
             raise ValueError(f"coords must be (B, 3, H, W, D) = {(B, 3, H, W, D)}; got {tuple(coords.shape)}")
 
     def _convc1_fusable(self, weight: torch.Tensor, bias: torch.Tensor, w: torch.Tensor) -> bool:
-        """The fused convc1 kernels cover a bf16 block without gradients, radius 1..4, 96 output channels and
-        no legacy level with W != D; fp32 blocks keep the reference's fp32 convc1 (update.py:246), since the
+        """The fused convc1 kernels cover a bf16 / fp16 block without gradients, radius 1..4, 96 output channels
+        and no legacy level with W != D; fp32 blocks keep the reference's fp32 convc1 (update.py:246), since the
         kernels' fp16 MFMA operands would cost ~1e-3 relative error."""
-        return (self.precision == "bf16"
+        return (self.precision in ("bf16", "fp16")
                 and not (torch.is_grad_enabled() and (weight.requires_grad or bias.requires_grad or
                                                       self._grad_fmaps is not None))
                 and 1 <= self.radius <= ops._lib.PROJ_MAX_RADIUS and w.shape[0] == ops._lib.PROJ_COUT
@@ -270,7 +279,7 @@ class CorrBlockFused(_Block):
         B, C, H, W, D = fmap1.shape
         self.shape = (B, C, H, W, D)
         self._lay = layout(H, W, D, num_levels, C)
-        self.precision = resolve_precision(fmap1, precision)
+        self.precision = resolve_precision(fmap1, precision, fp16_ok=False)
         self._dt = ops.dtype_code(self.precision)
         self._grad_fmaps = (fmap1, fmap2) if _wants_grad(fmap1, fmap2) else None
         if self._grad_fmaps is not None:

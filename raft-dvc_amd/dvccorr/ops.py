@@ -23,7 +23,7 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import DVC_BF16, DVC_BRICKED, DVC_F32, DVC_FIXED, DVC_LEGACY, bricked_levels, check, layout, lib
+from ._lib import DVC_BF16, DVC_BRICKED, DVC_F16, DVC_F32, DVC_FIXED, DVC_LEGACY, bricked_levels, check, layout, lib
 
 
 class _DtypeMap(dict):
@@ -33,7 +33,7 @@ class _DtypeMap(dict):
         return super().__getitem__(int(code) & ~DVC_BRICKED)
 
 
-_TORCH_DT = _DtypeMap({DVC_F32: torch.float32, DVC_BF16: torch.bfloat16})
+_TORCH_DT = _DtypeMap({DVC_F32: torch.float32, DVC_BF16: torch.bfloat16, DVC_F16: torch.float16})
 
 
 def dtype_code(precision: str) -> int:
@@ -41,7 +41,9 @@ def dtype_code(precision: str) -> int:
         return DVC_F32
     if precision in ("bf16", "bfloat16"):
         return DVC_BF16
-    raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
+    if precision in ("fp16", "float16", "f16", "half"):
+        return DVC_F16
+    raise ValueError(f"precision must be 'fp32', 'bf16' or 'fp16', got {precision!r}")
 
 
 def _ptr(t: torch.Tensor) -> ctypes.c_void_p:

@@ -142,7 +142,7 @@ class HipRows:
         w = weight.reshape(weight.shape[0], -1)
         generic = self.legacy and any(lw != ld and min(lh, lw, ld) > 1
                                       for lh, lw, ld in layout(H, W, D, self.L, C).levels())
-        fusable = (self.dt == ops.dtype_code("bf16") and 1 <= self.R <= ops._lib.PROJ_MAX_RADIUS
+        fusable = (self.dt in (ops.dtype_code("bf16"), ops.dtype_code("fp16")) and 1 <= self.R <= ops._lib.PROJ_MAX_RADIUS
                    and w.shape[0] == ops._lib.PROJ_COUT and not generic
                    and (self.impl == "materialised" or layout(H, W, D, self.L, C).c_pad in (32, 64, 128)))
         if not fusable:
@@ -191,7 +191,8 @@ class ShardedCorrBlock:
         self.shape = (B, C, Hs, W, D)
         self.num_levels, self.radius, self.legacy_wd_swap = num_levels, radius, legacy_wd_swap
         self.gather_output = gather_output
-        precision = resolve_precision(fmap1_slab, precision)
+        # (the on-the-fly rows take fp32 / bf16 operands only: fp16 resolves to bf16 there)
+        precision = resolve_precision(fmap1_slab, precision, fp16_ok=impl == "materialised")
         stream = torch.cuda.current_stream(fmap1_slab.device) if fmap1_slab.is_cuda else None
         if build_events is not None and stream is not None:
             e0 = torch.cuda.Event(enable_timing=True)

@@ -153,8 +153,10 @@ def test_precision_policy_host_logic(monkeypatch):
     f32, b16 = torch.zeros(1), torch.zeros(1, dtype=torch.bfloat16)
     assert dvccorr.resolve_precision(f32, None) == "fp32"
     assert dvccorr.resolve_precision(b16, None) == "bf16"
-    assert dvccorr.resolve_precision(torch.zeros(1, dtype=torch.float16), None) == "bf16"
+    assert dvccorr.resolve_precision(torch.zeros(1, dtype=torch.float16), None) == "fp16"
     assert dvccorr.resolve_precision(f32, "bf16") == "bf16"
+    assert dvccorr.resolve_precision(f32, "float16") == "fp16"
+    assert dvccorr.resolve_precision(f32, "fp16", fp16_ok=False) == "bf16"   # the on-the-fly block's operands
     monkeypatch.setenv("DVCCORR_PRECISION", "bf16")
     assert dvccorr.resolve_precision(f32, None) == "bf16"
     assert dvccorr.resolve_precision(b16, "fp32") == "fp32"

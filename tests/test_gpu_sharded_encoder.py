@@ -92,7 +92,9 @@ def _worker(rank, world, port, q):
             blk = ShardedCorrBlock(s0, s1, S, L, R, precision="bf16")
             out = blk(coords[:, :, h0:h1].contiguous())
             torch.cuda.synchronize()
-        q.put((rank, s0.cpu(), s1.cpu(), out.cpu()))
+        # numpy arrays travel as plain pickled bytes: a torch CPU tensor would be handed over as a shared-memory
+        # file descriptor, which races this process's exit (EOFError in the parent)
+        q.put((rank, s0.cpu().numpy(), s1.cpu().numpy(), out.cpu().numpy()))
     except Exception as e:   # report instead of hanging the parent
         q.put((rank, repr(e), None, None))
         raise
@@ -124,9 +126,9 @@ def test_two_ranks_on_one_device():
     assert all(p.exitcode == 0 for p in procs)
     dev = torch.device("cuda:0")
     enc, v0, v1, coords = _problem(dev)
-    s0 = torch.cat([got[r][0] for r in range(world)], dim=2).to(dev)
-    s1 = torch.cat([got[r][1] for r in range(world)], dim=2).to(dev)
-    out = torch.cat([got[r][2] for r in range(world)], dim=2).to(dev)
+    s0 = torch.cat([torch.from_numpy(got[r][0]) for r in range(world)], dim=2).to(dev)
+    s1 = torch.cat([torch.from_numpy(got[r][1]) for r in range(world)], dim=2).to(dev)
+    out = torch.cat([torch.from_numpy(got[r][2]) for r in range(world)], dim=2).to(dev)
     with torch.no_grad():
         f0, f1 = enc(torch.cat([v0, v1])).split(1)
         assert _rel(s0, f0) <= FEAT_TOL and _rel(s1, f1) <= FEAT_TOL

@@ -147,3 +147,35 @@ def test_convc1_oracle_matches_reference(case):
     f1, f2, coords, w, b, L, r, legacy = proj_inputs(g)
     ref = orc.motion_convc1(orc.corr_lookup(f1, f2, coords, L, r, legacy), w, b)
     assert orc.rel_err(ref, g["out"]) < 1e-5
+
+
+AMP_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "amp_*.npz")))
+
+
+@pytest.mark.parametrize("case", AMP_CASES)
+def test_amp_fixture_reproduced_by_restatement(case):
+    """The AMP (fp16) golden vectors (tests/golden/gen_amp_golden.py: the reference CorrBlock under
+    torch.autocast('cpu', dtype=torch.float16)) are reproduced bit for bit by oracle/torch_cpu.py under the same
+    autocast -- the restatement follows the reference's op sequence, so the fixtures are pinned here too."""
+    import torch
+    import prng
+    from oracle import torch_cpu
+    g = load_golden(case + ".npz")
+    B, C, H, W, D, L, r = (int(v) for v in g["shape"])
+    seed = int(g["seed"][0])
+    f1 = prng.normal(seed, (B, C, H, W, D))
+    f2 = prng.normal(seed + 1, (B, C, H, W, D))
+    coords = prng.flow_coords(seed + 2, B, H, W, D, float(g["max_flow"][0]))
+    legacy = bool(int(g["legacy"][0]))
+    with torch.no_grad(), torch.autocast("cpu", dtype=torch.float16):
+        if "out" in g:
+            out = torch_cpu.corr_lookup(torch.from_numpy(f1), torch.from_numpy(f2), torch.from_numpy(coords), L, r,
+                                        legacy).float().numpy()
+            assert np.array_equal(out, g["out"])
+        else:   # sampled rows of the big case: per-row build + lookup over those rows
+            rows = g["rows"]
+            pyr = torch_cpu.build_rows(torch.from_numpy(f1), torch.from_numpy(f2), L, 0, B * H * W * D)
+            out = torch_cpu.lookup_rows(pyr, torch.from_numpy(coords), r, legacy, 0, B * H * W * D).float().numpy()
+            flat = out.reshape(B, out.shape[1], -1) if out.ndim > 2 else out
+            got = np.stack([flat[q // (H * W * D), :, q % (H * W * D)] for q in rows])
+            assert orc.rel_err(got, g["out_rows"]) < 1e-6
