@@ -509,7 +509,8 @@ def main():
         lk = {"achieved": round(lk_roof, 1), "frac": round(lk_roof / HBM_PEAK_GBS, 4),
               "algorithmic_bytes_per_launch": lk_bytes, "avg_launch_ms": round(lk_avg, 4)}
         if args.precision == "fp32":
-            roof = {"kernel": "build (pack + k_build_f32, exact-f32 MFMA v_mfma_f32_32x32x2_f32)", "bound": "mfma",
+            roof = {"kernel": "build (pack + k_build_f32r, exact-f32 MFMA v_mfma_f32_32x32x2_f32, register-resident "
+                              "targets)", "bound": "mfma",
                     "achieved": round(tfs, 1), "peak": F32_PEAK_TFS, "unit": "TFLOP/s",
                     "frac": round(tfs / F32_PEAK_TFS, 4), "traffic": None, "flops_per_launch": bd_flops,
                     "avg_launch_ms": round(bd_avg, 4),

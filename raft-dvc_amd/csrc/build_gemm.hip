@@ -617,6 +617,155 @@ __global__ __launch_bounds__(256, 1) void k_build_f32(const float *__restrict__ 
     }
 }
 
+// Exact-f32 build, register-resident targets (round 3; C_pad in {32, 64, 128}).  k_build_f32 staged every
+// 128-column target tile through LDS (96 KB: one workgroup, one wave per SIMD), so each tile's epilogue,
+// barriers and stores left the matrix pipe idle (0.38 of the f32 MFMA peak at config #3's shape).  Here:
+//   * wave w owns target columns 32w..32w+31 of the tile and keeps their operands in REGISTERS: lane
+//     (h, r32) holds T[col 32w + r32][k = (CP/2) h .. (CP/2) h + CP/2) (16-byte loads, CP/8 per lane), and
+//     MFMA step s (of CP/2) feeds k = s (lane half 0) and k = CP/2 + s (lane half 1) of both operands, so
+//     every output is still one sum over all C channels in f32 (v_mfma_f32_32x32x2_f32);
+//   * the next tile's operands load into a second register set under this tile's MFMAs;
+//   * the 64-query tile stays in LDS (B operands, one ds_read_b128 per 4 steps per accumulator) next to a
+//     32 KB staging image for the epilogue: 64 KB per workgroup, two workgroups (two waves per SIMD) per CU,
+//     so one workgroup's epilogue runs under the other's MFMAs.
+template <int CP>
+__global__ __launch_bounds__(256, 2) void k_build_f32r(const float *__restrict__ Q, const float *__restrict__ T,
+                                                       float *__restrict__ corr, long long Nq,
+                                                       long long t_batch_rows, long long row_stride,
+                                                       long long col_begin, long long col_end, int nchunk,
+                                                       float scale) {
+    constexpr int KL = CP / 2;        // k values per lane half
+    constexpr int NL = KL / 4;        // 16-byte operand loads per lane per tile
+    constexpr int NCK = CP / 4;       // 16-byte chunks per query row
+    constexpr int QM = NCK - 1;       // chunk swizzle mask: chunk' = chunk ^ (row & QM)
+    __shared__ __attribute__((aligned(16))) u32x4 sQ[kFQ * NCK];
+    __shared__ __attribute__((aligned(16))) u32x4 sS[kFQ * 32];   // staging [64 q][32 chunks of 4 cols]
+    zero_guards(corr, Nq, row_stride, 4);
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int h = lane >> 5, r32 = lane & 31;
+    const int b = blockIdx.z;
+    const long long qtile = blockIdx.x / nchunk;
+    const int chunk = blockIdx.x % nchunk;
+    const long long q0 = qtile * kFQ;
+    const float *Qb = Q + (long long)b * Nq * CP;
+    const float *Tb = T + (long long)b * t_batch_rows * CP;
+    const long long ncol_tiles = (col_end - col_begin + kFP - 1) / kFP;
+    for (int id = t; id < kFQ * NCK; id += 256) {
+        const int row = id / NCK, c = id - row * NCK;
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (q0 + row < Nq) v = *reinterpret_cast<const u32x4 *>(Qb + (q0 + row) * CP + 4 * c);
+        sQ[row * NCK + (c ^ (row & QM))] = v;
+    }
+    if (chunk >= ncol_tiles) return;
+    // this lane's operand row inside a tile, and its k half
+    const int trow = 32 * w + r32, kbase = KL * h;
+    // operand loads hidden from the compiler's waitcnt bookkeeping (as in k_build_bf16_2b: it cannot carry the
+    // counts across the loop and would drain the epilogue stores with vmcnt(0) before every tile); the counted
+    // waits below name exactly the set about to be used.  Safe: the kernel does not spill (214 VGPRs at CP 128).
+    auto load_a = [&](u32x4 (&a)[NL], long long ct) {
+        const float *src = Tb + (col_begin + ct * kFP + trow) * CP + kbase;
+#pragma unroll
+        for (int i = 0; i < NL; ++i) asm_load16<true>(a[i], src + 4 * i);
+    };
+    constexpr int NST = (kFQ * 32) / 256;   // epilogue stores per thread
+    const long long nrow = Nq - q0 < kFQ ? Nq - q0 : kFQ;
+    // epilogue of one tile: scale, LDS image (chunk' = chunk ^ (q & 31)), whole 512-byte row segments out
+    auto epilogue = [&](const f32x16 (&acc)[2], long long ct) {
+        const long long p0 = col_begin + ct * kFP;
+        __syncthreads();   // the previous tile's image has been read
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int q = 32 * j + r32;
+                const int pch = 8 * w + 2 * g + h;
+                u32x4 v;
+                v[0] = __float_as_uint(acc[j][4 * g + 0] * scale);
+                v[1] = __float_as_uint(acc[j][4 * g + 1] * scale);
+                v[2] = __float_as_uint(acc[j][4 * g + 2] * scale);
+                v[3] = __float_as_uint(acc[j][4 * g + 3] * scale);
+                sS[q * 32 + (pch ^ (q & 31))] = v;
+            }
+        __syncthreads();
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            corr + ((long long)b * Nq + q0) * row_stride + p0, (short)0, (int)(nrow * row_stride * 4), 0x00020000);
+#pragma unroll
+        for (int it = 0; it < (kFQ * 32) / 256; ++it) {
+            const int id = it * 256 + t;
+            const int q = id >> 5, c = id & 31;
+            const int off = (p0 + 4 * c < col_end) ? (int)(q * row_stride * 4 + c * 16) : 0x7ffffff0;
+            __builtin_amdgcn_raw_buffer_store_b128(sS[q * 32 + (c ^ (q & 31))], rs, off, 0, 0);
+        }
+    };
+    auto mma = [&](const u32x4 (&a)[NL], f32x16 (&acc)[2]) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int k = 0; k < 16; ++k) acc[j][k] = 0.0f;
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+            u32x4 bq[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int row = 32 * j + r32, c = kbase / 4 + i;
+                bq[j] = sQ[row * NCK + (c ^ (row & QM))];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a[i][u]), __uint_as_float(bq[j][u]),
+                                                                  acc[j], 0, 0, 0);
+        }
+    };
+    u32x4 a0[NL], a1[NL];
+    long long ct = chunk;
+    __syncthreads();   // query tile in LDS (its loads were waited for by the compiler)
+    load_a(a0, ct);
+    const bool two = ct + nchunk < ncol_tiles;
+    if (two) load_a(a1, ct + nchunk);
+    // wait until the set `a` (issued before `younger` other hidden loads and `stores` epilogue stores) landed
+    auto wait_set = [&](u32x4 (&a)[NL], bool younger_loads, bool stores) {
+        if (younger_loads && stores) asm volatile("s_waitcnt vmcnt(%c0)" ::"i"(NL + NST) : "memory");
+        else if (younger_loads) asm volatile("s_waitcnt vmcnt(%c0)" ::"i"(NL) : "memory");
+        else if (stores) asm volatile("s_waitcnt vmcnt(%c0)" ::"i"(NST) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < NL; ++i) asm volatile("" : "+v"(a[i]));
+    };
+    wait_set(a0, two, false);
+    bool first = true;
+    while (true) {
+        f32x16 acc[2];
+        mma(a0, acc);
+        const bool more0 = ct + 2 * nchunk < ncol_tiles;
+        if (more0) load_a(a0, ct + 2 * nchunk);   // under the epilogue and the next MFMAs
+        epilogue(acc, ct);
+        ct += nchunk;
+        if (ct >= ncol_tiles) break;
+        // a1 was issued before a0's refill (if any) and this tile's stores
+        wait_set(a1, more0, true);
+        mma(a1, acc);
+        const bool more1 = ct + 2 * nchunk < ncol_tiles;
+        if (more1) load_a(a1, ct + 2 * nchunk);
+        epilogue(acc, ct);
+        ct += nchunk;
+        if (ct >= ncol_tiles) break;
+        wait_set(a0, more1, true);
+        first = false;
+    }
+    (void)first;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no hidden load in flight at exit
+}
+
+template __global__ void k_build_f32r<32>(const float *, const float *, float *, long long, long long, long long,
+                                          long long, long long, int, float);
+template __global__ void k_build_f32r<64>(const float *, const float *, float *, long long, long long, long long,
+                                          long long, long long, int, float);
+template __global__ void k_build_f32r<128>(const float *, const float *, float *, long long, long long, long long,
+                                           long long, long long, int, float);
+
 template __global__ void k_build_bf16<4, false, 0>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
                                                  long long, long long, long long, int, float);
 template __global__ void k_build_bf16<4, true, 0>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
