@@ -628,7 +628,10 @@ __global__ __launch_bounds__(256, 1) void k_build_f32(const float *__restrict__ 
 //   * the 64-query tile stays in LDS (B operands, one ds_read_b128 per 4 steps per accumulator) next to a
 //     32 KB staging image for the epilogue: 64 KB per workgroup, two workgroups (two waves per SIMD) per CU,
 //     so one workgroup's epilogue runs under the other's MFMAs.
-template <int CP>
+// WS (wave-private staging): each wave stages its own 32 columns x 64 queries (8 KB) and stores them as
+// 128-byte row pieces, so the tile loop has no workgroup barrier at all (the waves of a workgroup drift
+// freely and one wave's epilogue overlaps the others' MFMAs).
+template <int CP, bool WS>
 __global__ __launch_bounds__(256, 2) void k_build_f32r(const float *__restrict__ Q, const float *__restrict__ T,
                                                        float *__restrict__ corr, long long Nq,
                                                        long long t_batch_rows, long long row_stride,
@@ -670,7 +673,36 @@ __global__ __launch_bounds__(256, 2) void k_build_f32r(const float *__restrict__
     constexpr int NST = (kFQ * 32) / 256;   // epilogue stores per thread
     const long long nrow = Nq - q0 < kFQ ? Nq - q0 : kFQ;
     // epilogue of one tile: scale, LDS image (chunk' = chunk ^ (q & 31)), whole 512-byte row segments out
+    auto epilogue_ws = [&](const f32x16 (&acc)[2], long long ct) {
+        const long long p0 = col_begin + ct * kFP + 32 * w;   // this wave's 32 columns
+        u32x4 *sw = sS + w * (kFQ * 8);                         // [64 q][8 chunks of 4 cols], chunk' = c ^ (q & 7)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int q = 32 * j + r32, c = 2 * g + h;
+                u32x4 v;
+                v[0] = __float_as_uint(acc[j][4 * g + 0] * scale);
+                v[1] = __float_as_uint(acc[j][4 * g + 1] * scale);
+                v[2] = __float_as_uint(acc[j][4 * g + 2] * scale);
+                v[3] = __float_as_uint(acc[j][4 * g + 3] * scale);
+                sw[q * 8 + (c ^ (q & 7))] = v;
+            }
+        // (same wave wrote it: the compiler's lgkmcnt waits order the reads after the writes)
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            corr + ((long long)b * Nq + q0) * row_stride + p0, (short)0, (int)(nrow * row_stride * 4), 0x00020000);
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            const int q = 8 * it + (lane >> 3), c = lane & 7;
+            const int off = (p0 + 4 * c < col_end) ? (int)(q * row_stride * 4 + c * 16) : 0x7ffffff0;
+            __builtin_amdgcn_raw_buffer_store_b128(sw[q * 8 + (c ^ (q & 7))], rs, off, 0, 0);
+        }
+    };
     auto epilogue = [&](const f32x16 (&acc)[2], long long ct) {
+        if constexpr (WS) {
+            epilogue_ws(acc, ct);
+            return;
+        }
         const long long p0 = col_begin + ct * kFP;
         __syncthreads();   // the previous tile's image has been read
 #pragma unroll
@@ -759,11 +791,17 @@ __global__ __launch_bounds__(256, 2) void k_build_f32r(const float *__restrict__
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no hidden load in flight at exit
 }
 
-template __global__ void k_build_f32r<32>(const float *, const float *, float *, long long, long long, long long,
+template __global__ void k_build_f32r<32, true>(const float *, const float *, float *, long long, long long,
+                                                long long, long long, long long, int, float);
+template __global__ void k_build_f32r<32, false>(const float *, const float *, float *, long long, long long, long long,
                                           long long, long long, int, float);
-template __global__ void k_build_f32r<64>(const float *, const float *, float *, long long, long long, long long,
+template __global__ void k_build_f32r<64, true>(const float *, const float *, float *, long long, long long,
+                                                long long, long long, long long, int, float);
+template __global__ void k_build_f32r<64, false>(const float *, const float *, float *, long long, long long, long long,
                                           long long, long long, int, float);
-template __global__ void k_build_f32r<128>(const float *, const float *, float *, long long, long long, long long,
+template __global__ void k_build_f32r<128, true>(const float *, const float *, float *, long long, long long,
+                                                long long, long long, long long, int, float);
+template __global__ void k_build_f32r<128, false>(const float *, const float *, float *, long long, long long, long long,
                                            long long, long long, int, float);
 
 template __global__ void k_build_bf16<4, false, 0>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,

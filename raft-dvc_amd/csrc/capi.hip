@@ -35,7 +35,7 @@ __global__ void k_build_bf16_2b(const E *, const E *, E *, long long, int, long 
                                 long long, long long, int, float, int);
 __global__ void k_build_f32(const float *, const float *, float *, long long, int, long long, long long, long long,
                             long long, int, float);
-template <int CP>
+template <int CP, bool WS>
 __global__ void k_build_f32r(const float *, const float *, float *, long long, long long, long long, long long,
                              long long, int, float);
 template <typename T>
@@ -82,7 +82,7 @@ static thread_local int g_build_ablate = 0;       // diagnostics only: k_build_b
 // step 2.20 -> 2.11 ms -- the 2.46 GB pyramid never fits the caches it would otherwise sweep), 0 = default policy
 static thread_local int g_build_stpol = 1;
 static thread_local int g_build_variant = 1;      // 1 = two-barrier bf16-store kernel (k_build_bf16_2b), 0 = k_build_bf16
-static thread_local int g_build_f32_variant = 1;  // 1 = register-resident targets (k_build_f32r), 0 = k_build_f32
+static thread_local int g_build_f32_variant = 2;  // 2 = k_build_f32r, wave-private staging (default); 1 = k_build_f32r, workgroup staging; 0 = k_build_f32
 // fused lookup kernel where the MFMA path applies: 2 = k_fused_box 2x2x16, 8 waves (default),
 // 3 = k_fused_box 4x4x4 cubes, 8 waves, 4 = k_fused_box 2x2x16, 4 waves, 1 = k_fused_tile, 0 = two-stage VALU
 static thread_local int g_fused_variant = 2;
@@ -309,7 +309,7 @@ int dvc_set_tuning(const char *key, int value) {
         return DVC_OK;
     }
     if (!strcmp(key, "build_f32_variant")) {
-        if (value < 0 || value > 1) return fail(DVC_ERR_INVALID, "set_tuning: build_f32_variant %d", value);
+        if (value < 0 || value > 2) return fail(DVC_ERR_INVALID, "set_tuning: build_f32_variant %d", value);
         g_build_f32_variant = value;
         return DVC_OK;
     }
@@ -591,16 +591,17 @@ int dvc_corr_build(const void *packed_q, const void *packed_t, void *corr, int B
     } else if (in_dtype == DVC_F32) {
         if (store_dtype != DVC_F32)
             return fail(DVC_ERR_UNSUPPORTED, "build: float32 inputs need a float32 store");
-        if (g_build_f32_variant == 1 && (Cp == 32 || Cp == 64 || Cp == 128)) {
+        if (g_build_f32_variant >= 1 && (Cp == 32 || Cp == 64 || Cp == 128)) {
             // register-resident target operands, two workgroups per CU (k_build_f32r)
             dim3 grid((unsigned)(ceil_div(Nq, 64) * nchunk), 1, (unsigned)B);
             auto launch_r = [&](auto kern) {
                 kern<<<grid, 256, 0, s>>>((const float *)packed_q, (const float *)packed_t, (float *)corr, Nq,
                                           lay.row_stride, lay.row_stride, col_begin, col_end, nchunk, scale);
             };
-            if (Cp == 32) launch_r(k_build_f32r<32>);
-            else if (Cp == 64) launch_r(k_build_f32r<64>);
-            else launch_r(k_build_f32r<128>);
+            const bool ws = g_build_f32_variant == 2;   // wave-private staging, no workgroup barrier
+            if (Cp == 32) ws ? launch_r(k_build_f32r<32, true>) : launch_r(k_build_f32r<32, false>);
+            else if (Cp == 64) ws ? launch_r(k_build_f32r<64, true>) : launch_r(k_build_f32r<64, false>);
+            else ws ? launch_r(k_build_f32r<128, true>) : launch_r(k_build_f32r<128, false>);
             return check_launch("corr_build");
         }
         const size_t KC = std::min(Cp, 128);   // channels per LDS chunk (k_build_f32)

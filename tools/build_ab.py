@@ -42,7 +42,7 @@ nbytes = S ** 3 * sum(h * w * d for h, w, d in lay.levels()) * esz
 flops = 2.0 * S ** 6 * C
 res = {"size": S, "precision": a.precision}
 first = None
-defaults = {"build_f32_variant": 1, "build_variant": 1}
+defaults = {"build_f32_variant": 2, "build_variant": 1}
 for setting in [""] + [x for x in a.knobs.split(";") if x]:
     kv = [x.split("=") for x in setting.split(",") if x]
     for k, v in kv:
