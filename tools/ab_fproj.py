@@ -19,6 +19,8 @@ ap.add_argument("--size", type=int, default=128)
 ap.add_argument("--levels", type=int, default=2)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--ablate", default="0,1,3,7,2,4,6,8,16,24")
+ap.add_argument("--knobs", default="", help="';'-separated knob settings (key=value,...) timed at ablate 0 after the "
+                                            "ablations, outputs compared bitwise with the default's")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 S, L = a.size, a.levels
@@ -45,4 +47,22 @@ with torch.no_grad():
         res[v] = round(e0.elapsed_time(e1) / a.reps, 3)
         print(f"ablate {v}: {res[v]} ms per lookup_convc1", flush=True)
     _lib.set_tuning("fused_ablate", 0)
+    ref = blk.lookup_convc1(c, w, b).clone()
+    for setting in [x for x in a.knobs.split(";") if x]:
+        kv = [x.split("=") for x in setting.split(",")]
+        for k, v in kv:
+            _lib.set_tuning(k, int(v))
+        o = blk.lookup_convc1(c, w, b)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.reps):
+            blk.lookup_convc1(c, w, b)
+        e1.record()
+        torch.cuda.synchronize()
+        res[setting] = round(e0.elapsed_time(e1) / a.reps, 3)
+        print(f"{setting}: {res[setting]} ms per lookup_convc1, bitwise equal to default: {torch.equal(o, ref)}",
+              flush=True)
+        for k, v in kv:
+            _lib.set_tuning(k, 0)
 print(json.dumps({"size": S, "levels": L, "ms": res}))

@@ -20,22 +20,24 @@ def pick(d, prefix):
 note = "HBM bytes per launch: 2 x FETCH_SIZE + WRITE_SIZE (KB x 1024), rocprofv3 --pmc, gfx950; source: {}"
 out = {}
 m = json.load(open(os.path.join(P, "r02_pmc_mat32_f.json")))
+m3 = json.load(open(os.path.join(P, "r03", "r03_pmc_mat32.json")))
 out["materialised_bf16_32_L4_r4_n1"] = {
     "build_hbm_bytes_per_launch": hbm(pick(m, "k_build_bf16_2b")),
-    "lookup_hbm_bytes_per_launch": hbm(pick(m, "k_lookup_tile")),
-    "note": note.format("profiles/r02_pmc_mat32_f.json (DVC_BRICKED level 0)")}
+    "lookup_hbm_bytes_per_launch": hbm(pick(m3, "k_lookup_tile")),
+    "note": note.format("profiles/r03/r03_pmc_mat32.json (DVC_BRICKED level 0, round 3 lookup; build: "
+                        "profiles/r02_pmc_mat32_f.json)")}
 mp = json.load(open(os.path.join(P, "r02_pmc_mat32_convc1_f.json")))
 out["materialised_bf16_32_L4_r4_n1_convc1_fused"] = {
     "lookup_hbm_bytes_per_launch": hbm(pick(mp, "k_lookup_tile")),
     "note": note.format("profiles/r02_pmc_mat32_convc1_f.json (k_lookup_tile<PROJ>, DVC_BRICKED level 0)")}
-f = json.load(open(os.path.join(P, "r02_pmc_fused128.json")))
+f = json.load(open(os.path.join(P, "r03", "r03_pmc_fused128.json")))
 out["fused_bf16_128_L2_r4_n1"] = {
     "lookup_hbm_bytes_per_launch": hbm(pick(f, "k_fused_box")),
-    "note": note.format("profiles/r02_pmc_fused128.json")}
-fp = json.load(open(os.path.join(P, "r02_pmc_fused128_convc1.json")))
+    "note": note.format("profiles/r03/r03_pmc_fused128.json")}
+fp = json.load(open(os.path.join(P, "r03", "r03_pmc_fused128_convc1.json")))
 out["fused_bf16_128_L2_r4_n1_convc1_fused"] = {
     "lookup_hbm_bytes_per_launch": sum(hbm(pick(fp, k)) for k in ("k_otf_keys", "k_fused_proj", "k_rows_to_channels")),
-    "note": note.format("profiles/r02_pmc_fused128_convc1.json") + " (k_otf_keys + k_fused_proj + k_rows_to_channels)"}
+    "note": note.format("profiles/r03/r03_pmc_fused128_convc1.json") + " (k_otf_keys + k_fused_proj + k_rows_to_channels)"}
 old = json.load(open(os.path.join(P, "traffic.json")))
 for k, v in old.items():   # keep round-1 entries no round-2 pass replaced, marked as such
     if k not in out:
