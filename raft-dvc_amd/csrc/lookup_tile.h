@@ -38,11 +38,15 @@ namespace dvc {
 // NWV = 0: ceil(n / 3) waves of 3 output columns (the last one takes the rest); NWV > 0: NWV waves
 // with the columns dealt as evenly as possible (n = 9, NWV = 4: 3 + 2 + 2 + 2), so that two workgroups
 // put exactly two waves on each SIMD.
+// Staged chunks are 16 bytes for 16-bit pyramids and 8 bytes for fp32 ones (round 3): a run of 2r+2 fp32
+// values then spans at most 2r+4 staged values instead of 2r+8, so the fp32 plane strips shrink from
+// 41.5 KB to 31 KB and two workgroups fit a CU (one did before: 83 KB of LDS).
 template <typename T, int R, int NWV = 0> struct TileCfg {
     static constexpr int n = 2 * R + 1;
     static constexpr int NW = 2 * R + 2;                        // window planes / columns / run length
     static constexpr int ES = (int)sizeof(T);
-    static constexpr int CE = 16 / ES;                          // elements per 16-byte chunk
+    static constexpr int CB = ES == 4 ? 8 : 16;                 // bytes per staged chunk
+    static constexpr int CE = CB / ES;                          // elements per chunk
     static constexpr int ZWMAX = (NW + CE - 1 + CE - 1) / CE * CE;   // z-chunk span covering any run
     static constexpr int NWAVES = NWV > 0 ? NWV : (n + 2) / 3;
     static constexpr int COLS = NWV > 0 ? (n + NWV - 1) / NWV : 3;   // output columns of the widest wave
@@ -371,8 +375,8 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
         // slots keep earlier, finite data, and their weights are 0.
         int voff[C::MAXCH];
         unsigned pk[C::MAXCH];
-        // chunk index -> (query, column, z-chunk) by float reciprocals: idx < 2^12 and divisors <= 40, so
-        // (idx + 0.5) / d sits >= 1/80 from an integer while the float error is < 2^-11 (no integer divides)
+        // chunk index -> (query, column, z-chunk) by float reciprocals: idx < 2^12 and divisors <= 60, so
+        // (idx + 0.5) / d sits >= 1/120 from an integer while the float error is < 2^-11 (no integer divides)
         const int NCZ = NC * ZC;
         const float inv_ncz = 1.0f / (float)NCZ, inv_zc = 1.0f / (float)ZC;
         // byte offsets fit 32 bits (the buffer covers one tile's rows: 64 x row_stride x ES < 2^31)
@@ -402,28 +406,40 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
                                     : x * Dpl + zs;
             voff[k] = jj * rs_b + lev_b + (ihj * Wl * Dpl + inplane) * ES;
         }
-        auto load_plane = [&](int wp, u32x4 (&st)[C::MAXCH]) {
+        using Chunk = typename std::conditional<C::CB == 16, u32x4, u32x2>::type;
+        auto load_plane = [&](int wp, Chunk (&st)[C::MAXCH]) {
 #pragma unroll
             for (int k = 0; k < C::MAXCH; ++k) {
-                if constexpr ((ABL & 2) != 0) st[k] = u32x4{(unsigned)k, 0, 0, 0};
+                if constexpr ((ABL & 2) != 0) st[k] = Chunk{(unsigned)k};
                 else if (pk[k] & (1u << (16 + wp))) {
                     const int o = voff[k] + wp * plane_bytes;   // (bricks keep whole planes: same plane stride)
-                    if (ldpol == 2)
-                        st[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, o, 0, 2));
-                    else
-                        st[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, o, 0, 0));
+                    if constexpr (C::CB == 16) {
+                        if (ldpol == 2)
+                            st[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, o, 0, 2));
+                        else
+                            st[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, o, 0, 0));
+                    } else {
+                        if (ldpol == 2)
+                            st[k] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_in, o, 0, 2));
+                        else
+                            st[k] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_in, o, 0, 0));
+                    }
                 }
             }
         };
-        auto write_plane = [&](int slot, int wp, const u32x4 (&st)[C::MAXCH]) {
+        auto write_plane = [&](int slot, int wp, const Chunk (&st)[C::MAXCH]) {
             unsigned char *sb = smem + C::GUARD + slot * C::SLOT;
 #pragma unroll
             for (int k = 0; k < C::MAXCH; ++k) {
                 if (pk[k] & (1u << (16 + wp))) {
                     const unsigned o = (pk[k] & 0xffffu) * 8;
-                    u32x2 lo = {st[k][0], st[k][1]}, hi = {st[k][2], st[k][3]};
-                    *reinterpret_cast<u32x2 *>(sb + o) = lo;
-                    *reinterpret_cast<u32x2 *>(sb + o + 8) = hi;
+                    if constexpr (C::CB == 16) {
+                        u32x2 lo = {st[k][0], st[k][1]}, hi = {st[k][2], st[k][3]};
+                        *reinterpret_cast<u32x2 *>(sb + o) = lo;
+                        *reinterpret_cast<u32x2 *>(sb + o + 8) = hi;
+                    } else {
+                        *reinterpret_cast<u32x2 *>(sb + o) = st[k];
+                    }
                 }
             }
         };
@@ -444,7 +460,7 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
         // staged planes (relative index p = plane - a0): plane p + 2 is loaded into st[p & 1]
         // two rows before it is written
         constexpr int NPL = NA + 1;   // window planes this workgroup reads
-        u32x4 st[2][C::MAXCH];
+        Chunk st[2][C::MAXCH];
         ZRun<n> zp[NU + 1];       // z-lerped columns of the lower plane of the current row
         load_plane(a0, st[0]);
         load_plane(a0 + 1, st[1]);
