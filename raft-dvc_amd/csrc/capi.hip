@@ -74,6 +74,9 @@ static thread_local char g_err[512] = "";
 // tuning call on one host thread never changes the kernels another thread launches.
 static thread_local int g_lookup_variant = -1;   // tuning knobs (dvc_set_tuning)
 static thread_local int g_lookup_ablate = 0;
+// diagnostics: device address of a timeline buffer (16 x u64 per workgroup) for the default four-wave r = 4
+// tile instances, set as two 32-bit halves (tuning "lookup_trace_lo" / "lookup_trace_hi"; 0 = off)
+static thread_local int g_trace_lo = 0, g_trace_hi = 0;
 static thread_local int g_lookup_nt = 1;          // nontemporal output stores in the tile kernel
 static thread_local int g_lookup_order = 1;       // tile kernel level order (LookupArgs::order)
 static thread_local int g_lookup_ldpol = 0;       // tile kernel load cache policy (LookupArgs::ldpol)
@@ -129,6 +132,7 @@ static int fill_lookup_args(LookupArgs &A, const dvc_layout &lay, const void *co
     A.order = g_lookup_order;
     A.ldpol = g_lookup_ldpol;
     A.proj_w = nullptr; A.proj_b = nullptr; A.proj_out = nullptr;
+    A.trace = (unsigned long long *)(((unsigned long long)(unsigned)g_trace_hi << 32) | (unsigned)g_trace_lo);
     A.split_levels = 0;
     A.brick = 0;
     return DVC_OK;
@@ -158,8 +162,13 @@ static bool tile_ok(const LookupArgs &A, size_t esz) {
 // two chunks read 6 and 5 of the 2r+2 window planes).  Round 2 A/B (tools/ab_split.py, bitwise-equal
 // outputs): at 64 tiles ACH 5 24.9 us, no row split 26.6, ACH 3 28.0, ACH 2 31.1; at 128 tiles no row
 // split 39.1, ACH 5 41.2, ACH 3 43.6.
-static constexpr long long kSplitTiles = 512, kSplitRows = 512;
-static thread_local int g_split_ach = 5;          // rows per chunk of the row split (0 = no row split; 2, 3, 5)
+// Round 3: launches of fewer than 1024 tiles split by level too -- config #3 (512 tiles): 2048 workgroups in
+// four rounds, so the hardware dispatcher rebalances the uneven workgroup times (88-136 us with one
+// workgroup per slot, tools/trace_lookup.py); tools/ab_lookup.py, bitwise equal, 149.2 -> 145.2 us median.
+static constexpr long long kSplitTiles = 1024, kSplitRows = 512;
+static thread_local int g_split_ach = 5;
+// launches with fewer query tiles than this take one (tile, level) pair per workgroup (tuning "split_tiles")
+static thread_local long long g_split_tiles = kSplitTiles;          // rows per chunk of the row split (0 = no row split; 2, 3, 5)
 // r = 4 tile kernel: 4 = four waves of 3 + 2 + 2 + 2 output columns (default: two workgroups put two waves
 // on every SIMD), 0 = three 3-column waves.  Round 2 A/B (tools/ab_waves.py, bitwise-equal outputs, median
 // of 40 calls): config #3 bf16 151.8 -> 150.0 us, fp32 220.7 -> 213.9; one rank's slab of an 8 / 4 / 2-way
@@ -186,7 +195,7 @@ template <typename T, bool NT>
 static void launch_tile_nt(const LookupArgs &A0, hipStream_t s) {
     LookupArgs A = A0;
     const long long tiles = (long long)A.B * A.nqb;
-    A.split_levels = tiles < kSplitTiles && A.nl > 1;
+    A.split_levels = tiles < g_split_tiles && A.nl > 1;
     const int n = 2 * A.r + 1;
     const int ach = g_split_ach;
     const bool split_rows = NT && A.split_levels && tiles * A.nl < kSplitRows && n > ach && ach > 0;
@@ -206,6 +215,13 @@ static void launch_tile_nt(const LookupArgs &A0, hipStream_t s) {
     }
     if constexpr (NT) {
         if (bal) {
+            if constexpr (std::is_same<T, bf16_t>::value) {
+                if (A.trace) {   // diagnostics only: timeline stamps
+                    if (split_rows) k_lookup_tile<T, 4, true, 8, false, 5, 4><<<blocks, threads, 0, s>>>(A);
+                    else k_lookup_tile<T, 4, true, 8, false, 0, 4><<<blocks, threads, 0, s>>>(A);
+                    return;
+                }
+            }
             if (split_rows) {
                 k_lookup_tile<T, 4, true, 0, false, 5, 4><<<blocks, threads, 0, s>>>(A);
                 return;
@@ -293,6 +309,11 @@ int dvc_set_tuning(const char *key, int value) {
         g_lookup_stpol = value;
         return DVC_OK;
     }
+    if (!strcmp(key, "split_tiles")) {
+        if (value < 0) return fail(DVC_ERR_INVALID, "set_tuning: split_tiles %d", value);
+        g_split_tiles = value;
+        return DVC_OK;
+    }
     if (!strcmp(key, "split_ach")) {
         if (value != 0 && value != 2 && value != 3 && value != 5)
             return fail(DVC_ERR_INVALID, "set_tuning: split_ach %d (0, 2, 3 or 5)", value);
@@ -347,6 +368,8 @@ int dvc_set_tuning(const char *key, int value) {
         g_build_ablate = value;
         return DVC_OK;
     }
+    if (!strcmp(key, "lookup_trace_lo")) { g_trace_lo = value; return DVC_OK; }   // diagnostics only
+    if (!strcmp(key, "lookup_trace_hi")) { g_trace_hi = value; return DVC_OK; }
     if (!strcmp(key, "lookup_ablate")) {   // diagnostics only (outputs become invalid)
         g_lookup_ablate = value;
         return DVC_OK;

@@ -82,6 +82,7 @@ struct LookupArgs {
     const void *proj_w;
     const float *proj_b;
     float *proj_out;
+    unsigned long long *trace;   // diagnostics only (tile kernel ABL & 8): per-workgroup s_memrealtime stamps
 };
 
 template <typename T> struct StoreT;

@@ -256,6 +256,20 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
         }
     }
 
+    // ABL & 8 (diagnostics only): thread 0 stamps s_memrealtime (100 MHz) at checkpoints of the first level it
+    // processes into A.trace[wg * 16 + k] with a vector (buffer) store
+    const long long wg = ((long long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    int trace_level = 1;   // only the first level is traced
+    auto stamp = [&](int k) {
+        if constexpr ((ABL & 8) != 0) {
+            if (tid == 0 && (trace_level || k == 15) && k < 16)
+                __builtin_amdgcn_raw_buffer_store_b64(
+                    __builtin_bit_cast(u32x2, (unsigned long long)__builtin_amdgcn_s_memrealtime()),
+                    __builtin_amdgcn_make_buffer_rsrc(A.trace, (short)0, 0x7fffffff, 0x00020000),
+                    (int)((wg * 16 + k) * 8), 0, 0);
+        }
+    };
+    stamp(0);
     // zero the LDS once: guards and strip padding are read (with zero weight) and must be finite
     for (int i = tid * 16; i < C::LDS; i += C::THREADS * 16) *reinterpret_cast<u32x4 *>(smem + i) = u32x4{0, 0, 0, 0};
 
@@ -353,6 +367,7 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
             coff[k] = lane * SQ + (cl * ZW + rz) * ES;
         }
 
+        stamp(1);
         __syncthreads();   // previous level's LDS reads are done; table free
         if (wave == 0) {
             tab[0][lane] = min(max(ih, -2 * NW), Hl);
@@ -362,6 +377,7 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
             tab[4][lane] = iu;
         }
         __syncthreads();
+        stamp(2);
         // a bricked level (DVC_BRICKED, bit l of A.brick): voxel (y, x, z) at
         // ((y * W/8 + x/8) * Dp/8 + z/8) * 64 + (x%8) * 8 + z%8, i.e. (1, 8, 8) bricks of one 128-byte
         // line, so the strip of a window plane touches lines of 8 columns x 8 z instead of 2 x 32
@@ -466,11 +482,14 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
         load_plane(a0 + 1, st[1]);
         write_plane(0, a0, st[0]);
         if (2 < NPL) load_plane(a0 + 2, st[0]);
+        stamp(3);
         __syncthreads();          // plane a0 in slot 0
+        stamp(4);
 #pragma unroll
         for (int k = 0; k <= NU; ++k) lerp_col(0, k, zp[k]);
         write_plane(1, a0 + 1, st[1]);
         __syncthreads();          // plane a0 + 1 in slot 1
+        stamp(5);
 #pragma unroll
         for (int ia = 0; ia < NA; ++ia) {
             const int a = a0 + ia;
@@ -555,6 +574,7 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
             }
             if (ia + 2 < NPL) write_plane(ia & 1, a + 2, st[ia & 1]);   // plane a+2 into the slot of plane a (read in row a-1)
             __syncthreads();
+            stamp(6 + ia);
         }
     };
 
@@ -581,7 +601,9 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
         } else {
             rows(l, std::integral_constant<int, NU_LAST>{});
         }
+        trace_level = 0;
     }
+    stamp(15);
 }
 
 }  // namespace dvc

@@ -12,5 +12,8 @@ template __global__ void k_lookup_tile<bf16_t, 4, true, 0, false, 0, 4, 0>(Looku
 template __global__ void k_lookup_tile<bf16_t, 4, true, 0, false, 0, 4, 16>(LookupArgs);
 template __global__ void k_lookup_tile<bf16_t, 4, true, 0, false, 0, 4, 18>(LookupArgs);
 template __global__ void k_lookup_tile<bf16_t, 4, true, 0, false, 0, 4, 17>(LookupArgs);
+// timeline stamps (tuning "lookup_trace", dvc_lookup_trace_buffer): the default four-wave r = 4 instances
+template __global__ void k_lookup_tile<bf16_t, 4, true, 8, false, 0, 4>(LookupArgs);
+template __global__ void k_lookup_tile<bf16_t, 4, true, 8, false, 5, 4>(LookupArgs);
 
 }  // namespace dvc

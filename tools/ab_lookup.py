@@ -43,7 +43,9 @@ b = ((torch.rand(96, generator=g) * 2 - 1) / K ** 0.5).to(dev)
 def apply(ks, reset=False):
     for item in filter(None, ks.split(",")):
         k, v = item.split("=")
-        _lib.set_tuning(k, {"lookup_stpol": -1}.get(k, 0) if reset else int(v))
+        # (reset to the library defaults, not 0: lookup_waves is 4, split_tiles 1024, lookup_stpol -1)
+        _lib.set_tuning(k, {"lookup_stpol": -1, "lookup_waves": 4, "split_tiles": 1024, "split_ach": 5,
+                            "lookup_variant": 2, "lookup_nt": 1, "lookup_order": 1}.get(k, 0) if reset else int(v))
 
 
 with torch.no_grad():
