@@ -639,6 +639,37 @@ __global__ __launch_bounds__(256) void k_cell_starts(const unsigned long long *_
 // nsplit > 1 (coarse levels: a handful of bricks, each reached by most queries): workgroup
 // (brick, split) takes the origin rows row = 4 split + wave (mod 4 nsplit) and writes its partial
 // sums to dTp[split][brick][64][Cp]; k_grad_t_reduce adds the nsplit partials in split order.
+// Deal the 64-query chunks of a brick's origin rows round-robin to the nwid waves of the brick (wave wid):
+// rows are read 64 at a time (one lane each), their chunk counts prefix-summed across the wave, and only the
+// rows holding a chunk of this wave are visited (body(row, s, e, first owned chunk)).  Round 3: dealing whole
+// ROWS to the waves left the coarse levels' few populated rows (16 of 169 at level 3 of config #3) on a few
+// waves (332 us for a 64-target level).
+template <typename Range, typename Body>
+__device__ __forceinline__ void deal_chunks(int nrows, int wid, int nwid, int lane, Range range, Body body) {
+    int gch = 0;
+    for (int g0 = 0; g0 < nrows; g0 += 64) {
+        int ms = 0, me = 0;
+        if (g0 + lane < nrows) range(g0 + lane, ms, me);
+        const int mch = (me - ms + 63) >> 6;
+        int inc = mch;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int t = __shfl_up(inc, d);
+            if (lane >= d) inc += t;
+        }
+        int c1 = wid - (gch + inc - mch) % nwid;
+        if (c1 < 0) c1 += nwid;
+        unsigned long long own = __ballot(c1 < mch);
+        gch += __builtin_amdgcn_readlane(inc, 63);
+        while (own) {
+            const int k = __builtin_ctzll(own);
+            own &= own - 1;
+            body(g0 + k, __builtin_amdgcn_readlane(ms, k), __builtin_amdgcn_readlane(me, k),
+                 __builtin_amdgcn_readlane(c1, k));
+        }
+    }
+}
+
 template <typename TT, int R>
 __global__ __launch_bounds__(256) void k_grad_t(const TT *__restrict__ Qp, const unsigned long long *__restrict__ keys,
                                                 const int *__restrict__ starts, float *__restrict__ dT,
@@ -675,15 +706,20 @@ __global__ __launch_bounds__(256) void k_grad_t(const TT *__restrict__ Qp, const
     // Queries are streamed 64 keys at a time (one coalesced key load per lane, broadcast with
     // shuffles) in groups of kTBatch partners, the loads of group k+1 in flight while group k's
     // 64 x kTBatch FMAs run: the loop is bound by its dependent gathers otherwise.
-    for (int row = 4 * split + w; row < nrows; row += 4 * nsplit) {
+    const int wid = 4 * split + w, nwid = 4 * nsplit;   // 64-query chunks dealt round-robin (deal_chunks)
+    auto range = [&](int row, int &s, int &e) {
+        const long long cb = ((long long)(oy0 + row / nox) * CX + (ox0 + row % nox)) * CZ;
+        s = starts[cb + oz0];
+        e = starts[cb + oz1 + 1];
+    };
+    deal_chunks(nrows, wid, nwid, lane, range, [&](int row, int s, int e, int c1) {
         const int oy = oy0 + row / nox, ox = ox0 + row % nox;
         const long long cbase = ((long long)oy * CX + ox) * CZ;
-        const int s = starts[cbase + oz0], e = starts[cbase + oz1 + 1];
         // window position of this lane's target for a query of origin o' = (oy, ox, ozq)
         const int py = ty - oy + nh - 1, px = tx - ox + nu - 1;
         const bool yxok = tval && (unsigned)py < (unsigned)nh && (unsigned)px < (unsigned)nu;
         const int pyx = (py * nu + px) * nv;
-        for (int base = s; base < e; base += 64) {
+        for (int base = s + 64 * c1; base < e; base += 64 * nwid) {
             const int nk = min(64, e - base);
             const unsigned long long key = lane < nk ? keys[base + lane] : 0ull;
             const int qq_l = (int)(unsigned)(key & 0xffffffffu);
@@ -719,7 +755,7 @@ __global__ __launch_bounds__(256) void k_grad_t(const TT *__restrict__ Qp, const
                 }
             }
         }
-    }
+    });
     reduce4(acc, red, w, lane);
     if (w == 0 && cok) {
         if (nsplit > 1) {
@@ -815,10 +851,16 @@ __global__ __launch_bounds__(256) void k_grad_t_mfma(const bf16_t *__restrict__ 
         for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[T][ct][i] = 0.0f;
-    for (int row = 4 * split + w; row < nrows; row += 4 * nsplit) {
+    // 64-query chunks of the brick's origin rows dealt round-robin to the 4 nsplit waves of the brick
+    const int wid = 4 * split + w, nwid = 4 * nsplit;
+    auto range = [&](int row, int &s, int &e) {
+        const long long cb = ((long long)(oy0 + row / nox) * CX + (ox0 + row % nox)) * CZ;
+        s = starts[cb + oz0];
+        e = starts[cb + oz1 + 1];
+    };
+    deal_chunks(nrows, wid, nwid, lane, range, [&](int row, int s, int e, int c1) {
         const int oy = oy0 + row / nox, ox = ox0 + row % nox;
         const long long cbase = ((long long)oy * CX + ox) * CZ;
-        const int s = starts[cbase + oz0], e = starts[cbase + oz1 + 1];
         int pyxT[2];
         bool yxT[2];
 #pragma unroll
@@ -827,7 +869,7 @@ __global__ __launch_bounds__(256) void k_grad_t_mfma(const bf16_t *__restrict__ 
             yxT[T] = tvT[T] && (unsigned)py < (unsigned)nh && (unsigned)px < (unsigned)nu;
             pyxT[T] = (py * nu + px) * nv;
         }
-        for (int base = s; base < e; base += 64) {
+        for (int base = s + 64 * c1; base < e; base += 64 * nwid) {
             const int nk = min(64, e - base);
             const unsigned long long key = lane < nk ? keys[base + lane] : 0ull;
             const int qq_l = (int)(unsigned)(key & 0xffffffffu);
@@ -874,7 +916,7 @@ __global__ __launch_bounds__(256) void k_grad_t_mfma(const bf16_t *__restrict__ 
                 }
             }
         }
-    }
+    });
     // cross-wave sum in a fixed order: waves 2, 3 -> 0, 1; wave 1 -> 0
     auto put = [&](int slot) {
 #pragma unroll
@@ -938,6 +980,8 @@ __global__ __launch_bounds__(256) void k_grad_t_reduce(const float *__restrict__
     const int y = by * 4 + (i >> 4), x = bx * 4 + ((i >> 2) & 3), z = bz * 4 + (i & 3);
     if (y >= Hl || x >= Wl || z >= Dl) return;
     f32x2 acc = {0.0f, 0.0f};
+    // split order (deterministic); the loads are independent of the running sum, so they are issued in batches
+#pragma unroll 8
     for (int sp = 0; sp < nsplit; ++sp)
         acc += *reinterpret_cast<const f32x2 *>(dTp + (((long long)sp * nbricks + brick) * 64 + i) * A.Cp + c0);
     const long long row = (long long)b * A.row_stride + A.off[l] + ((long long)y * Wl + x) * Dpl + z;
@@ -1023,11 +1067,12 @@ static void win_dims(const dvc_layout &lay, int l, int radius, bool legacy, int 
 
 // k_grad_t split factor of level l: enough (brick, split) workgroups for ~2 per CU, at most one origin
 // row per wave and split
-static int grad_t_splits(const dvc_layout &lay, int l, const int nw[3]) {
+// splits per brick: ~512 workgroups per level, each wave of a split owning >= ~1 chunk of 64 queries on
+// average (the chunks, not the origin rows, are dealt to the waves)
+static int grad_t_splits(const dvc_layout &lay, int l, long long Nq) {
     const long long bricks = (long long)((lay.H[l] + 3) / 4) * ((lay.W[l] + 3) / 4) * ((lay.D[l] + 3) / 4);
-    const long long rows = (long long)(std::min(lay.H[l], 4) + nw[0] - 1) * (std::min(lay.W[l], 4) + nw[1] - 1);
     long long sp = (512 + bricks - 1) / bricks;
-    sp = std::min(sp, std::max(1LL, rows / 4));
+    sp = std::min(sp, std::max(1LL, Nq / 256));
     return (int)std::max(1LL, std::min(sp, 256LL));
 }
 
@@ -1045,7 +1090,7 @@ static void bwd_plan(int B, long long Nq, const dvc_layout &lay, int radius, boo
         P.goff[l] = (long long)(gw / sizeof(float));
         gw += (size_t)B * Nq * P.nw[l][0] * P.nw[l][1] * P.nw[l][2] * sizeof(float);
         cells = std::max(cells, level_cells(lay, l, P.nw[l]));
-        const int sp = grad_t_splits(lay, l, P.nw[l]);
+        const int sp = grad_t_splits(lay, l, Nq);
         const long long bricks = (long long)((lay.H[l] + 3) / 4) * ((lay.W[l] + 3) / 4) * ((lay.D[l] + 3) / 4);
         if (sp > 1) part = std::max<size_t>(part, (size_t)sp * (size_t)bricks * 64 * (size_t)lay.c_pad * sizeof(float));
     }
@@ -1144,7 +1189,7 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
             k_cell_starts<<<(unsigned)((ncell + 1 + 255) / 256), 256, 0, s>>>(kout, A.Nq, ncell, starts);
             if (!launched("cell_starts")) return DVC_ERR_LAUNCH;
             const long long bricks = (long long)((A.H[l] + 3) / 4) * ((A.W[l] + 3) / 4) * ((A.D[l] + 3) / 4);
-            const int sp = grad_t_splits(lay, l, P.nw[l]);
+            const int sp = grad_t_splits(lay, l, A.Nq);
             if constexpr (std::is_same<TT, bf16_t>::value) {
                 // matrix-core path: sorted + transposed query rows, then 16-query MFMA batches
                 k_qt_sorted<<<dim3((unsigned)(P.nq_pad / 64), (unsigned)ngroups), 256, 0, s>>>(Q, kout, qt, A.Nq,
