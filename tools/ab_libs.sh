@@ -5,6 +5,6 @@ set -u
 A=$1; B=$2; shift 2
 for i in 1 2 3; do
   for L in "$A" "$B"; do
-    DVCCORR_LIB=$L timeout -k 5 120 python tools/ab_lookup.py "$@" || exit 1
+    DVCCORR_LIB=$L timeout -k 5 120 python ${SCRIPT:-tools/ab_lookup.py} "$@" || exit 1
   done
 done
