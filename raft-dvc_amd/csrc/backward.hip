@@ -41,6 +41,13 @@
 
 namespace dvc {
 
+// waves per SIMD the MFMA gradient kernels (k_grad_q_mfma, k_grad_t_mfma) are compiled for: at 1 their 256
+// VGPRs + 128 accumulators leave one wave per SIMD and every gather's latency exposed; at 2 they spill a few
+// dwords and run 13-18 % faster (round 3, tools/ab_bwd.py).  k_win_grad stays at one wave (2: 250 -> 368 us).
+#ifndef DVC_BWD_OCC
+#define DVC_BWD_OCC 2
+#endif
+
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 struct BwdArgs {
@@ -55,7 +62,31 @@ struct BwdArgs {
     long long off[DVC_MAX_LEVELS], goff[DVC_MAX_LEVELS];
     float scale;
     int cbase;   // first channel of this launch's 128-channel group (C_pad > 128: one launch per group)
+    // target-gradient pass, all levels in one sort and one launch (round 3): level l's window-origin cells are
+    // [coff[l], coff[l] + ncell_l] of one key space (the last one: windows outside the level); its workgroups
+    // are [gt_blk0[l], gt_blk0[l + 1]) of the k_grad_t launch, gt_sp[l] splits per brick, partial sums at
+    // gt_poff[l] (floats) of the split buffer; the split reduction's threads of level l start at gt_r0[l]
+    long long coff[DVC_MAX_LEVELS];
+    int gt_blk0[DVC_MAX_LEVELS + 1], gt_sp[DVC_MAX_LEVELS];
+    long long gt_poff[DVC_MAX_LEVELS], gt_r0[DVC_MAX_LEVELS + 1];
 };
+
+// (level, brick, split) of this k_grad_t workgroup (wave-uniform: from blockIdx and the level table)
+struct GtBlock {
+    int l, brick, split, nsplit;
+};
+__device__ __forceinline__ GtBlock gt_block(const BwdArgs &A) {
+    const int bx = (int)blockIdx.x;
+    int l = 0;
+    while (l + 1 < A.L && bx >= A.gt_blk0[l + 1]) ++l;
+    GtBlock g;
+    g.l = l;
+    g.nsplit = A.gt_sp[l];
+    const int local = bx - A.gt_blk0[l];
+    g.split = local % g.nsplit;
+    g.brick = local / g.nsplit;
+    return g;
+}
 
 __device__ __forceinline__ long long bw_nw3(const BwdArgs &A, int l) {
     return (long long)A.nwh[l] * A.nwu[l] * A.nwv[l];
@@ -448,35 +479,49 @@ __global__ __launch_bounds__(256) void k_transpose_targets(const bf16_t *__restr
     }
 }
 
-template <int NCT>   // channel tiles of 32 (C_pad / 32)
-__global__ __launch_bounds__(256) void k_grad_q_mfma(const bf16_t *__restrict__ Ttr, long long rows_pad,
-                                                     float *__restrict__ dQ, BwdArgs A) {
-    constexpr int NREG = 2 * NCT * 16;
-    __shared__ __attribute__((aligned(16))) float red[2][NREG][64];
-    const int lane = threadIdx.x & 63, m = lane & 31, h = lane >> 5;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+// Round 3: the workgroup's four waves split the CHANNELS (wave w = channel tile w of 32), not the rows, so a
+// wave accumulates dQ[64 queries][32 channels] in 32 registers (was [64][128] in 128 accumulators + 256 VGPRs:
+// one wave per SIMD, every gather's latency exposed).  Per (union row, 16-target z batch) all 256 threads stage
+// once, into a double-buffered LDS tile: the target rows Ttr[128 ch][16 z] (one 16-byte load per thread) and the
+// 64 queries' window gradients G[64][16 z] as bf16 hi + lo (four 4-byte loads per thread, only the window's own
+// values: a query whose window misses the row or the z batch loads nothing); the next batch's loads fly while
+// the current one's MFMAs run, one barrier per batch.  Level groups (blockIdx.y) write separate partial dQ
+// (the heavy level 0 alone, the coarse levels together), summed in a fixed order by k_unpack_sum.
+template <int NCT>   // channel tiles of 32 (C_pad / 32, <= 4 per launch)
+__global__ __launch_bounds__(256, 4) void k_grad_q_mfma(const bf16_t *__restrict__ Ttr, long long rows_pad,
+                                                        float *__restrict__ dQp, long long part_stride, BwdArgs A) {
+    __shared__ __attribute__((aligned(16))) bf16_t Tl[2][128][16];   // [buf][channel][z]
+    __shared__ __attribute__((aligned(16))) bf16_t Gh[2][64][16];    // [buf][query][z], hi part
+    __shared__ __attribute__((aligned(16))) bf16_t Gl[2][64][16];    // lo part
+    const int tid = threadIdx.x, lane = tid & 63, m = lane & 31, h = lane >> 5;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nbz = (A.Dq + 3) >> 2, nbx = (A.Wq + 3) >> 2, nby = (A.Hq + 3) >> 2;
     int t = blockIdx.x;
     const int bz = t % nbz; t /= nbz;
     const int bx = t % nbx; t /= nbx;
     const int by = t % nby;
     const int b = t / nby;
-    // lane-as-query view (union bounds): query i = lane of the box
+    // level group: y = 0 level 0, y = 1 levels 1 .. L-1 (gridDim.y = 1: every level)
+    const int lg0 = gridDim.y == 1 ? 0 : (blockIdx.y == 0 ? 0 : 1);
+    const int lg1 = gridDim.y == 1 ? A.L : (blockIdx.y == 0 ? 1 : A.L);
+    // lane-as-query view (union bounds, row skipping): query i = lane of the box
     const int qy = by * 4 + (lane >> 4), qx = bx * 4 + ((lane >> 2) & 3), qz = bz * 4 + (lane & 3);
     const bool active = qy < A.Hq && qx < A.Wq && qz < A.Dq;
     const long long q = active ? ((long long)qy * A.Wq + qx) * A.Dq + qz : 0;
     float cy = 0.0f, cx = 0.0f, cz = 0.0f;
     if (active) load_coords(A.coords, b, A.Nq, q, cy, cx, cz);
-    f32x16 acc[2][NCT];
+    // staging roles: T -- channel tc = tid >> 1, z half th = tid & 1; G -- query sq = tid >> 2, z quarter sp
+    const int tc = tid >> 1, th = tid & 1;
+    const int sq = tid >> 2, sp = tid & 3;
+    const bool tcok = tc < 32 * NCT;
+    f32x16 acc[2];
 #pragma unroll
     for (int T = 0; T < 2; ++T)
 #pragma unroll
-        for (int ct = 0; ct < NCT; ++ct)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) acc[T][ct][i] = 0.0f;
+        for (int i = 0; i < 16; ++i) acc[T][i] = 0.0f;
     const int BIG = 1 << 29;
-    const bf16_t *tb = Ttr + ((long long)b * A.Cp + A.cbase) * rows_pad;   // this launch's channel group
-    for (int l = 0; l < A.L; ++l) {
+    const bf16_t *tb = Ttr + ((long long)b * A.Cp + A.cbase + tc) * rows_pad;   // this thread's staged channel
+    for (int l = lg0; l < lg1; ++l) {
         if (A.zero[l]) continue;
         const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
         const int nh = A.nwh[l], nu = A.nwu[l], nv = A.nwv[l];
@@ -489,106 +534,102 @@ __global__ __launch_bounds__(256) void k_grad_q_mfma(const bf16_t *__restrict__ 
         const int xs = max(bw_wave_min(live ? iu : BIG), 0), xe = min(bw_wave_max(live ? iu : -BIG) + nu - 1, Wl - 1);
         const int nx = xe - xs + 1;
         const int nrows = (ye >= ys && nx > 0) ? (ye - ys + 1) * nx : 0;
-        // z range of the box's windows (at most 16 + 2r wide: one or two 16-target batches per row)
         const int zlo = max(bw_wave_min(live ? iv : BIG), 0);
         const int zhi = min(bw_wave_max(live ? iv : -BIG) + nv - 1, Dl - 1);
-        // A-operand rows: queries 32 T + m
-        int ohT[2], ouT[2], ovT[2];
-        bool lvT[2];
-        const float *gT[2];
-#pragma unroll
-        for (int T = 0; T < 2; ++T) {
-            const int src = 32 * T + m;
-            ohT[T] = __shfl(ih, src); ouT[T] = __shfl(iu, src); ovT[T] = __shfl(iv, src);
-            lvT[T] = __shfl((int)live, src) != 0;
-            const long long qT = (long long)__shfl((int)q, src);
-            gT[T] = A.gwin + A.goff[l] + ((long long)b * A.Nq + qT) * bw_nw3(A, l);
-        }
-        for (int row = w; row < nrows; row += 4) {
+        const int nzb = zhi >= zlo ? (zhi - zlo + 16) >> 4 : 0;
+        // the staged query's window origin and gradient rows
+        const int gsrc = sq & 63;   // (sq < 64 always: 256 threads / 4)
+        const int oh_s = __shfl(ih, gsrc), ou_s = __shfl(iu, gsrc), ov_s = __shfl(iv, gsrc);
+        const bool lv_s = __shfl((int)live, gsrc) != 0;
+        const long long q_s = (long long)__shfl((int)q, gsrc);
+        const float *g_s = A.gwin + A.goff[l] + ((long long)b * A.Nq + q_s) * bw_nw3(A, l);
+        // iteration sequence (identical in every wave): union rows that some window of the box contains, each
+        // with its nzb z batches
+        auto row_live = [&](int row) {
             const int y = ys + row / nx, x = xs + row % nx;
-            bool rokT[2];
-            int gofT[2];
-#pragma unroll
-            for (int T = 0; T < 2; ++T) {
-                const int wy = y - ohT[T], wx = x - ouT[T];
-                rokT[T] = lvT[T] && (unsigned)wy < (unsigned)nh && (unsigned)wx < (unsigned)nu;
-                gofT[T] = (wy * nu + wx) * nv;
-            }
-            // rows of the union box that no window of the box contains
             const bool rk = live && (unsigned)(y - ih) < (unsigned)nh && (unsigned)(x - iu) < (unsigned)nu;
-            if (__ballot(rk) == 0) continue;
+            return __ballot(rk) != 0;
+        };
+        auto next_row = [&](int row) {
+            while (row < nrows && !row_live(row)) ++row;
+            return row;
+        };
+        // staged registers of one batch
+        u32x4 treg;
+        u32x2 ghr, glr;
+        auto load = [&](int row, int zb) {
+            const int y = ys + row / nx, x = xs + row % nx;
+            const int z0 = zlo + 16 * zb;
             const long long trow = A.off[l] + ((long long)y * Wl + x) * Dpl;
-            for (int z0 = zlo; z0 <= zhi; z0 += 16) {
-                bf16x8 tbv[NCT];
+            treg = u32x4{0u, 0u, 0u, 0u};
+            if (tcok) __builtin_memcpy(&treg, tb + trow + z0 + 8 * th, 16);
+            const int wy = y - oh_s, wx = x - ou_s;
+            const bool rok = lv_s && (unsigned)wy < (unsigned)nh && (unsigned)wx < (unsigned)nu;
+            const float *gr = g_s + (wy * nu + wx) * nv;
+            float g[4];
 #pragma unroll
-                for (int ct = 0; ct < NCT; ++ct) {
-                    u32x4 v;
-                    __builtin_memcpy(&v, tb + (long long)(32 * ct + m) * rows_pad + trow + z0 + 8 * h, 16);
-                    tbv[ct] = __builtin_bit_cast(bf16x8, v);
-                }
+            for (int k = 0; k < 4; ++k) {
+                const int wz = z0 + 4 * sp + k - ov_s;
+                g[k] = rok && (unsigned)wz < (unsigned)nv ? gr[wz] : 0.0f;
+            }
+            unsigned hi[4], lo[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const __bf16 hb = (__bf16)g[k];
+                hi[k] = __builtin_bit_cast(unsigned short, hb);
+                lo[k] = __builtin_bit_cast(unsigned short, (__bf16)(g[k] - (float)hb));
+            }
+            ghr = u32x2{hi[0] | (hi[1] << 16), hi[2] | (hi[3] << 16)};
+            glr = u32x2{lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16)};
+        };
+        auto store = [&](int buf) {
+            *reinterpret_cast<u32x4 *>(&Tl[buf][tc][8 * th]) = treg;
+            *reinterpret_cast<u32x2 *>(&Gh[buf][sq][4 * sp]) = ghr;
+            *reinterpret_cast<u32x2 *>(&Gl[buf][sq][4 * sp]) = glr;
+        };
+        int row = nzb > 0 ? next_row(0) : nrows, zb = 0;
+        if (row >= nrows) continue;
+        __syncthreads();   // the previous level's last batch has been read
+        load(row, zb);
+        store(0);
+        __syncthreads();
+        int buf = 0;
+        while (true) {
+            // the next batch: next z batch of this row, else the next live row
+            int nrow = row, nzbi = zb + 1;
+            if (nzbi >= nzb) { nzbi = 0; nrow = next_row(row + 1); }
+            const bool more = nrow < nrows;
+            if (more) load(nrow, nzbi);
+            if (w < NCT) {
+                const bf16x8 bt = *reinterpret_cast<const bf16x8 *>(&Tl[buf][32 * w + m][8 * h]);
 #pragma unroll
                 for (int T = 0; T < 2; ++T) {
-                    const int wz0 = z0 + 8 * h - ovT[T];
-                    // the 8 window values as two 16-byte loads (neighbouring rows' values and the 256-byte
-                    // guards around dwin are read and masked): row offset clamped to the query's window
-                    const float *gp = gT[T] + (rokT[T] ? gofT[T] : 0) + wz0;
-                    float gv[8];
-                    __builtin_memcpy(gv, gp, 32);
-                    bf16x8 ghi, glo;
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        const int wz = wz0 + k;
-                        const float g = rokT[T] && (unsigned)wz < (unsigned)nv ? gv[k] : 0.0f;
-                        const __bf16 hi = (__bf16)g;
-                        ghi[k] = hi;
-                        glo[k] = (__bf16)(g - (float)hi);
-                    }
-#pragma unroll
-                    for (int ct = 0; ct < NCT; ++ct) {
-                        acc[T][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ghi, tbv[ct], acc[T][ct], 0, 0, 0);
-                        acc[T][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(glo, tbv[ct], acc[T][ct], 0, 0, 0);
-                    }
+                    const bf16x8 ah = *reinterpret_cast<const bf16x8 *>(&Gh[buf][32 * T + m][8 * h]);
+                    const bf16x8 al = *reinterpret_cast<const bf16x8 *>(&Gl[buf][32 * T + m][8 * h]);
+                    acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bt, acc[T], 0, 0, 0);
+                    acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bt, acc[T], 0, 0, 0);
                 }
             }
+            if (!more) break;
+            store(buf ^ 1);
+            __syncthreads();
+            buf ^= 1;
+            row = nrow;
+            zb = nzbi;
         }
     }
-    auto put = [&](int slot) {
-#pragma unroll
-        for (int T = 0; T < 2; ++T)
-#pragma unroll
-            for (int ct = 0; ct < NCT; ++ct)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) red[slot][(T * NCT + ct) * 16 + i][lane] = acc[T][ct][i];
-    };
-    auto add = [&](int slot) {
-#pragma unroll
-        for (int T = 0; T < 2; ++T)
-#pragma unroll
-            for (int ct = 0; ct < NCT; ++ct)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) acc[T][ct][i] += red[slot][(T * NCT + ct) * 16 + i][lane];
-    };
-    __syncthreads();
-    if (w >= 2) put(w - 2);
-    __syncthreads();
-    if (w < 2) add(w);
-    __syncthreads();
-    if (w == 1) put(0);
-    __syncthreads();
-    if (w != 0) return;
-    add(0);
-    // acc[T][ct][i] = D[query 32 T + 8 (i / 4) + 4 h + i % 4][channel 32 ct + m]
+    if (w >= NCT) return;
+    // acc[T][i] = D[query 32 T + 8 (i / 4) + 4 h + i % 4][channel 32 w + m]
+    float *dq = dQp + (long long)blockIdx.y * part_stride;
 #pragma unroll
     for (int T = 0; T < 2; ++T)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             const int qi = 32 * T + 8 * (i >> 2) + 4 * h + (i & 3);
             const int y = by * 4 + (qi >> 4), x = bx * 4 + ((qi >> 2) & 3), z = bz * 4 + (qi & 3);
-            if (y < A.Hq && x < A.Wq && z < A.Dq) {
-                float *dst = dQ + ((long long)b * A.Nq + ((long long)y * A.Wq + x) * A.Dq + z) * A.Cp + A.cbase + m;
-#pragma unroll
-                for (int ct = 0; ct < NCT; ++ct) dst[32 * ct] = acc[T][ct][i] * A.scale;
-            }
+            if (y < A.Hq && x < A.Wq && z < A.Dq)
+                dq[((long long)b * A.Nq + ((long long)y * A.Wq + x) * A.Dq + z) * A.Cp + A.cbase + 32 * w + m] =
+                    acc[T][i] * A.scale;
         }
 }
 
@@ -597,8 +638,9 @@ __global__ __launch_bounds__(256) void k_grad_q_mfma(const bf16_t *__restrict__ 
 // [0, S_l + nw - 2] exactly when the window meets the level; others sort last.
 // ---------------------------------------------------------------------------------
 template <int R>
-__global__ __launch_bounds__(256) void k_bw_keys(BwdArgs A, int b, int l, unsigned long long *__restrict__ keys) {
+__global__ __launch_bounds__(256) void k_bw_keys(BwdArgs A, int b, unsigned long long *__restrict__ keys) {
     const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
+    const int l = (int)blockIdx.y;
     if (q >= A.Nq) return;
     float cy, cx, cz;
     load_coords(A.coords, b, A.Nq, q, cy, cx, cz);
@@ -609,9 +651,10 @@ __global__ __launch_bounds__(256) void k_bw_keys(BwdArgs A, int b, int l, unsign
     const int oy = ih + A.nwh[l] - 1, ox = iu + A.nwu[l] - 1, oz = iv + A.nwv[l] - 1;
     const int CY = A.H[l] + A.nwh[l] - 1, CX = A.W[l] + A.nwu[l] - 1, CZ = A.D[l] + A.nwv[l] - 1;
     const long long ncell = (long long)CY * CX * CZ;
-    const bool in = !ax.dead && (unsigned)oy < (unsigned)CY && (unsigned)ox < (unsigned)CX && (unsigned)oz < (unsigned)CZ;
-    const long long cell = in ? ((long long)oy * CX + ox) * CZ + oz : ncell;
-    keys[q] = ((unsigned long long)cell << 32) | (unsigned long long)(unsigned)q;
+    const bool in = !A.zero[l] && !ax.dead && (unsigned)oy < (unsigned)CY && (unsigned)ox < (unsigned)CX &&
+                    (unsigned)oz < (unsigned)CZ;
+    const long long cell = A.coff[l] + (in ? ((long long)oy * CX + ox) * CZ + oz : ncell);
+    keys[(long long)l * A.Nq + q] = ((unsigned long long)cell << 32) | (unsigned long long)(unsigned)q;
 }
 
 // starts[c] = first sorted index whose cell >= c, for c in [0, ncell]: one thread per cell, a binary
@@ -673,7 +716,10 @@ __device__ __forceinline__ void deal_chunks(int nrows, int wid, int nwid, int la
 template <typename TT, int R>
 __global__ __launch_bounds__(256) void k_grad_t(const TT *__restrict__ Qp, const unsigned long long *__restrict__ keys,
                                                 const int *__restrict__ starts, float *__restrict__ dT,
-                                                float *__restrict__ dTp, int nsplit, BwdArgs A, int b, int l) {
+                                                float *__restrict__ dTp, BwdArgs A, int b) {
+    const GtBlock gb = gt_block(A);
+    const int l = gb.l, nsplit = gb.nsplit, split = gb.split, brick = gb.brick;
+    starts += A.coff[l];
     __shared__ __attribute__((aligned(16))) float gs_all[4][kTBatch][64];
     __shared__ __attribute__((aligned(16))) f32x2 red[2][64][64];
     const int lane = threadIdx.x & 63;
@@ -682,9 +728,7 @@ __global__ __launch_bounds__(256) void k_grad_t(const TT *__restrict__ Qp, const
     const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
     const int nh = A.nwh[l], nu = A.nwu[l], nv = A.nwv[l];
     const long long nw3 = bw_nw3(A, l);
-    const int nbz = (Dl + 3) >> 2, nbx = (Wl + 3) >> 2;
-    const int split = (int)(blockIdx.x % nsplit);
-    const int brick = (int)(blockIdx.x / nsplit);
+    const int nbz = (Dl + 3) >> 2, nbx = (Wl + 3) >> 2, nby = (Hl + 3) >> 2;
     int t = brick;
     const int bz = t % nbz; t /= nbz;
     const int bx = t % nbx;
@@ -714,7 +758,7 @@ __global__ __launch_bounds__(256) void k_grad_t(const TT *__restrict__ Qp, const
     };
     deal_chunks(nrows, wid, nwid, lane, range, [&](int row, int s, int e, int c1) {
         const int oy = oy0 + row / nox, ox = ox0 + row % nox;
-        const long long cbase = ((long long)oy * CX + ox) * CZ;
+        const long long cbase = ((long long)oy * CX + ox) * CZ + A.coff[l];   // (keys hold global cells)
         // window position of this lane's target for a query of origin o' = (oy, ox, ozq)
         const int py = ty - oy + nh - 1, px = tx - ox + nu - 1;
         const bool yxok = tval && (unsigned)py < (unsigned)nh && (unsigned)px < (unsigned)nu;
@@ -759,7 +803,7 @@ __global__ __launch_bounds__(256) void k_grad_t(const TT *__restrict__ Qp, const
     reduce4(acc, red, w, lane);
     if (w == 0 && cok) {
         if (nsplit > 1) {
-            float *pp = dTp + ((long long)split * gridDim.x / nsplit + brick) * 64 * A.Cp + c0;
+            float *pp = dTp + A.gt_poff[l] + ((long long)split * nbz * nbx * nby + brick) * 64 * A.Cp + c0;
 #pragma unroll
             for (int i = 0; i < 64; ++i) *reinterpret_cast<f32x2 *>(pp + (long long)i * A.Cp) = acc[i];
             return;
@@ -787,8 +831,8 @@ __global__ __launch_bounds__(256) void k_grad_t(const TT *__restrict__ Qp, const
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_qt_sorted(const bf16_t *__restrict__ Q,
                                                    const unsigned long long *__restrict__ keys,
-                                                   bf16_t *__restrict__ Qt, long long Nq, long long NqPad, int Cp,
-                                                   int b) {
+                                                   bf16_t *__restrict__ Qt, long long Nq, long long nkeys,
+                                                   long long NqPad, int Cp, int b) {
     __shared__ __attribute__((aligned(16))) bf16_t tile[64][128 + 8];
     const long long i0 = (long long)blockIdx.x * 64;
     const int cb = 128 * (int)blockIdx.y, cg = min(128, Cp - cb);   // this block's channel group
@@ -796,7 +840,7 @@ __global__ __launch_bounds__(256) void k_qt_sorted(const bf16_t *__restrict__ Q,
     for (int id = threadIdx.x; id < 64 * nch; id += 256) {
         const int r = id / nch, ch = id - r * nch;
         u32x4 v = {0u, 0u, 0u, 0u};
-        if (i0 + r < Nq) {
+        if (i0 + r < nkeys) {
             const long long q = (long long)(keys[i0 + r] & 0xffffffffull);
             v = *reinterpret_cast<const u32x4 *>(Q + ((long long)b * Nq + q) * Cp + cb + ch * 8);
         }
@@ -810,141 +854,130 @@ __global__ __launch_bounds__(256) void k_qt_sorted(const bf16_t *__restrict__ Q,
     }
 }
 
-template <int NCT>   // channel tiles of 32 (C_pad / 32)
-__global__ __launch_bounds__(256) void k_grad_t_mfma(const bf16_t *__restrict__ Qt, long long NqPad,
-                                                     const unsigned long long *__restrict__ keys,
-                                                     const int *__restrict__ starts, float *__restrict__ dT,
-                                                     float *__restrict__ dTp, int nsplit, BwdArgs A, int b, int l) {
-    constexpr int NREG = 2 * NCT * 16;   // accumulator floats per lane
-    __shared__ __attribute__((aligned(16))) float red[2][NREG][64];
-    const int lane = threadIdx.x & 63, m = lane & 31, h = lane >> 5;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+// Round 3: as k_grad_q_mfma, the four waves split the channels (wave w = channel tile w: dT[64 targets][32 ch]
+// in 32 registers, no cross-wave reduction) and every (16-query batch) is staged once per workgroup into a
+// double-buffered LDS tile: the sorted+transposed query rows Qt[128 ch][16] (one 16-byte load per thread) and
+// the 64 targets' window gradients G[64][16 queries] as bf16 hi + lo (four gathers per thread); the next
+// batch's loads fly while the current one's MFMAs run.  The 64-query chunks of the brick's origin rows are
+// dealt to the workgroups of the brick (splits).
+template <int NCT>   // channel tiles of 32 (C_pad / 32, <= 4 per launch)
+__global__ __launch_bounds__(256, 4) void k_grad_t_mfma(const bf16_t *__restrict__ Qt, long long NqPad,
+                                                        const unsigned long long *__restrict__ keys,
+                                                        const int *__restrict__ starts, float *__restrict__ dT,
+                                                        float *__restrict__ dTp, BwdArgs A, int b) {
+    const GtBlock gb = gt_block(A);
+    const int l = gb.l, nsplit = gb.nsplit, split = gb.split, brick = gb.brick;
+    starts += A.coff[l];
+    __shared__ __attribute__((aligned(16))) bf16_t Ql[2][128][16];   // [buf][channel][query]
+    __shared__ __attribute__((aligned(16))) bf16_t Gh[2][64][16];    // [buf][target][query], hi part
+    __shared__ __attribute__((aligned(16))) bf16_t Gl[2][64][16];    // lo part
+    const int tid = threadIdx.x, lane = tid & 63, m = lane & 31, h = lane >> 5;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
     const int nh = A.nwh[l], nu = A.nwu[l], nv = A.nwv[l];
     const long long nw3 = bw_nw3(A, l);
-    const int nbz = (Dl + 3) >> 2, nbx = (Wl + 3) >> 2;
-    const int split = (int)(blockIdx.x % nsplit);
-    const int brick = (int)(blockIdx.x / nsplit);
+    const int nbz = (Dl + 3) >> 2, nbx = (Wl + 3) >> 2, nby = (Hl + 3) >> 2;
     int t = brick;
     const int bz = t % nbz; t /= nbz;
     const int bx = t % nbx;
     const int by = t / nbx;
-    // this lane's A-operand rows: targets 32 T + m of the brick
-    int tyT[2], txT[2], tzT[2];
-    bool tvT[2];
-#pragma unroll
-    for (int T = 0; T < 2; ++T) {
-        const int i = 32 * T + m;
-        tyT[T] = by * 4 + (i >> 4); txT[T] = bx * 4 + ((i >> 2) & 3); tzT[T] = bz * 4 + (i & 3);
-        tvT[T] = tyT[T] < Hl && txT[T] < Wl && tzT[T] < Dl;
-    }
+    // staging roles: Q -- channel tc = tid >> 1, query half th; G -- target st = tid >> 2, query quarter sp
+    const int tc = tid >> 1, th = tid & 1;
+    const int st = tid >> 2, sp = tid & 3;
+    const bool tcok = tc < 32 * NCT;
+    const int ty = by * 4 + (st >> 4), tx = bx * 4 + ((st >> 2) & 3), tz = bz * 4 + (st & 3);
+    const bool tval = ty < Hl && tx < Wl && tz < Dl;
     const int CX = Wl + nu - 1, CZ = Dl + nv - 1;
     const int oy0 = by * 4, oy1 = min(by * 4 + 3, Hl - 1) + nh - 1;
     const int ox0 = bx * 4, ox1 = min(bx * 4 + 3, Wl - 1) + nu - 1;
     const int oz0 = bz * 4, oz1 = min(bz * 4 + 3, Dl - 1) + nv - 1;
     const int nox = ox1 - ox0 + 1, nrows = (oy1 - oy0 + 1) * nox;
     const float *gl = A.gwin + A.goff[l] + (long long)b * A.Nq * nw3;
-    f32x16 acc[2][NCT];
+    const bf16_t *qrow = Qt + (long long)(A.cbase + tc) * NqPad;   // this thread's staged channel
+    f32x16 acc[2];
 #pragma unroll
     for (int T = 0; T < 2; ++T)
 #pragma unroll
-        for (int ct = 0; ct < NCT; ++ct)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) acc[T][ct][i] = 0.0f;
-    // 64-query chunks of the brick's origin rows dealt round-robin to the 4 nsplit waves of the brick
-    const int wid = 4 * split + w, nwid = 4 * nsplit;
+        for (int i = 0; i < 16; ++i) acc[T][i] = 0.0f;
+    int buf = 0;
+    // 64-query chunks of the brick's origin rows dealt round-robin to the nsplit workgroups of the brick (every
+    // wave of the workgroup walks the same chunks)
     auto range = [&](int row, int &s, int &e) {
         const long long cb = ((long long)(oy0 + row / nox) * CX + (ox0 + row % nox)) * CZ;
         s = starts[cb + oz0];
         e = starts[cb + oz1 + 1];
     };
-    deal_chunks(nrows, wid, nwid, lane, range, [&](int row, int s, int e, int c1) {
+    deal_chunks(nrows, split, nsplit, lane, range, [&](int row, int s, int e, int c1) {
         const int oy = oy0 + row / nox, ox = ox0 + row % nox;
-        const long long cbase = ((long long)oy * CX + ox) * CZ;
-        int pyxT[2];
-        bool yxT[2];
-#pragma unroll
-        for (int T = 0; T < 2; ++T) {
-            const int py = tyT[T] - oy + nh - 1, px = txT[T] - ox + nu - 1;
-            yxT[T] = tvT[T] && (unsigned)py < (unsigned)nh && (unsigned)px < (unsigned)nu;
-            pyxT[T] = (py * nu + px) * nv;
-        }
-        for (int base = s + 64 * c1; base < e; base += 64 * nwid) {
+        const long long cbase = ((long long)oy * CX + ox) * CZ + A.coff[l];   // (keys hold global cells)
+        // window position (y, x) of the staged target for a query of origin o' = (oy, ox, *)
+        const int py = ty - oy + nh - 1, px = tx - ox + nu - 1;
+        const bool yxok = tval && (unsigned)py < (unsigned)nh && (unsigned)px < (unsigned)nu;
+        const int pyx = (py * nu + px) * nv;
+        for (int base = s + 64 * c1; base < e; base += 64 * nsplit) {
             const int nk = min(64, e - base);
             const unsigned long long key = lane < nk ? keys[base + lane] : 0ull;
             const int qq_l = (int)(unsigned)(key & 0xffffffffu);
             const int oz_l = (int)((long long)(key >> 32) - cbase);
-            for (int kb = 0; 16 * kb < nk; ++kb) {
-                const int k0 = 16 * kb + 8 * h;   // this lane's 8 queries: stream slots k0 .. k0 + 7
-                // B operands first (their loads fly while G is gathered)
-                bf16x8 qb[NCT];
+            u32x4 qreg;
+            u32x2 ghr, glr;
+            auto load = [&](int kb) {
+                qreg = u32x4{0u, 0u, 0u, 0u};
+                if (tcok) __builtin_memcpy(&qreg, qrow + base + 16 * kb + 8 * th, 16);   // (zero-padded past the keys)
+                float g[4];
 #pragma unroll
-                for (int ct = 0; ct < NCT; ++ct) {
-                    const bf16_t *src = Qt + (long long)(A.cbase + 32 * ct + m) * NqPad + base + k0;
-                    u32x4 v;
-                    __builtin_memcpy(&v, src, 16);   // 2-byte aligned 16-byte load
-                    qb[ct] = __builtin_bit_cast(bf16x8, v);
-                }
-                float g[2][8];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const int idx = k0 + k;
+                for (int k = 0; k < 4; ++k) {
+                    const int idx = 16 * kb + 4 * sp + k;
                     const bool in = idx < nk;
                     const int qq = __shfl(qq_l, in ? idx : 0);
-                    const int oz = __shfl(oz_l, in ? idx : 0);
+                    const int pz = tz - __shfl(oz_l, in ? idx : 0) + nv - 1;
+                    g[k] = in && yxok && (unsigned)pz < (unsigned)nv ? gl[(long long)qq * nw3 + pyx + pz] : 0.0f;
+                }
+                unsigned hi[4], lo[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const __bf16 hb = (__bf16)g[k];
+                    hi[k] = __builtin_bit_cast(unsigned short, hb);
+                    lo[k] = __builtin_bit_cast(unsigned short, (__bf16)(g[k] - (float)hb));
+                }
+                ghr = u32x2{hi[0] | (hi[1] << 16), hi[2] | (hi[3] << 16)};
+                glr = u32x2{lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16)};
+            };
+            auto store = [&](int bb) {
+                *reinterpret_cast<u32x4 *>(&Ql[bb][tc][8 * th]) = qreg;
+                *reinterpret_cast<u32x2 *>(&Gh[bb][st][4 * sp]) = ghr;
+                *reinterpret_cast<u32x2 *>(&Gl[bb][st][4 * sp]) = glr;
+            };
+            const int nb = (nk + 15) >> 4;
+            load(0);
+            __syncthreads();   // the previous chunk's last batch has been read
+            store(buf);
+            __syncthreads();
+            for (int kb = 0; kb < nb; ++kb) {
+                const bool more = kb + 1 < nb;
+                if (more) load(kb + 1);
+                if (w < NCT) {
+                    const bf16x8 bq = *reinterpret_cast<const bf16x8 *>(&Ql[buf][32 * w + m][8 * h]);
 #pragma unroll
                     for (int T = 0; T < 2; ++T) {
-                        const int pz = tzT[T] - oz + nv - 1;
-                        const bool ok = in && yxT[T] && (unsigned)pz < (unsigned)nv;
-                        g[T][k] = ok ? gl[(long long)qq * nw3 + pyxT[T] + pz] : 0.0f;
+                        const bf16x8 ah = *reinterpret_cast<const bf16x8 *>(&Gh[buf][32 * T + m][8 * h]);
+                        const bf16x8 al = *reinterpret_cast<const bf16x8 *>(&Gl[buf][32 * T + m][8 * h]);
+                        acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bq, acc[T], 0, 0, 0);
+                        acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bq, acc[T], 0, 0, 0);
                     }
                 }
-#pragma unroll
-                for (int T = 0; T < 2; ++T) {
-                    bf16x8 ghi, glo;
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        const __bf16 hi = (__bf16)g[T][k];
-                        ghi[k] = hi;
-                        glo[k] = (__bf16)(g[T][k] - (float)hi);
-                    }
-#pragma unroll
-                    for (int ct = 0; ct < NCT; ++ct) {
-                        acc[T][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ghi, qb[ct], acc[T][ct], 0, 0, 0);
-                        acc[T][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(glo, qb[ct], acc[T][ct], 0, 0, 0);
-                    }
+                if (more) {
+                    store(buf ^ 1);
+                    __syncthreads();
+                    buf ^= 1;
                 }
             }
         }
     });
-    // cross-wave sum in a fixed order: waves 2, 3 -> 0, 1; wave 1 -> 0
-    auto put = [&](int slot) {
-#pragma unroll
-        for (int T = 0; T < 2; ++T)
-#pragma unroll
-            for (int ct = 0; ct < NCT; ++ct)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) red[slot][(T * NCT + ct) * 16 + i][lane] = acc[T][ct][i];
-    };
-    auto add = [&](int slot) {
-#pragma unroll
-        for (int T = 0; T < 2; ++T)
-#pragma unroll
-            for (int ct = 0; ct < NCT; ++ct)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) acc[T][ct][i] += red[slot][(T * NCT + ct) * 16 + i][lane];
-    };
-    __syncthreads();
-    if (w >= 2) put(w - 2);
-    __syncthreads();
-    if (w < 2) add(w);
-    __syncthreads();
-    if (w == 1) put(0);
-    __syncthreads();
-    if (w != 0) return;
-    add(0);
-    // D layout (32x32 MFMA): acc[T][ct][i] = D[target 32 T + 8 (i / 4) + 4 h + i % 4][channel 32 ct + m]
+    if (w >= NCT) return;
+    // D layout (32x32 MFMA): acc[T][i] = D[target 32 T + 8 (i / 4) + 4 h + i % 4][channel 32 w + m]
     const float sc = A.scale;
+    const int ch = A.cbase + 32 * w + m;
 #pragma unroll
     for (int T = 0; T < 2; ++T)
 #pragma unroll
@@ -952,14 +985,10 @@ __global__ __launch_bounds__(256) void k_grad_t_mfma(const bf16_t *__restrict__ 
             const int ti = 32 * T + 8 * (i >> 2) + 4 * h + (i & 3);
             const int y = by * 4 + (ti >> 4), x = bx * 4 + ((ti >> 2) & 3), z = bz * 4 + (ti & 3);
             if (nsplit > 1) {
-                float *pp = dTp + (((long long)split * gridDim.x / nsplit + brick) * 64 + ti) * A.Cp + A.cbase + m;
-#pragma unroll
-                for (int ct = 0; ct < NCT; ++ct) pp[32 * ct] = acc[T][ct][i];
+                dTp[A.gt_poff[l] + (((long long)split * nbz * nbx * nby + brick) * 64 + ti) * A.Cp + ch] = acc[T][i];
             } else if (y < Hl && x < Wl && z < Dl) {
-                float *dst = dT + ((long long)b * A.row_stride + A.off[l] + ((long long)y * Wl + x) * Dpl + z) * A.Cp +
-                             A.cbase + m;
-#pragma unroll
-                for (int ct = 0; ct < NCT; ++ct) dst[32 * ct] = acc[T][ct][i] * sc;
+                dT[((long long)b * A.row_stride + A.off[l] + ((long long)y * Wl + x) * Dpl + z) * A.Cp + ch] =
+                    acc[T][i] * sc;
             }
         }
 }
@@ -967,10 +996,16 @@ __global__ __launch_bounds__(256) void k_grad_t_mfma(const bf16_t *__restrict__ 
 // dT rows of level l <- scale * sum over the nsplit partials (split order: deterministic).  One thread per
 // (brick target, channel pair).
 __global__ __launch_bounds__(256) void k_grad_t_reduce(const float *__restrict__ dTp, float *__restrict__ dT,
-                                                       int nsplit, int nbricks, BwdArgs A, int b, int l) {
-    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+                                                       BwdArgs A, int b) {
+    long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
     const int cp2 = A.Cp / 2;
-    if (idx >= (long long)nbricks * 64 * cp2) return;
+    if (idx >= A.gt_r0[A.L]) return;
+    int l = 0;
+    while (l + 1 < A.L && idx >= A.gt_r0[l + 1]) ++l;
+    idx -= A.gt_r0[l];
+    const int nsplit = A.gt_sp[l];
+    const int nbricks = ((A.H[l] + 3) >> 2) * ((A.W[l] + 3) >> 2) * ((A.D[l] + 3) >> 2);
+    dTp += A.gt_poff[l];
     const int c0 = 2 * (int)(idx % cp2);
     const int i = (int)((idx / cp2) % 64);
     const int brick = (int)(idx / (cp2 * 64LL));
@@ -1001,6 +1036,8 @@ struct UnpackArgs {
     int Hs[DVC_MAX_LEVELS], Ws[DVC_MAX_LEVELS], Ds[DVC_MAX_LEVELS], Dps[DVC_MAX_LEVELS];
     long long offs[DVC_MAX_LEVELS];
     float wts[DVC_MAX_LEVELS];
+    int nsum;            // src holds nsum partial sums sstride floats apart, added in order (k_grad_q_mfma)
+    long long sstride;
 };
 
 __global__ __launch_bounds__(256) void k_unpack_sum(UnpackArgs U) {
@@ -1020,8 +1057,12 @@ __global__ __launch_bounds__(256) void k_unpack_sum(UnpackArgs U) {
             const int x = (int)(yx % U.W), y = (int)(yx / U.W);
             for (int l = 0; l < U.ns; ++l) {
                 const int py = y >> l, px = x >> l, pz = z >> l;
-                if (py < U.Hs[l] && px < U.Ws[l] && pz < U.Ds[l])
-                    s += U.wts[l] * src[(U.offs[l] + ((long long)py * U.Ws[l] + px) * U.Dps[l] + pz) * U.Cp + c0 + c];
+                if (py < U.Hs[l] && px < U.Ws[l] && pz < U.Ds[l]) {
+                    const float *p = src + (U.offs[l] + ((long long)py * U.Ws[l] + px) * U.Dps[l] + pz) * U.Cp + c0 + c;
+                    float v = p[0];
+                    for (int k = 1; k < U.nsum; ++k) v += p[k * U.sstride];
+                    s += U.wts[l] * v;
+                }
             }
         }
         tile[vl][c] = s;
@@ -1043,6 +1084,9 @@ static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct BwdPlan {
     size_t gwin, dq, dt, keys, starts, temp, part, qt, ttr, total;
+    long long coff[DVC_MAX_LEVELS + 1];   // first window-origin cell of each level in the merged key space
+    int sp[DVC_MAX_LEVELS];               // k_grad_t splits per brick
+    long long poff[DVC_MAX_LEVELS];       // split-partial offsets (floats)
     long long rows_pad;  // Ttr row length (pyramid rows + slack for the 16-target batches)
     long long nq_pad;   // Qt row length (sorted queries + zero padding for the 16-query batches)
     int nw[DVC_MAX_LEVELS][3];   // window box (h, u, v) per level
@@ -1076,6 +1120,9 @@ static int grad_t_splits(const dvc_layout &lay, int l, long long Nq) {
     return (int)std::max(1LL, std::min(sp, 256LL));
 }
 
+// k_grad_q_mfma level groups (blockIdx.y): level 0 alone and the coarse levels together, two partial dQ
+static int grad_q_parts(int L) { return L > 1 ? 2 : 1; }
+
 static long long level_cells(const dvc_layout &lay, int l, const int nw[3]) {
     return (long long)(lay.H[l] + nw[0] - 1) * (lay.W[l] + nw[1] - 1) * (lay.D[l] + nw[2] - 1);
 }
@@ -1084,27 +1131,34 @@ static void bwd_plan(int B, long long Nq, const dvc_layout &lay, int radius, boo
     size_t gw = 0;
     long long cells = 0;
     size_t part = 0;
-    for (int l = 0; l < lay.num_levels; ++l) {
+    const int L = lay.num_levels;
+    for (int l = 0; l < L; ++l) {
         win_dims(lay, l, radius, legacy, P.nw[l]);
         gw = al256(gw);   // k_win_grad stores 8-byte pairs
         P.goff[l] = (long long)(gw / sizeof(float));
         gw += (size_t)B * Nq * P.nw[l][0] * P.nw[l][1] * P.nw[l][2] * sizeof(float);
-        cells = std::max(cells, level_cells(lay, l, P.nw[l]));
-        const int sp = grad_t_splits(lay, l, Nq);
+        P.coff[l] = cells;
+        cells += level_cells(lay, l, P.nw[l]) + 1;   // + the level's "outside" cell
+        P.sp[l] = grad_t_splits(lay, l, Nq);
         const long long bricks = (long long)((lay.H[l] + 3) / 4) * ((lay.W[l] + 3) / 4) * ((lay.D[l] + 3) / 4);
-        if (sp > 1) part = std::max<size_t>(part, (size_t)sp * (size_t)bricks * 64 * (size_t)lay.c_pad * sizeof(float));
+        P.poff[l] = (long long)(part / sizeof(float));
+        if (P.sp[l] > 1 && !lay.zero_level[l])
+            part += (size_t)P.sp[l] * (size_t)bricks * 64 * (size_t)lay.c_pad * sizeof(float);
     }
+    P.coff[L] = cells;
+    // the target-gradient pass sorts the keys of all L levels of one batch element at once
+    const long long nkeys = (long long)L * Nq;
     P.gwin = al256(gw) + 512;   // + 256-byte guards before and after (k_grad_q_mfma's 8-float loads)
-    P.dq = al256((size_t)B * Nq * lay.c_pad * sizeof(float));
+    P.dq = al256((size_t)grad_q_parts(L) * B * Nq * lay.c_pad * sizeof(float));
     P.dt = al256((size_t)B * lay.row_stride * lay.c_pad * sizeof(float));
-    P.keys = al256((size_t)Nq * sizeof(unsigned long long));
+    P.keys = al256((size_t)nkeys * sizeof(unsigned long long));
     P.starts = al256((size_t)(cells + 1) * sizeof(int));
     size_t tb = 0;
     (void)rocprim::radix_sort_keys(nullptr, tb, (unsigned long long *)nullptr, (unsigned long long *)nullptr,
-                                   (size_t)Nq, 0u, 64u, (hipStream_t)0);
+                                   (size_t)nkeys, 0u, 64u, (hipStream_t)0);
     P.temp = al256(tb);
     P.part = al256(std::max<size_t>(part, 256));
-    P.nq_pad = ((Nq + 16 + 63) / 64) * 64;
+    P.nq_pad = ((nkeys + 16 + 63) / 64) * 64;
     P.qt = al256((size_t)P.nq_pad * lay.c_pad * sizeof(bf16_t));   // bf16 path only (sized always)
     P.rows_pad = ((lay.row_stride + 32 + 1) / 2) * 2;
     P.ttr = al256((size_t)B * lay.c_pad * P.rows_pad * sizeof(bf16_t));   // bf16 path only (sized always)
@@ -1151,18 +1205,22 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
         if (!launched("win_grad_generic")) return DVC_ERR_LAUNCH;
     }
     const long long boxes = (long long)A.B * ((A.Hq + 3) / 4) * ((A.Wq + 3) / 4) * ((A.Dq + 3) / 4);
+    // partial dQ per level group of the MFMA path (qparts of them, qstride floats apart)
+    const int qparts = std::is_same<TT, bf16_t>::value ? grad_q_parts(A.L) : 1;
+    const long long qstride = (long long)A.B * A.Nq * A.Cp;
     if constexpr (std::is_same<TT, bf16_t>::value) {
         dim3 tg((unsigned)((P.rows_pad + 63) / 64), (unsigned)A.B, (unsigned)ngroups);
         k_transpose_targets<<<tg, 256, 0, s>>>(Tt, ttr, A.row_stride, P.rows_pad, A.Cp);
         if (!launched("transpose_targets")) return DVC_ERR_LAUNCH;
+        const dim3 qg((unsigned)boxes, (unsigned)qparts);   // level groups: {0}, {1 .. L-1}
         for (int g = 0; g < ngroups; ++g) {
             BwdArgs Ag = A;
             Ag.cbase = 128 * g;
             switch (std::min(128, A.Cp - Ag.cbase) / 32) {
-            case 1: k_grad_q_mfma<1><<<(unsigned)boxes, 256, 0, s>>>(ttr, P.rows_pad, dq, Ag); break;
-            case 2: k_grad_q_mfma<2><<<(unsigned)boxes, 256, 0, s>>>(ttr, P.rows_pad, dq, Ag); break;
-            case 3: k_grad_q_mfma<3><<<(unsigned)boxes, 256, 0, s>>>(ttr, P.rows_pad, dq, Ag); break;
-            default: k_grad_q_mfma<4><<<(unsigned)boxes, 256, 0, s>>>(ttr, P.rows_pad, dq, Ag); break;
+            case 1: k_grad_q_mfma<1><<<qg, 256, 0, s>>>(ttr, P.rows_pad, dq, qstride, Ag); break;
+            case 2: k_grad_q_mfma<2><<<qg, 256, 0, s>>>(ttr, P.rows_pad, dq, qstride, Ag); break;
+            case 3: k_grad_q_mfma<3><<<qg, 256, 0, s>>>(ttr, P.rows_pad, dq, qstride, Ag); break;
+            default: k_grad_q_mfma<4><<<qg, 256, 0, s>>>(ttr, P.rows_pad, dq, qstride, Ag); break;
             }
         }
     } else {
@@ -1173,57 +1231,72 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
         }
     }
     if (!launched("grad_q")) return DVC_ERR_LAUNCH;
-    for (int b = 0; b < A.B; ++b)
-        for (int l = 0; l < A.L; ++l) {
-            if (A.zero[l]) continue;
-            const long long ncell = level_cells(lay, l, P.nw[l]);
-            unsigned bits = 1;
-            while ((1LL << bits) <= ncell) ++bits;
-            k_bw_keys<R><<<(unsigned)((A.Nq + 255) / 256), 256, 0, s>>>(A, b, l, kin);
-            if (!launched("keys")) return DVC_ERR_LAUNCH;
-            size_t tb = P.temp;
-            if (rocprim::radix_sort_keys(temp, tb, kin, kout, (size_t)A.Nq, 0u, 32u + bits, s) != hipSuccess) {
-                snprintf(err, errlen, "corr_backward: radix sort failed");
-                return DVC_ERR_RUNTIME;
-            }
-            k_cell_starts<<<(unsigned)((ncell + 1 + 255) / 256), 256, 0, s>>>(kout, A.Nq, ncell, starts);
-            if (!launched("cell_starts")) return DVC_ERR_LAUNCH;
-            const long long bricks = (long long)((A.H[l] + 3) / 4) * ((A.W[l] + 3) / 4) * ((A.D[l] + 3) / 4);
-            const int sp = grad_t_splits(lay, l, A.Nq);
-            if constexpr (std::is_same<TT, bf16_t>::value) {
-                // matrix-core path: sorted + transposed query rows, then 16-query MFMA batches
-                k_qt_sorted<<<dim3((unsigned)(P.nq_pad / 64), (unsigned)ngroups), 256, 0, s>>>(Q, kout, qt, A.Nq,
-                                                                                           P.nq_pad, A.Cp, b);
-                if (!launched("qt_sorted")) return DVC_ERR_LAUNCH;
-                const unsigned g = (unsigned)(bricks * sp);
-                for (int cg = 0; cg < ngroups; ++cg) {
-                    BwdArgs Ag = A;
-                    Ag.cbase = 128 * cg;
-                    switch (std::min(128, A.Cp - Ag.cbase) / 32) {
-                    case 1: k_grad_t_mfma<1><<<g, 256, 0, s>>>(qt, P.nq_pad, kout, starts, dt, dtp, sp, Ag, b, l); break;
-                    case 2: k_grad_t_mfma<2><<<g, 256, 0, s>>>(qt, P.nq_pad, kout, starts, dt, dtp, sp, Ag, b, l); break;
-                    case 3: k_grad_t_mfma<3><<<g, 256, 0, s>>>(qt, P.nq_pad, kout, starts, dt, dtp, sp, Ag, b, l); break;
-                    default: k_grad_t_mfma<4><<<g, 256, 0, s>>>(qt, P.nq_pad, kout, starts, dt, dtp, sp, Ag, b, l); break;
-                    }
+    // target gradients: per batch element, the queries of every level in window-origin order (one key
+    // space, one sort), then one k_grad_t launch over every level's (brick, split) workgroups, coarse levels'
+    // split partials reduced by one launch
+    int nblk = 0;
+    long long nred = 0;
+    for (int l = 0; l < A.L; ++l) {
+        const long long bricks = (long long)((A.H[l] + 3) / 4) * ((A.W[l] + 3) / 4) * ((A.D[l] + 3) / 4);
+        A.coff[l] = P.coff[l];
+        A.gt_sp[l] = P.sp[l];
+        A.gt_poff[l] = P.poff[l];
+        A.gt_blk0[l] = nblk;
+        A.gt_r0[l] = nred;
+        if (A.zero[l]) continue;   // a size-1 level gets no gradient (its dT rows are never read)
+        nblk += (int)(bricks * P.sp[l]);
+        if (P.sp[l] > 1) nred += bricks * 64 * (A.Cp / 2);
+    }
+    A.gt_blk0[A.L] = nblk;
+    A.gt_r0[A.L] = nred;
+    const long long ncell = P.coff[A.L] - 1;   // the last level's outside cell
+    const long long nkeys = (long long)A.L * A.Nq;
+    unsigned bits = 1;
+    while ((1LL << bits) <= ncell) ++bits;
+    for (int b = 0; b < A.B; ++b) {
+        k_bw_keys<R><<<dim3((unsigned)((A.Nq + 255) / 256), (unsigned)A.L), 256, 0, s>>>(A, b, kin);
+        if (!launched("keys")) return DVC_ERR_LAUNCH;
+        size_t tb = P.temp;
+        if (rocprim::radix_sort_keys(temp, tb, kin, kout, (size_t)nkeys, 0u, 32u + bits, s) != hipSuccess) {
+            snprintf(err, errlen, "corr_backward: radix sort failed");
+            return DVC_ERR_RUNTIME;
+        }
+        k_cell_starts<<<(unsigned)((ncell + 1 + 255) / 256), 256, 0, s>>>(kout, nkeys, ncell, starts);
+        if (!launched("cell_starts")) return DVC_ERR_LAUNCH;
+        if (nblk == 0) continue;
+        if constexpr (std::is_same<TT, bf16_t>::value) {
+            // matrix-core path: sorted + transposed query rows, then 16-query MFMA batches
+            k_qt_sorted<<<dim3((unsigned)(P.nq_pad / 64), (unsigned)ngroups), 256, 0, s>>>(Q, kout, qt, A.Nq, nkeys,
+                                                                                       P.nq_pad, A.Cp, b);
+            if (!launched("qt_sorted")) return DVC_ERR_LAUNCH;
+            for (int cg = 0; cg < ngroups; ++cg) {
+                BwdArgs Ag = A;
+                Ag.cbase = 128 * cg;
+                switch (std::min(128, A.Cp - Ag.cbase) / 32) {
+                case 1: k_grad_t_mfma<1><<<nblk, 256, 0, s>>>(qt, P.nq_pad, kout, starts, dt, dtp, Ag, b); break;
+                case 2: k_grad_t_mfma<2><<<nblk, 256, 0, s>>>(qt, P.nq_pad, kout, starts, dt, dtp, Ag, b); break;
+                case 3: k_grad_t_mfma<3><<<nblk, 256, 0, s>>>(qt, P.nq_pad, kout, starts, dt, dtp, Ag, b); break;
+                default: k_grad_t_mfma<4><<<nblk, 256, 0, s>>>(qt, P.nq_pad, kout, starts, dt, dtp, Ag, b); break;
                 }
-            } else {
-                for (int cg = 0; cg < ngroups; ++cg) {
-                    BwdArgs Ag = A;
-                    Ag.cbase = 128 * cg;
-                    k_grad_t<TT, R><<<(unsigned)(bricks * sp), 256, 0, s>>>(Q, kout, starts, dt, dtp, sp, Ag, b, l);
-                }
             }
-            if (!launched("grad_t")) return DVC_ERR_LAUNCH;
-            if (sp > 1) {
-                const long long nt = bricks * 64 * (A.Cp / 2);
-                k_grad_t_reduce<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(dtp, dt, sp, (int)bricks, A, b, l);
-                if (!launched("grad_t_reduce")) return DVC_ERR_LAUNCH;
+        } else {
+            for (int cg = 0; cg < ngroups; ++cg) {
+                BwdArgs Ag = A;
+                Ag.cbase = 128 * cg;
+                k_grad_t<TT, R><<<nblk, 256, 0, s>>>(Q, kout, starts, dt, dtp, Ag, b);
             }
         }
+        if (!launched("grad_t")) return DVC_ERR_LAUNCH;
+        if (nred > 0) {
+            k_grad_t_reduce<<<(unsigned)((nred + 255) / 256), 256, 0, s>>>(dtp, dt, A, b);
+            if (!launched("grad_t_reduce")) return DVC_ERR_LAUNCH;
+        }
+    }
     // dfmap1 (B, C, Nq) <- dQ
     UnpackArgs U{};
     U.src = dq; U.dst = g1; U.src_bstride = A.Nq; U.N = A.Nq; U.C = C; U.Cp = A.Cp; U.W = A.Wq; U.D = A.Dq;
     U.ns = 1; U.Hs[0] = A.Hq; U.Ws[0] = A.Wq; U.Ds[0] = A.Dq; U.Dps[0] = A.Dq; U.offs[0] = 0; U.wts[0] = 1.0f;
+    U.nsum = qparts; U.sstride = qstride;
     dim3 g1grid((unsigned)((A.Nq + 63) / 64), (unsigned)((C + 63) / 64), (unsigned)A.B);
     k_unpack_sum<<<g1grid, 256, 0, s>>>(U);
     if (!launched("unpack_q")) return DVC_ERR_LAUNCH;
@@ -1234,6 +1307,7 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     // slot l = level l (the unpack shifts coordinates by the slot index); a zero level's
     // dT rows are never written, so its slot gets an empty extent
     V.ns = lay.num_levels;
+    V.nsum = 1; V.sstride = 0;
     float wl = 1.0f;
     for (int l = 0; l < lay.num_levels; ++l, wl *= 0.125f) {
         V.Hs[l] = lay.zero_level[l] ? 0 : lay.H[l];
@@ -1262,11 +1336,12 @@ int corr_backward(const void *packed_q, const void *packed_t, const float *coord
     const bool legacy = convention == DVC_LEGACY;
     BwdPlan P;
     bwd_plan(B, Nq, lay, radius, legacy, P);
-    for (int l = 0; l < lay.num_levels; ++l)
-        if (level_cells(lay, l, P.nw[l]) >= (1LL << 31) - 1 || Nq >= (1LL << 31) - 1) {
-            snprintf(err, errlen, "corr_backward: volume too large for 32-bit keys");
-            return DVC_ERR_UNSUPPORTED;
-        }
+    // merged key space: every level's cells (+ one outside cell each) in 31 bits, and the sorted positions of
+    // all levels' queries (int cell starts) below 2^31
+    if (P.coff[lay.num_levels] >= (1LL << 31) - 1 || (long long)lay.num_levels * Nq >= (1LL << 31) - 1) {
+        snprintf(err, errlen, "corr_backward: volume too large for 32-bit keys");
+        return DVC_ERR_UNSUPPORTED;
+    }
     BwdArgs A{};
     A.coords = coords; A.gout = grad_out; A.Nq = Nq; A.row_stride = lay.row_stride;
     A.B = B; A.L = lay.num_levels; A.legacy = legacy; A.Wq = lay.W[0]; A.Dq = lay.D[0];
