@@ -49,6 +49,26 @@ namespace dvc {
 #endif
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// LDS-DMA (global_load_lds_dword / _dwordx4): each lane's 4 / 16 bytes from its own global address land at
+// LDS byte lds + 4 / 16 * lane (lds wave-uniform).  Issued from asm so hipcc leaves them out of its s_waitcnt
+// bookkeeping (it would otherwise drain them with vmcnt(0) before every LDS read): the kernel counts them
+// itself with s_waitcnt vmcnt(N) and a raw s_barrier before reading the data.
+__device__ __forceinline__ unsigned lds_addr(const void *p) {
+    return __builtin_amdgcn_readfirstlane(
+        (unsigned)(uintptr_t)(const __attribute__((address_space(3))) unsigned char *)(p));
+}
+__device__ __forceinline__ void glds16(const void *g, unsigned lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void glds4(const void *g, unsigned lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
 
 struct BwdArgs {
     const float *coords;   // (B, 3, Nq)
@@ -147,7 +167,17 @@ template <> __device__ __forceinline__ f32x2 load2<f16_t>(const f16_t *p) {
 // window plane i and column j, combines output rows a in {i, i-1} and columns
 // u in {j, j-1}, then spreads each v over window z in {v, v+1}.
 // ---------------------------------------------------------------------------------
-template <int R>
+// One window gradient as the MFMA kernels' operand pair: bf16(g) in the low half, bf16(g - bf16(g)) in the high
+// half (their products keep ~16 mantissa bits of g; the bf16 operands are bf16 already)
+__device__ __forceinline__ unsigned bf16_hilo(float g) {
+    const __bf16 hb = (__bf16)g;
+    return (unsigned)__builtin_bit_cast(unsigned short, hb) |
+           ((unsigned)__builtin_bit_cast(unsigned short, (__bf16)(g - (float)hb)) << 16);
+}
+
+// HILO: the window gradients leave as bf16_hilo pairs (the bf16 path's MFMA kernels read them as operands
+// directly), else as fp32
+template <int R, bool HILO>
 __global__ __launch_bounds__(256) void k_win_grad(BwdArgs A) {
     constexpr int n = 2 * R + 1, NW = 2 * R + 2, NW3 = NW * NW * NW;
     const int lane = threadIdx.x & 63;
@@ -232,9 +262,15 @@ __global__ __launch_bounds__(256) void k_win_grad(BwdArgs A) {
                 o[v] = __builtin_fmaf(wz0[v], gz, o[v]);
                 o[v + 1] = __builtin_fmaf(wz1[v], gz, o[v + 1]);
             }
-            f32x2 *dst = reinterpret_cast<f32x2 *>(gw + (i * NW + j) * NW);
+            if constexpr (HILO) {
+                u32x2 *dst = reinterpret_cast<u32x2 *>(gw + (i * NW + j) * NW);
 #pragma unroll
-            for (int k = 0; k < NW / 2; ++k) dst[k] = f32x2{o[2 * k], o[2 * k + 1]};
+                for (int k = 0; k < NW / 2; ++k) dst[k] = u32x2{bf16_hilo(o[2 * k]), bf16_hilo(o[2 * k + 1])};
+            } else {
+                f32x2 *dst = reinterpret_cast<f32x2 *>(gw + (i * NW + j) * NW);
+#pragma unroll
+                for (int k = 0; k < NW / 2; ++k) dst[k] = f32x2{o[2 * k], o[2 * k + 1]};
+            }
 #pragma unroll
             for (int v = 0; v < n; ++v) Pp[v] = Pc[v];
         }
@@ -248,7 +284,7 @@ __global__ __launch_bounds__(256) void k_win_grad(BwdArgs A) {
 // Generic (legacy W != D) levels: lane = query; the window box is zeroed, then every output's
 // (up to) 8 in-range corners are added in output order with grid_sample's weights
 // (tri_sample in common.h).  The box is private to the lane: no atomics, fixed order.
-template <int R>
+template <int R, bool HILO>
 __global__ __launch_bounds__(256) void k_win_grad_generic(BwdArgs A) {
     constexpr int n = 2 * R + 1;
     const int lane = threadIdx.x & 63;
@@ -317,6 +353,9 @@ __global__ __launch_bounds__(256) void k_win_grad_generic(BwdArgs A) {
                 }
             }
         }
+    }
+    if constexpr (HILO) {   // the lane's finished box into bf16_hilo pairs, in place
+        for (long long i = 0; i < nw3; ++i) reinterpret_cast<unsigned *>(gw)[i] = bf16_hilo(gw[i]);
     }
 }
 
@@ -479,20 +518,63 @@ __global__ __launch_bounds__(256) void k_transpose_targets(const bf16_t *__restr
     }
 }
 
-// Round 3: the workgroup's four waves split the CHANNELS (wave w = channel tile w of 32), not the rows, so a
-// wave accumulates dQ[64 queries][32 channels] in 32 registers (was [64][128] in 128 accumulators + 256 VGPRs:
-// one wave per SIMD, every gather's latency exposed).  Per (union row, 16-target z batch) all 256 threads stage
-// once, into a double-buffered LDS tile: the target rows Ttr[128 ch][16 z] (one 16-byte load per thread) and the
-// 64 queries' window gradients G[64][16 z] as bf16 hi + lo (four 4-byte loads per thread, only the window's own
-// values: a query whose window misses the row or the z batch loads nothing); the next batch's loads fly while
-// the current one's MFMAs run, one barrier per batch.  Level groups (blockIdx.y) write separate partial dQ
-// (the heavy level 0 alone, the coarse levels together), summed in a fixed order by k_unpack_sum.
+// Round 3: the workgroup's four waves split the CHANNELS (wave w = channel tile w of 32), so a wave accumulates
+// dQ[64 queries][32 channels] in 32 registers (the round-2 kernel held [64][128] in 128 accumulators + 256
+// VGPRs: one wave per SIMD, every gather's latency exposed).  Per (union row, 16-target z batch) the 256 threads
+// copy the batch straight into LDS with LDS-DMA buffer loads (no VGPR destination, 32-bit offsets): the target
+// rows Ttr[128 ch][16 z] (one 16-byte DMA per thread) and the 64 queries' window gradients G[64][16 z] as
+// bf16_hilo pairs (four 4-byte DMAs per thread; values outside a query's window are out of the buffer's range
+// and land as 0).  The pairs are the MFMA's A operand as they stand -- K runs over (z, hi/lo), and the B operand
+// repeats each target row twice -- so no wave converts anything.  kQStages LDS stages keep kQStages - 2
+// batches in flight across the raw barrier that retires the current one (a counted vmcnt: a __syncthreads()
+// would drain every DMA in flight).  Both tiles are XOR-swizzled through the DMA source offsets so the operand
+// reads are free of bank conflicts.  Level groups (blockIdx.y) write separate partial dQ (level 0 alone, the
+// coarse levels together), summed in a fixed order by k_unpack_sum.
+constexpr int kQRows = 1024;   // batches listed at a time (a box's union at +-2 flows, r = 4: 17^2 rows x 2)
+constexpr int kQStages = 4;    // LDS stages of the batch pipeline (kQStages - 2 in flight across the barrier)
+constexpr unsigned kOOB = 0x80000000u;   // a buffer offset past every range (reads 0)
+// diagnostics builds only (tools/build_variant.sh -DDVC_GQ_ABL=n): 1 no MFMAs, 2 no G DMAs, 4 no T DMAs
+#ifndef DVC_GQ_ABL
+#define DVC_GQ_ABL 0
+#endif
+
+// a raw buffer descriptor (base, stride 0, num_records bytes, the same flags as make_buffer_rsrc's elsewhere)
+// as four SGPRs (the asm operand s[N:N+3])
+__device__ __forceinline__ u32x4 sgpr_rsrc(const void *base, unsigned bytes) {
+    const unsigned long long p = (unsigned long long)base;
+    return u32x4{(unsigned)__builtin_amdgcn_readfirstlane((unsigned)p),
+                 (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(p >> 32) & 0xffffu),
+                 (unsigned)__builtin_amdgcn_readfirstlane(bytes), 0x00020000u};
+}
+template <typename Width>
+__device__ __forceinline__ void blds(u32x4 rs, unsigned voff, unsigned lds, Width) {
+    unsigned keep;
+    if constexpr (Width::value == 16)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+                     "s_mov_b32 m0, %0" : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds) : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\t"
+                     "s_mov_b32 m0, %0" : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds) : "memory");
+}
+using W16 = std::integral_constant<int, 16>;
+using W4 = std::integral_constant<int, 4>;
+
+// {a.lo, a.lo, a.hi, a.hi, b.lo, ...}: four bf16 each repeated (the B operand over K = (z, hi/lo))
+__device__ __forceinline__ bf16x8 dup_bf16x4(u32x2 v) {
+    u32x4 r;
+    r[0] = __builtin_amdgcn_perm(v[0], v[0], 0x01000100u);
+    r[1] = __builtin_amdgcn_perm(v[0], v[0], 0x03020302u);
+    r[2] = __builtin_amdgcn_perm(v[1], v[1], 0x01000100u);
+    r[3] = __builtin_amdgcn_perm(v[1], v[1], 0x03020302u);
+    return __builtin_bit_cast(bf16x8, r);
+}
+
 template <int NCT>   // channel tiles of 32 (C_pad / 32, <= 4 per launch)
 __global__ __launch_bounds__(256, 4) void k_grad_q_mfma(const bf16_t *__restrict__ Ttr, long long rows_pad,
                                                         float *__restrict__ dQp, long long part_stride, BwdArgs A) {
-    __shared__ __attribute__((aligned(16))) bf16_t Tl[2][128][16];   // [buf][channel][z]
-    __shared__ __attribute__((aligned(16))) bf16_t Gh[2][64][16];    // [buf][query][z], hi part
-    __shared__ __attribute__((aligned(16))) bf16_t Gl[2][64][16];    // lo part
+    constexpr int STAGE = 8192;                      // bytes: T tile (4 KB, bf16) + G tile (4 KB, hi/lo pairs)
+    __shared__ __attribute__((aligned(16))) unsigned char stg[kQStages * STAGE];
+    __shared__ unsigned qrows[kQRows + 2];           // batches (y | x << 11 | z0 << 22), count, next row
     const int tid = threadIdx.x, lane = tid & 63, m = lane & 31, h = lane >> 5;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nbz = (A.Dq + 3) >> 2, nbx = (A.Wq + 3) >> 2, nby = (A.Hq + 3) >> 2;
@@ -504,23 +586,29 @@ __global__ __launch_bounds__(256, 4) void k_grad_q_mfma(const bf16_t *__restrict
     // level group: y = 0 level 0, y = 1 levels 1 .. L-1 (gridDim.y = 1: every level)
     const int lg0 = gridDim.y == 1 ? 0 : (blockIdx.y == 0 ? 0 : 1);
     const int lg1 = gridDim.y == 1 ? A.L : (blockIdx.y == 0 ? 1 : A.L);
-    // lane-as-query view (union bounds, row skipping): query i = lane of the box
+    // lane-as-query view (union bounds, row list): query i = lane of the box
     const int qy = by * 4 + (lane >> 4), qx = bx * 4 + ((lane >> 2) & 3), qz = bz * 4 + (lane & 3);
     const bool active = qy < A.Hq && qx < A.Wq && qz < A.Dq;
-    const long long q = active ? ((long long)qy * A.Wq + qx) * A.Dq + qz : 0;
+    const long long qb0 = ((long long)by * 4 * A.Wq + bx * 4) * A.Dq + bz * 4;   // the box's first query
+    const int qrel = active ? (int)(((long long)qy * A.Wq + qx) * A.Dq + qz - qb0) : 0;
     float cy = 0.0f, cx = 0.0f, cz = 0.0f;
-    if (active) load_coords(A.coords, b, A.Nq, q, cy, cx, cz);
-    // staging roles: T -- channel tc = tid >> 1, z half th = tid & 1; G -- query sq = tid >> 2, z quarter sp
-    const int tc = tid >> 1, th = tid & 1;
-    const int sq = tid >> 2, sp = tid & 3;
-    const bool tcok = tc < 32 * NCT;
+    if (active) load_coords(A.coords, b, A.Nq, qb0 + qrel, cy, cx, cz);
+    // T DMA role: channel tc = 32 w + lane / 2 (clamped into the launch's channels: rows past them are never
+    // read), physical 16-byte chunk lane & 1 of its 32-byte row, holding the z half (lane & 1) ^ (row >> 3 & 1)
+    const int tc = 32 * w + (lane >> 1);
+    const int thalf = (lane & 1) ^ ((tc >> 3) & 1);
+    const int cg = min(128, A.Cp - A.cbase);
+    const u32x4 rs_t = sgpr_rsrc(Ttr + ((long long)b * A.Cp + A.cbase) * rows_pad, (unsigned)(cg * rows_pad * 2));
+    const unsigned tvo = (unsigned)(((long long)(tc < cg ? tc : 0) * rows_pad + 8 * thalf) * 2);
+    // G DMA role, instruction k: query gq = 16 w + 4 k + lane / 16, physical dword lane & 15 of its 64-byte row =
+    // logical z 4 ((lane >> 2 & 3) ^ (gq >> 2 & 3)) + (lane & 3)
     f32x16 acc[2];
 #pragma unroll
     for (int T = 0; T < 2; ++T)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[T][i] = 0.0f;
     const int BIG = 1 << 29;
-    const bf16_t *tb = Ttr + ((long long)b * A.Cp + A.cbase + tc) * rows_pad;   // this thread's staged channel
+    const unsigned sbase = lds_addr(stg);
     for (int l = lg0; l < lg1; ++l) {
         if (A.zero[l]) continue;
         const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
@@ -534,88 +622,97 @@ __global__ __launch_bounds__(256, 4) void k_grad_q_mfma(const bf16_t *__restrict
         const int xs = max(bw_wave_min(live ? iu : BIG), 0), xe = min(bw_wave_max(live ? iu : -BIG) + nu - 1, Wl - 1);
         const int nx = xe - xs + 1;
         const int nrows = (ye >= ys && nx > 0) ? (ye - ys + 1) * nx : 0;
-        const int zlo = max(bw_wave_min(live ? iv : BIG), 0);
+        // z batches of 16 from an 8-aligned start (16-byte aligned target rows)
+        const int zlo = max(bw_wave_min(live ? iv : BIG), 0) & ~7;
         const int zhi = min(bw_wave_max(live ? iv : -BIG) + nv - 1, Dl - 1);
         const int nzb = zhi >= zlo ? (zhi - zlo + 16) >> 4 : 0;
-        // the staged query's window origin and gradient rows
-        const int gsrc = sq & 63;   // (sq < 64 always: 256 threads / 4)
-        const int oh_s = __shfl(ih, gsrc), ou_s = __shfl(iu, gsrc), ov_s = __shfl(iv, gsrc);
-        const bool lv_s = __shfl((int)live, gsrc) != 0;
-        const long long q_s = (long long)__shfl((int)q, gsrc);
-        const float *g_s = A.gwin + A.goff[l] + ((long long)b * A.Nq + q_s) * bw_nw3(A, l);
-        // iteration sequence (identical in every wave): union rows that some window of the box contains, each
-        // with its nzb z batches
-        auto row_live = [&](int row) {
-            const int y = ys + row / nx, x = xs + row % nx;
-            const bool rk = live && (unsigned)(y - ih) < (unsigned)nh && (unsigned)(x - iu) < (unsigned)nu;
-            return __ballot(rk) != 0;
-        };
-        auto next_row = [&](int row) {
-            while (row < nrows && !row_live(row)) ++row;
-            return row;
-        };
-        // staged registers of one batch
-        u32x4 treg;
-        u32x2 ghr, glr;
-        auto load = [&](int row, int zb) {
-            const int y = ys + row / nx, x = xs + row % nx;
-            const int z0 = zlo + 16 * zb;
-            const long long trow = A.off[l] + ((long long)y * Wl + x) * Dpl;
-            treg = u32x4{0u, 0u, 0u, 0u};
-            if (tcok) __builtin_memcpy(&treg, tb + trow + z0 + 8 * th, 16);
-            const int wy = y - oh_s, wx = x - ou_s;
-            const bool rok = lv_s && (unsigned)wy < (unsigned)nh && (unsigned)wx < (unsigned)nu;
-            const float *gr = g_s + (wy * nu + wx) * nv;
-            float g[4];
+        // the box's window gradients of this level as one buffer (the box spans < 4 (W, D) planes of queries)
+        const int nw3 = (int)bw_nw3(A, l);
+        const u32x4 rs_g = sgpr_rsrc(A.gwin + A.goff[l] + ((long long)b * A.Nq + qb0) * nw3,
+                                     (unsigned)min((long long)(3 * A.Wq * A.Dq + 3 * A.Dq + 4) * nw3 * 4, 0x7fffffffLL));
+        // this thread's four G queries: window origin and first gradient (bytes)
+        int goh[4], gou[4], gov[4], gqo[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int wz = z0 + 4 * sp + k - ov_s;
-                g[k] = rok && (unsigned)wz < (unsigned)nv ? gr[wz] : 0.0f;
+        for (int k = 0; k < 4; ++k) {
+            const int gq = 16 * w + 4 * k + (lane >> 4);
+            // (every shuffle runs on all lanes: under a branch, ds_bpermute reads 0 from switched-off lanes)
+            const bool lv = __shfl((int)live, gq) != 0;
+            const int sh = __shfl(ih, gq);
+            goh[k] = lv ? sh : -BIG;   // (dead / inactive queries take no values)
+            gou[k] = __shfl(iu, gq);
+            gov[k] = __shfl(iv, gq) - 4 * (((lane >> 2) & 3) ^ ((gq >> 2) & 3)) - (lane & 3);
+            gqo[k] = __shfl(qrel, gq) * nw3;
+        }
+        const unsigned tvl = tvo + (unsigned)(A.off[l] * 2);
+        // one batch's DMAs into stage st: 1 T + 4 G per thread
+        auto issue = [&](int it, int st) {
+            const unsigned e = qrows[it];
+            const int y = (int)(e & 2047u), x = (int)((e >> 11) & 2047u), z0 = (int)(e >> 22);
+            const unsigned sb = sbase + st * STAGE;
+            if (!(DVC_GQ_ABL & 4)) blds(rs_t, tvl + (unsigned)(((y * Wl + x) * Dpl + z0) * 2), sb + 1024 * w, W16{});
+#pragma unroll
+            for (int k = 0; k < 4 && !(DVC_GQ_ABL & 2); ++k) {
+                const int wy = y - goh[k], wx = x - gou[k], wz = z0 - gov[k];
+                const bool ok = (unsigned)wy < (unsigned)nh && (unsigned)wx < (unsigned)nu && (unsigned)wz < (unsigned)nv;
+                blds(rs_g, ok ? (unsigned)((gqo[k] + (wy * nu + wx) * nv + wz) * 4) : kOOB, sb + 4096 + 256 * (4 * w + k),
+                     W4{});
             }
-            unsigned hi[4], lo[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const __bf16 hb = (__bf16)g[k];
-                hi[k] = __builtin_bit_cast(unsigned short, hb);
-                lo[k] = __builtin_bit_cast(unsigned short, (__bf16)(g[k] - (float)hb));
-            }
-            ghr = u32x2{hi[0] | (hi[1] << 16), hi[2] | (hi[3] << 16)};
-            glr = u32x2{lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16)};
         };
-        auto store = [&](int buf) {
-            *reinterpret_cast<u32x4 *>(&Tl[buf][tc][8 * th]) = treg;
-            *reinterpret_cast<u32x2 *>(&Gh[buf][sq][4 * sp]) = ghr;
-            *reinterpret_cast<u32x2 *>(&Gl[buf][sq][4 * sp]) = glr;
-        };
-        int row = nzb > 0 ? next_row(0) : nrows, zb = 0;
-        if (row >= nrows) continue;
-        __syncthreads();   // the previous level's last batch has been read
-        load(row, zb);
-        store(0);
-        __syncthreads();
-        int buf = 0;
-        while (true) {
-            // the next batch: next z batch of this row, else the next live row
-            int nrow = row, nzbi = zb + 1;
-            if (nzbi >= nzb) { nzbi = 0; nrow = next_row(row + 1); }
-            const bool more = nrow < nrows;
-            if (more) load(nrow, nzbi);
-            if (w < NCT) {
-                const bf16x8 bt = *reinterpret_cast<const bf16x8 *>(&Tl[buf][32 * w + m][8 * h]);
-#pragma unroll
-                for (int T = 0; T < 2; ++T) {
-                    const bf16x8 ah = *reinterpret_cast<const bf16x8 *>(&Gh[buf][32 * T + m][8 * h]);
-                    const bf16x8 al = *reinterpret_cast<const bf16x8 *>(&Gl[buf][32 * T + m][8 * h]);
-                    acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bt, acc[T], 0, 0, 0);
-                    acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bt, acc[T], 0, 0, 0);
+        // the batches: every z batch of each union row some window of the box contains, listed by wave 0 (lane =
+        // query, one ballot per row), at most kQRows at a time; no divisions in the batch loop
+        for (int rnext = nzb > 0 ? 0 : nrows; rnext < nrows;) {
+            __syncthreads();   // the previous batches and list have been read (no DMA in flight here)
+            if (w == 0) {
+                int cnt = 0, row0 = rnext;
+                int y = ys + row0 / nx, x = xs + row0 % nx;
+                for (; row0 < nrows && cnt + nzb <= kQRows; ++row0) {
+                    const bool rk = live && (unsigned)(y - ih) < (unsigned)nh && (unsigned)(x - iu) < (unsigned)nu;
+                    if (__ballot(rk) != 0) {
+                        if (lane < nzb)
+                            qrows[cnt + lane] = (unsigned)y | ((unsigned)x << 11) | ((unsigned)(zlo + 16 * lane) << 22);
+                        cnt += nzb;
+                    }
+                    if (++x > xe) { x = xs; ++y; }
+                }
+                if (lane == 0) {
+                    qrows[kQRows] = cnt;
+                    qrows[kQRows + 1] = row0;
                 }
             }
-            if (!more) break;
-            store(buf ^ 1);
             __syncthreads();
-            buf ^= 1;
-            row = nrow;
-            zb = nzbi;
+            const int nit = (int)qrows[kQRows];
+            rnext = (int)qrows[kQRows + 1];
+            if (nit == 0) continue;
+            // batches 0 .. kQStages - 2 in flight (past the end: the last batch again, into a stage never read)
+#pragma unroll
+            for (int k = 0; k < kQStages - 1; ++k) issue(min(k, nit - 1), k);
+            for (int it = 0; it < nit; ++it) {
+                // batch it has landed (this thread's DMAs; kQStages - 2 newer batches may fly), then every thread's
+                // has, and every wave is done with batch it - 1, whose stage the next DMA refills
+                constexpr int kDma = ((DVC_GQ_ABL & 4) ? 0 : 1) + ((DVC_GQ_ABL & 2) ? 0 : 4);   // DMAs per batch
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kDma * (kQStages - 2)) : "memory");
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+                issue(min(it + kQStages - 1, nit - 1), (it + kQStages - 1) % kQStages);
+                if (w < NCT && !(DVC_GQ_ABL & 1)) {
+                    const unsigned char *sb = stg + (it % kQStages) * STAGE;
+                    const int r = 32 * w + m, rsw = (r >> 3) & 1;
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {   // z 8 j .. 8 j + 7: K = 16 (z, hi/lo) pairs
+                        // B: this lane's 4 targets z = 8 j + 4 h .. + 3 of channel r, each twice
+                        const u32x2 tv = *reinterpret_cast<const u32x2 *>(sb + r * 32 + 16 * (j ^ rsw) + 8 * h);
+                        const bf16x8 bt = dup_bf16x4(tv);
+#pragma unroll
+                        for (int T = 0; T < 2; ++T) {
+                            const int gq = 32 * T + m, sw = (gq >> 2) & 3;
+                            const bf16x8 ag =
+                                *reinterpret_cast<const bf16x8 *>(sb + 4096 + gq * 64 + 16 * ((2 * j + h) ^ sw));
+                            acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ag, bt, acc[T], 0, 0, 0);
+                        }
+                    }
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tail's duplicate DMAs have landed
         }
     }
     if (w >= NCT) return;
@@ -892,7 +989,7 @@ __global__ __launch_bounds__(256, 4) void k_grad_t_mfma(const bf16_t *__restrict
     const int ox0 = bx * 4, ox1 = min(bx * 4 + 3, Wl - 1) + nu - 1;
     const int oz0 = bz * 4, oz1 = min(bz * 4 + 3, Dl - 1) + nv - 1;
     const int nox = ox1 - ox0 + 1, nrows = (oy1 - oy0 + 1) * nox;
-    const float *gl = A.gwin + A.goff[l] + (long long)b * A.Nq * nw3;
+    const unsigned *glp = reinterpret_cast<const unsigned *>(A.gwin + A.goff[l] + (long long)b * A.Nq * nw3);
     const bf16_t *qrow = Qt + (long long)(A.cbase + tc) * NqPad;   // this thread's staged channel
     f32x16 acc[2];
 #pragma unroll
@@ -924,24 +1021,17 @@ __global__ __launch_bounds__(256, 4) void k_grad_t_mfma(const bf16_t *__restrict
             auto load = [&](int kb) {
                 qreg = u32x4{0u, 0u, 0u, 0u};
                 if (tcok) __builtin_memcpy(&qreg, qrow + base + 16 * kb + 8 * th, 16);   // (zero-padded past the keys)
-                float g[4];
+                unsigned d[4];   // bf16_hilo pairs (k_win_grad<R, true>)
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const int idx = 16 * kb + 4 * sp + k;
                     const bool in = idx < nk;
                     const int qq = __shfl(qq_l, in ? idx : 0);
                     const int pz = tz - __shfl(oz_l, in ? idx : 0) + nv - 1;
-                    g[k] = in && yxok && (unsigned)pz < (unsigned)nv ? gl[(long long)qq * nw3 + pyx + pz] : 0.0f;
+                    d[k] = in && yxok && (unsigned)pz < (unsigned)nv ? glp[(long long)qq * nw3 + pyx + pz] : 0u;
                 }
-                unsigned hi[4], lo[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const __bf16 hb = (__bf16)g[k];
-                    hi[k] = __builtin_bit_cast(unsigned short, hb);
-                    lo[k] = __builtin_bit_cast(unsigned short, (__bf16)(g[k] - (float)hb));
-                }
-                ghr = u32x2{hi[0] | (hi[1] << 16), hi[2] | (hi[3] << 16)};
-                glr = u32x2{lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16)};
+                ghr = u32x2{(d[0] & 0xffffu) | (d[1] << 16), (d[2] & 0xffffu) | (d[3] << 16)};
+                glr = u32x2{(d[0] >> 16) | (d[1] & 0xffff0000u), (d[2] >> 16) | (d[3] & 0xffff0000u)};
             };
             auto store = [&](int bb) {
                 *reinterpret_cast<u32x4 *>(&Ql[bb][tc][8 * th]) = qreg;
@@ -1186,6 +1276,11 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     bf16_t *qt = (bf16_t *)(ws + P.gwin + P.dq + P.dt + 2 * P.keys + P.starts + P.temp + P.part);
     bf16_t *ttr = (bf16_t *)(ws + P.gwin + P.dq + P.dt + 2 * P.keys + P.starts + P.temp + P.part + P.qt);
     A.gwin = (float *)(ws + 256);
+    // the 256-byte guard before the window gradients is the zero source of the MFMA kernels' LDS-DMA gathers
+    if (hipMemsetAsync(ws, 0, 256, s) != hipSuccess) {
+        snprintf(err, errlen, "corr_backward: guard clear failed");
+        return DVC_ERR_RUNTIME;
+    }
     auto launched = [&](const char *what) {
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) {
@@ -1196,12 +1291,12 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     };
     const long long nqb = (A.Nq + 63) / 64;
     const int ngroups = (A.Cp + 127) / 128;   // 128-channel groups: one launch of each gradient kernel per group
-    k_win_grad<R><<<(unsigned)((A.B * A.L * nqb + 3) / 4), 256, 0, s>>>(A);
+    k_win_grad<R, std::is_same<TT, bf16_t>::value><<<(unsigned)((A.B * A.L * nqb + 3) / 4), 256, 0, s>>>(A);
     if (!launched("win_grad")) return DVC_ERR_LAUNCH;
     bool any_generic = false;
     for (int l = 0; l < A.L; ++l) any_generic |= A.generic[l] != 0;
     if (any_generic) {
-        k_win_grad_generic<R><<<(unsigned)((A.B * A.L * nqb + 3) / 4), 256, 0, s>>>(A);
+        k_win_grad_generic<R, std::is_same<TT, bf16_t>::value><<<(unsigned)((A.B * A.L * nqb + 3) / 4), 256, 0, s>>>(A);
         if (!launched("win_grad_generic")) return DVC_ERR_LAUNCH;
     }
     const long long boxes = (long long)A.B * ((A.Hq + 3) / 4) * ((A.Wq + 3) / 4) * ((A.Dq + 3) / 4);
@@ -1340,6 +1435,12 @@ int corr_backward(const void *packed_q, const void *packed_t, const float *coord
     // all levels' queries (int cell starts) below 2^31
     if (P.coff[lay.num_levels] >= (1LL << 31) - 1 || (long long)lay.num_levels * Nq >= (1LL << 31) - 1) {
         snprintf(err, errlen, "corr_backward: volume too large for 32-bit keys");
+        return DVC_ERR_UNSUPPORTED;
+    }
+    // k_grad_q_mfma lists its batches as y | x << 11 | z << 22
+    if (lay.H[0] >= 2048 || lay.W[0] >= 2048 || lay.D[0] >= 1024) {
+        snprintf(err, errlen, "corr_backward: level 0 of %d x %d x %d exceeds 2047 x 2047 x 1023", lay.H[0], lay.W[0],
+                 lay.D[0]);
         return DVC_ERR_UNSUPPORTED;
     }
     BwdArgs A{};

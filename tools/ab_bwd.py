@@ -18,6 +18,9 @@ from dvccorr import ops  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--size", type=int, default=32)
+ap.add_argument("--shape", default="", help="H,W,D (default: size^3)")
+ap.add_argument("--levels", type=int, default=4)
+ap.add_argument("--radius", type=int, default=4)
 ap.add_argument("--channels", type=int, default=128)
 ap.add_argument("--precision", default="bf16")
 ap.add_argument("--reps", type=int, default=20)
@@ -25,29 +28,30 @@ ap.add_argument("--save", default="")
 ap.add_argument("--compare", default="")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
-S, C, L, R = a.size, a.channels, 4, 4
+S, C, L, R = a.size, a.channels, a.levels, a.radius
+H, W, D = (int(v) for v in a.shape.split(",")) if a.shape else (S, S, S)
 g = torch.Generator(device="cpu").manual_seed(7)
-f1 = torch.randn(1, C, S, S, S, generator=g).to(dev)
-f2 = torch.randn(1, C, S, S, S, generator=g).to(dev)
-c = (torch.stack(torch.meshgrid(*[torch.arange(S, dtype=torch.float32)] * 3, indexing="ij"))[None]
-     + (torch.rand(1, 3, S, S, S, generator=g) * 4 - 2)).to(dev)
+f1 = torch.randn(1, C, H, W, D, generator=g).to(dev)
+f2 = torch.randn(1, C, H, W, D, generator=g).to(dev)
+c = (torch.stack(torch.meshgrid(*[torch.arange(n, dtype=torch.float32) for n in (H, W, D)], indexing="ij"))[None]
+     + (torch.rand(1, 3, H, W, D, generator=g) * 4 - 2)).to(dev)
 dt = ops.dtype_code(a.precision)
 q = ops.pack_queries(f1.reshape(1, C, -1), dt)
 t = ops.pack_targets(f2, L, dt)
-gout = torch.randn(1, L * (2 * R + 1) ** 3, S ** 3, generator=g).to(dev)
+gout = torch.randn(1, L * (2 * R + 1) ** 3, H * W * D, generator=g).to(dev)
 cf = c.reshape(1, 3, -1).contiguous()
 for _ in range(3):
-    d1, d2 = ops.corr_backward(q, t, cf, gout, C, S, S, S, L, R, False, dt)
+    d1, d2 = ops.corr_backward(q, t, cf, gout, C, H, W, D, L, R, False, dt)
 torch.cuda.synchronize()
 ts = []
 for _ in range(a.reps):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    d1, d2 = ops.corr_backward(q, t, cf, gout, C, S, S, S, L, R, False, dt)
+    d1, d2 = ops.corr_backward(q, t, cf, gout, C, H, W, D, L, R, False, dt)
     e1.record()
     torch.cuda.synchronize()
     ts.append(e0.elapsed_time(e1))
-d1b, d2b = ops.corr_backward(q, t, cf, gout, C, S, S, S, L, R, False, dt)
+d1b, d2b = ops.corr_backward(q, t, cf, gout, C, H, W, D, L, R, False, dt)
 torch.cuda.synchronize()
 rep = bool(torch.equal(d1, d1b) and torch.equal(d2, d2b))
 print(f"lib={os.path.basename(os.environ.get('DVCCORR_LIB', 'libdvccorr.so'))} size={S} C={C} {a.precision} "
@@ -60,3 +64,7 @@ if a.compare:
         r = ref[k]
         err = ((v.cpu() - r).abs().max() / r.abs().max()).item()
         print(f"  {k}: max|diff|/max|ref| = {err:.3e} bitwise={torch.equal(v.cpu(), r)}")
+        if k == "d1" and err > 1e-3:   # where: per 32-channel tile, per query z
+            dd = (v.cpu() - r).abs()[0]
+            print("    per 32-ch tile:", [round(float(dd[i:i + 32].max()), 4) for i in range(0, dd.shape[0], 32)])
+            print("    per query z:", [round(float(x), 4) for x in dd.reshape(dd.shape[0], H, W, D).amax((0, 1, 2))])
