@@ -547,14 +547,14 @@ __device__ __forceinline__ u32x4 sgpr_rsrc(const void *base, unsigned bytes) {
                  (unsigned)__builtin_amdgcn_readfirstlane(bytes), 0x00020000u};
 }
 template <typename Width>
-__device__ __forceinline__ void blds(u32x4 rs, unsigned voff, unsigned lds, Width) {
-    unsigned keep;
+__device__ __forceinline__ void blds(u32x4 rs, unsigned voff, unsigned soff, unsigned lds, Width) {
+    unsigned keep;   // byte offset voff (per lane) + soff (wave-uniform)
     if constexpr (Width::value == 16)
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
-                     "s_mov_b32 m0, %0" : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds) : "memory");
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
+                     "s_mov_b32 m0, %0" : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds), "s"(soff) : "memory");
     else
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\t"
-                     "s_mov_b32 m0, %0" : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds) : "memory");
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, %4 offen lds\n\t"
+                     "s_mov_b32 m0, %0" : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds), "s"(soff) : "memory");
 }
 using W16 = std::integral_constant<int, 16>;
 using W4 = std::integral_constant<int, 4>;
@@ -646,16 +646,17 @@ __global__ __launch_bounds__(256, 4) void k_grad_q_mfma(const bf16_t *__restrict
         const unsigned tvl = tvo + (unsigned)(A.off[l] * 2);
         // one batch's DMAs into stage st: 1 T + 4 G per thread
         auto issue = [&](int it, int st) {
-            const unsigned e = qrows[it];
+            const unsigned e = __builtin_amdgcn_readfirstlane(qrows[it]);
             const int y = (int)(e & 2047u), x = (int)((e >> 11) & 2047u), z0 = (int)(e >> 22);
             const unsigned sb = sbase + st * STAGE;
-            if (!(DVC_GQ_ABL & 4)) blds(rs_t, tvl + (unsigned)(((y * Wl + x) * Dpl + z0) * 2), sb + 1024 * w, W16{});
+            if (!(DVC_GQ_ABL & 4))   // (the batch's row: a scalar offset)
+                blds(rs_t, tvl, (unsigned)(((y * Wl + x) * Dpl + z0) * 2), sb + 1024 * w, W16{});
 #pragma unroll
             for (int k = 0; k < 4 && !(DVC_GQ_ABL & 2); ++k) {
                 const int wy = y - goh[k], wx = x - gou[k], wz = z0 - gov[k];
                 const bool ok = (unsigned)wy < (unsigned)nh && (unsigned)wx < (unsigned)nu && (unsigned)wz < (unsigned)nv;
-                blds(rs_g, ok ? (unsigned)((gqo[k] + (wy * nu + wx) * nv + wz) * 4) : kOOB, sb + 4096 + 256 * (4 * w + k),
-                     W4{});
+                blds(rs_g, ok ? (unsigned)((gqo[k] + (wy * nu + wx) * nv + wz) * 4) : kOOB, 0u,
+                     sb + 4096 + 256 * (4 * w + k), W4{});
             }
         };
         // the batches: every z batch of each union row some window of the box contains, listed by wave 0 (lane =

@@ -183,7 +183,7 @@ def test_repeatable_under_poisoned_memory():
     """Regression check of the round-2 packed-FP32 hazard: the caching allocator is
     filled with -7 / 3e4 / NaN between calls, so every workspace the kernels get holds stale values; 30
     calls of the case that failed then (12x10x16, C=64, L=3, r=2) must all equal the first, bit for bit.
-    Before the fix 3-5 % of such calls differed in lanes 48-63 of a few chunks (tools/dbg_poison3.py)."""
+    Before the fix 3-5 % of such calls differed in lanes 48-63 of a few chunks (a debug repro of round 2, since folded into this test)."""
     import dvccorr
     from dvccorr import ops
     H, W, D = 12, 10, 16
