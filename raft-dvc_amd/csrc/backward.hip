@@ -583,9 +583,12 @@ __global__ __launch_bounds__(256, 4) void k_grad_q_mfma(const bf16_t *__restrict
     const int bx = t % nbx; t /= nbx;
     const int by = t % nby;
     const int b = t / nby;
-    // level group: y = 0 level 0, y = 1 levels 1 .. L-1 (gridDim.y = 1: every level)
-    const int lg0 = gridDim.y == 1 ? 0 : (blockIdx.y == 0 ? 0 : 1);
-    const int lg1 = gridDim.y == 1 ? A.L : (blockIdx.y == 0 ? 1 : A.L);
+    // level groups (gridDim.y = grad_q_parts(L)): 1 -- every level; 2 -- level 0, then levels 1 .. L-1; 3 -- the
+    // first and second half of level 0's union rows, then levels 1 .. L-1
+    const int np = gridDim.y, py = blockIdx.y;
+    const int lg0 = np == 1 || py < np - 1 ? 0 : 1;
+    const int lg1 = np == 1 ? A.L : (py < np - 1 ? 1 : A.L);
+    const int rhalf = np == 3 && py < 2 ? py + 1 : 0;   // 1 / 2: first / second half of level 0's rows
     // lane-as-query view (union bounds, row list): query i = lane of the box
     const int qy = by * 4 + (lane >> 4), qx = bx * 4 + ((lane >> 2) & 3), qz = bz * 4 + (lane & 3);
     const bool active = qy < A.Hq && qx < A.Wq && qz < A.Dq;
@@ -661,12 +664,13 @@ __global__ __launch_bounds__(256, 4) void k_grad_q_mfma(const bf16_t *__restrict
         };
         // the batches: every z batch of each union row some window of the box contains, listed by wave 0 (lane =
         // query, one ballot per row), at most kQRows at a time; no divisions in the batch loop
-        for (int rnext = nzb > 0 ? 0 : nrows; rnext < nrows;) {
+        const int rend = rhalf == 1 ? nrows / 2 : nrows;
+        for (int rnext = nzb == 0 ? nrows : (rhalf == 2 ? nrows / 2 : 0); rnext < rend;) {
             __syncthreads();   // the previous batches and list have been read (no DMA in flight here)
             if (w == 0) {
                 int cnt = 0, row0 = rnext;
                 int y = ys + row0 / nx, x = xs + row0 % nx;
-                for (; row0 < nrows && cnt + nzb <= kQRows; ++row0) {
+                for (; row0 < rend && cnt + nzb <= kQRows; ++row0) {
                     const bool rk = live && (unsigned)(y - ih) < (unsigned)nh && (unsigned)(x - iu) < (unsigned)nu;
                     if (__ballot(rk) != 0) {
                         if (lane < nzb)
@@ -1211,8 +1215,11 @@ static int grad_t_splits(const dvc_layout &lay, int l, long long Nq) {
     return (int)std::max(1LL, std::min(sp, 256LL));
 }
 
-// k_grad_q_mfma level groups (blockIdx.y): level 0 alone and the coarse levels together, two partial dQ
-static int grad_q_parts(int L) { return L > 1 ? 2 : 1; }
+// k_grad_q_mfma level groups (blockIdx.y): level 0 alone (or its two row halves) and the coarse levels together
+#ifndef DVC_GQ_PARTS
+#define DVC_GQ_PARTS 2
+#endif
+static int grad_q_parts(int L) { return L > 1 ? DVC_GQ_PARTS : 1; }
 
 static long long level_cells(const dvc_layout &lay, int l, const int nw[3]) {
     return (long long)(lay.H[l] + nw[0] - 1) * (lay.W[l] + nw[1] - 1) * (lay.D[l] + nw[2] - 1);
