@@ -89,6 +89,9 @@ struct BwdArgs {
     long long coff[DVC_MAX_LEVELS];
     int gt_blk0[DVC_MAX_LEVELS + 1], gt_sp[DVC_MAX_LEVELS];
     long long gt_poff[DVC_MAX_LEVELS], gt_r0[DVC_MAX_LEVELS + 1];
+    // k_grad_q_mfma's target tiles (k_tile_targets): level l's tiles are [tz0[l], tz0[l + 1]), one per (row (y, x),
+    // 8-aligned z start), each [128 channels][16 z] bf16 = 4 KB
+    long long tz0[DVC_MAX_LEVELS + 1];
 };
 
 // (level, brick, split) of this k_grad_t workgroup (wave-uniform: from blockIdx and the level table)
@@ -489,33 +492,39 @@ __global__ __launch_bounds__(256) void k_grad_q(const TT *__restrict__ Tt, float
 // 2b. bf16 path of step 2 on the matrix cores.  Per 4x4x4 query box, union row (y, x) and
 // 16-target z batch: dQ[64 queries][Cp] += G[64 queries][16 targets] x T[16 targets][Cp] on
 // v_mfma_f32_32x32x16_bf16 (queries = M, channels = N, targets = K); G = the queries' window
-// gradients (8 consecutive z per lane: contiguous in dwin), split into bf16 hi + lo as in 4b.
-// The B operand needs 8 consecutive targets per lane: k_transpose_targets first writes the
-// packed targets channel-major, Ttr[b][c][row] (+32 zero-filled slack elements).
+// gradients as bf16 hi + lo pairs (k_win_grad<R, true>).  The B operand needs consecutive targets
+// per lane: k_tile_targets first writes the packed targets as channel-major 16-z tiles.
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_transpose_targets(const bf16_t *__restrict__ Tt, bf16_t *__restrict__ Ttr,
-                                                           long long rows, long long rows_pad, int Cp) {
-    __shared__ __attribute__((aligned(16))) bf16_t tile[64][128 + 8];
-    const int b = blockIdx.y;
-    const long long r0 = (long long)blockIdx.x * 64;
-    const int cb = 128 * (int)blockIdx.z, cg = min(128, Cp - cb);   // this block's channel group
-    const int nch = cg / 8;
-    const bf16_t *src = Tt + (long long)b * rows * Cp + cb;
-    for (int id = threadIdx.x; id < 64 * nch; id += 256) {
-        const int r = id / nch, ch = id - r * nch;
+// Target tiles of the dQ kernel: per level row (y, x) and 8-aligned z start 8 k, the packed targets of z = 8 k ..
+// 8 k + 15 (zeros past the padded row) of one 128-channel group, channel-major, [c][16 z] bf16 = 4 KB, with the two
+// 16-byte halves of channel c swapped when (c >> 3) & 1 (the dQ kernel's bank-conflict-free B reads).  A batch's
+// target operand is then one contiguous 4 KB LDS-DMA (the channel-major rows of round 2 cost one 128-byte line
+// per 32 bytes used, and the dQ kernel was bound by that L2 traffic).
+__global__ __launch_bounds__(256) void k_tile_targets(const bf16_t *__restrict__ Tt, bf16_t *__restrict__ Tz, BwdArgs A) {
+    __shared__ __attribute__((aligned(16))) bf16_t tile[16][128 + 8];
+    const long long t = blockIdx.x;
+    const int g = blockIdx.y, b = blockIdx.z, ng = gridDim.y;
+    int l = 0;
+    while (l + 1 < A.L && t >= A.tz0[l + 1]) ++l;
+    const int kb = A.Dp[l] >> 3;
+    const long long local = t - A.tz0[l];
+    const long long row = local / kb;
+    const int z0 = 8 * (int)(local - row * kb);
+    const int cb = 128 * g, cg = min(128, A.Cp - cb);
+    const bf16_t *src = Tt + ((long long)b * A.row_stride + A.off[l] + row * A.Dp[l]) * A.Cp + cb;
+    {
+        const int z = threadIdx.x >> 4, ch = threadIdx.x & 15;   // 16 z x 16 chunks of 8 channels
         u32x4 v = {0u, 0u, 0u, 0u};
-        if (r0 + r < rows) v = *reinterpret_cast<const u32x4 *>(src + (r0 + r) * Cp + ch * 8);
-        *reinterpret_cast<u32x4 *>(&tile[r][ch * 8]) = v;
+        if (z0 + z < A.Dp[l] && 8 * ch < cg) v = *reinterpret_cast<const u32x4 *>(src + (long long)(z0 + z) * A.Cp + 8 * ch);
+        *reinterpret_cast<u32x4 *>(&tile[z][8 * ch]) = v;
     }
     __syncthreads();
-    bf16_t *dst = Ttr + ((long long)b * Cp + cb) * rows_pad;
-    for (int id = threadIdx.x; id < cg * 32; id += 256) {
-        const int c = id >> 5, rp = id & 31;
-        if (r0 + 2 * rp < rows_pad) {
-            const unsigned lo = tile[2 * rp][c], hi = tile[2 * rp + 1][c];
-            *reinterpret_cast<unsigned *>(dst + (long long)c * rows_pad + r0 + 2 * rp) = lo | (hi << 16);
-        }
-    }
+    const int c = threadIdx.x >> 1, hh = threadIdx.x & 1;   // channel, logical z half
+    unsigned w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (unsigned)tile[8 * hh + 2 * i][c] | ((unsigned)tile[8 * hh + 2 * i + 1][c] << 16);
+    bf16_t *dst = Tz + (((long long)b * ng + g) * A.tz0[A.L] + t) * 2048 + c * 16 + 8 * (hh ^ ((c >> 3) & 1));
+    *reinterpret_cast<u32x4 *>(dst) = u32x4{w[0], w[1], w[2], w[3]};
 }
 
 // Round 3: the workgroup's four waves split the CHANNELS (wave w = channel tile w of 32), so a wave accumulates
@@ -570,8 +579,8 @@ __device__ __forceinline__ bf16x8 dup_bf16x4(u32x2 v) {
 }
 
 template <int NCT>   // channel tiles of 32 (C_pad / 32, <= 4 per launch)
-__global__ __launch_bounds__(256, 4) void k_grad_q_mfma(const bf16_t *__restrict__ Ttr, long long rows_pad,
-                                                        float *__restrict__ dQp, long long part_stride, BwdArgs A) {
+__global__ __launch_bounds__(256, 4) void k_grad_q_mfma(const bf16_t *__restrict__ Tz, float *__restrict__ dQp,
+                                                        long long part_stride, BwdArgs A) {
     constexpr int STAGE = 8192;                      // bytes: T tile (4 KB, bf16) + G tile (4 KB, hi/lo pairs)
     __shared__ __attribute__((aligned(16))) unsigned char stg[kQStages * STAGE];
     __shared__ unsigned qrows[kQRows + 2];           // batches (y | x << 11 | z0 << 22), count, next row
@@ -596,13 +605,11 @@ __global__ __launch_bounds__(256, 4) void k_grad_q_mfma(const bf16_t *__restrict
     const int qrel = active ? (int)(((long long)qy * A.Wq + qx) * A.Dq + qz - qb0) : 0;
     float cy = 0.0f, cx = 0.0f, cz = 0.0f;
     if (active) load_coords(A.coords, b, A.Nq, qb0 + qrel, cy, cx, cz);
-    // T DMA role: channel tc = 32 w + lane / 2 (clamped into the launch's channels: rows past them are never
-    // read), physical 16-byte chunk lane & 1 of its 32-byte row, holding the z half (lane & 1) ^ (row >> 3 & 1)
-    const int tc = 32 * w + (lane >> 1);
-    const int thalf = (lane & 1) ^ ((tc >> 3) & 1);
-    const int cg = min(128, A.Cp - A.cbase);
-    const u32x4 rs_t = sgpr_rsrc(Ttr + ((long long)b * A.Cp + A.cbase) * rows_pad, (unsigned)(cg * rows_pad * 2));
-    const unsigned tvo = (unsigned)(((long long)(tc < cg ? tc : 0) * rows_pad + 8 * thalf) * 2);
+    // T DMA: the batch's 4 KB target tile (k_tile_targets) as it stands, 16 bytes per thread
+    const long long ntz = A.tz0[A.L];
+    const u32x4 rs_t = sgpr_rsrc(Tz + (((long long)b * ((A.Cp + 127) / 128) + A.cbase / 128) * ntz) * 2048,
+                                 (unsigned)min(ntz * 4096, 0x7fffffffLL));
+    const unsigned tvo = 16u * (unsigned)tid;
     // G DMA role, instruction k: query gq = 16 w + 4 k + lane / 16, physical dword lane & 15 of its 64-byte row =
     // logical z 4 ((lane >> 2 & 3) ^ (gq >> 2 & 3)) + (lane & 3)
     f32x16 acc[2];
@@ -646,14 +653,15 @@ __global__ __launch_bounds__(256, 4) void k_grad_q_mfma(const bf16_t *__restrict
             gov[k] = __shfl(iv, gq) - 4 * (((lane >> 2) & 3) ^ ((gq >> 2) & 3)) - (lane & 3);
             gqo[k] = __shfl(qrel, gq) * nw3;
         }
-        const unsigned tvl = tvo + (unsigned)(A.off[l] * 2);
+        const long long tzl = A.tz0[l];
+        const int kbl = Dpl >> 3;
         // one batch's DMAs into stage st: 1 T + 4 G per thread
         auto issue = [&](int it, int st) {
             const unsigned e = __builtin_amdgcn_readfirstlane(qrows[it]);
             const int y = (int)(e & 2047u), x = (int)((e >> 11) & 2047u), z0 = (int)(e >> 22);
             const unsigned sb = sbase + st * STAGE;
             if (!(DVC_GQ_ABL & 4))   // (the batch's row: a scalar offset)
-                blds(rs_t, tvl, (unsigned)(((y * Wl + x) * Dpl + z0) * 2), sb + 1024 * w, W16{});
+                blds(rs_t, tvo, (unsigned)((tzl + (long long)(y * Wl + x) * kbl + (z0 >> 3)) * 4096), sb + 1024 * w, W16{});
 #pragma unroll
             for (int k = 0; k < 4 && !(DVC_GQ_ABL & 2); ++k) {
                 const int wy = y - goh[k], wx = x - gou[k], wz = z0 - gov[k];
@@ -1182,7 +1190,7 @@ struct BwdPlan {
     long long coff[DVC_MAX_LEVELS + 1];   // first window-origin cell of each level in the merged key space
     int sp[DVC_MAX_LEVELS];               // k_grad_t splits per brick
     long long poff[DVC_MAX_LEVELS];       // split-partial offsets (floats)
-    long long rows_pad;  // Ttr row length (pyramid rows + slack for the 16-target batches)
+    long long tz0[DVC_MAX_LEVELS + 1];   // k_tile_targets: first tile of each level
     long long nq_pad;   // Qt row length (sorted queries + zero padding for the 16-query batches)
     int nw[DVC_MAX_LEVELS][3];   // window box (h, u, v) per level
     long long goff[DVC_MAX_LEVELS];
@@ -1258,8 +1266,13 @@ static void bwd_plan(int B, long long Nq, const dvc_layout &lay, int radius, boo
     P.part = al256(std::max<size_t>(part, 256));
     P.nq_pad = ((nkeys + 16 + 63) / 64) * 64;
     P.qt = al256((size_t)P.nq_pad * lay.c_pad * sizeof(bf16_t));   // bf16 path only (sized always)
-    P.rows_pad = ((lay.row_stride + 32 + 1) / 2) * 2;
-    P.ttr = al256((size_t)B * lay.c_pad * P.rows_pad * sizeof(bf16_t));   // bf16 path only (sized always)
+    long long nt = 0;
+    for (int l = 0; l < L; ++l) {
+        P.tz0[l] = nt;
+        nt += (long long)lay.H[l] * lay.W[l] * (lay.Dp[l] / 8);
+    }
+    P.tz0[L] = nt;
+    P.ttr = al256((size_t)B * ((lay.c_pad + 127) / 128) * nt * 4096);   // bf16 path only (sized always)
     P.total = P.gwin + P.dq + P.dt + 2 * P.keys + P.starts + P.temp + P.part + P.qt + P.ttr;
 }
 
@@ -1312,18 +1325,18 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     const int qparts = std::is_same<TT, bf16_t>::value ? grad_q_parts(A.L) : 1;
     const long long qstride = (long long)A.B * A.Nq * A.Cp;
     if constexpr (std::is_same<TT, bf16_t>::value) {
-        dim3 tg((unsigned)((P.rows_pad + 63) / 64), (unsigned)A.B, (unsigned)ngroups);
-        k_transpose_targets<<<tg, 256, 0, s>>>(Tt, ttr, A.row_stride, P.rows_pad, A.Cp);
-        if (!launched("transpose_targets")) return DVC_ERR_LAUNCH;
+        for (int l = 0; l <= A.L; ++l) A.tz0[l] = P.tz0[l];
+        k_tile_targets<<<dim3((unsigned)P.tz0[A.L], (unsigned)ngroups, (unsigned)A.B), 256, 0, s>>>(Tt, ttr, A);
+        if (!launched("tile_targets")) return DVC_ERR_LAUNCH;
         const dim3 qg((unsigned)boxes, (unsigned)qparts);   // level groups: {0}, {1 .. L-1}
         for (int g = 0; g < ngroups; ++g) {
             BwdArgs Ag = A;
             Ag.cbase = 128 * g;
             switch (std::min(128, A.Cp - Ag.cbase) / 32) {
-            case 1: k_grad_q_mfma<1><<<qg, 256, 0, s>>>(ttr, P.rows_pad, dq, qstride, Ag); break;
-            case 2: k_grad_q_mfma<2><<<qg, 256, 0, s>>>(ttr, P.rows_pad, dq, qstride, Ag); break;
-            case 3: k_grad_q_mfma<3><<<qg, 256, 0, s>>>(ttr, P.rows_pad, dq, qstride, Ag); break;
-            default: k_grad_q_mfma<4><<<qg, 256, 0, s>>>(ttr, P.rows_pad, dq, qstride, Ag); break;
+            case 1: k_grad_q_mfma<1><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag); break;
+            case 2: k_grad_q_mfma<2><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag); break;
+            case 3: k_grad_q_mfma<3><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag); break;
+            default: k_grad_q_mfma<4><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag); break;
             }
         }
     } else {
