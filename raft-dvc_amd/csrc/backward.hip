@@ -930,57 +930,56 @@ __global__ __launch_bounds__(256) void k_grad_t(const TT *__restrict__ Qp, const
 }
 
 // ---------------------------------------------------------------------------------
-// 4b. bf16 path of step 4 on the matrix cores.  Per target brick and batch of 16 streamed
-// queries, dT[64 targets][Cp] += G[64 targets][16 queries] x Q[16 queries][Cp] on
-// v_mfma_f32_32x32x16_bf16 (targets = M, channels = N, queries = K).  G (the fp32 window
-// gradients) enters as two bf16 terms, hi = bf16(g) and lo = bf16(g - hi), so the product
-// keeps ~16 mantissa bits of g (Q is bf16 already): two MFMAs per tile.  The B operand needs 8
-// consecutive queries per lane: k_qt_sorted first writes Q transposed and permuted into the
-// level's sorted order, Qt[c][i] = Q[q_i][c] (zeros past Nq), so a lane's 8 queries are one
-// 16-byte load.
+// 4b. bf16 path of step 4 on the matrix cores.  Per target brick and batch of 16 streamed queries,
+// dT[64 targets][Cp] += G[64 targets][16 queries] x Q[16 queries][Cp] on v_mfma_f32_32x32x16_bf16 (targets =
+// M, channels = N, K = (query, hi/lo)): G enters as the bf16_hilo pairs k_win_grad wrote (hi = bf16(g), lo =
+// bf16(g - hi): the products keep ~16 mantissa bits of g; Q is bf16 already) and the B operand repeats each
+// query row twice.  k_qt_tiles first writes the queries in the sorted order as channel-major tiles of 16 sorted
+// positions from every 8-aligned start, [128 ch][16] bf16 = 4 KB (the halves of channel c swapped when
+// (c >> 3) & 1), so a batch's B operand is one contiguous tile.
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_qt_sorted(const bf16_t *__restrict__ Q,
-                                                   const unsigned long long *__restrict__ keys,
-                                                   bf16_t *__restrict__ Qt, long long Nq, long long nkeys,
-                                                   long long NqPad, int Cp, int b) {
-    __shared__ __attribute__((aligned(16))) bf16_t tile[64][128 + 8];
-    const long long i0 = (long long)blockIdx.x * 64;
-    const int cb = 128 * (int)blockIdx.y, cg = min(128, Cp - cb);   // this block's channel group
-    const int nch = cg / 8;
-    for (int id = threadIdx.x; id < 64 * nch; id += 256) {
-        const int r = id / nch, ch = id - r * nch;
+__global__ __launch_bounds__(256) void k_qt_tiles(const bf16_t *__restrict__ Q, const unsigned long long *__restrict__ keys,
+                                                  bf16_t *__restrict__ Qz, long long Nq, long long nkeys, int Cp, int b) {
+    __shared__ __attribute__((aligned(16))) bf16_t tile[16][128 + 8];
+    const long long t = blockIdx.x, ntq = gridDim.x;
+    const int g = blockIdx.y, cb = 128 * g, cg = min(128, Cp - cb);
+    {
+        const int r = threadIdx.x >> 4, ch = threadIdx.x & 15;   // 16 sorted positions x 16 chunks of 8 channels
+        const long long i = 8 * t + r;
         u32x4 v = {0u, 0u, 0u, 0u};
-        if (i0 + r < nkeys) {
-            const long long q = (long long)(keys[i0 + r] & 0xffffffffull);
-            v = *reinterpret_cast<const u32x4 *>(Q + ((long long)b * Nq + q) * Cp + cb + ch * 8);
+        if (i < nkeys && 8 * ch < cg) {
+            const long long q = (long long)(keys[i] & 0xffffffffull);
+            v = *reinterpret_cast<const u32x4 *>(Q + ((long long)b * Nq + q) * Cp + cb + 8 * ch);
         }
-        *reinterpret_cast<u32x4 *>(&tile[r][ch * 8]) = v;
+        *reinterpret_cast<u32x4 *>(&tile[r][8 * ch]) = v;
     }
     __syncthreads();
-    for (int id = threadIdx.x; id < cg * 32; id += 256) {
-        const int c = id >> 5, qp = id & 31;
-        const unsigned lo = tile[2 * qp][c], hi = tile[2 * qp + 1][c];
-        *reinterpret_cast<unsigned *>(Qt + (long long)(cb + c) * NqPad + i0 + 2 * qp) = lo | (hi << 16);
-    }
+    const int c = threadIdx.x >> 1, hh = threadIdx.x & 1;
+    unsigned w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (unsigned)tile[8 * hh + 2 * i][c] | ((unsigned)tile[8 * hh + 2 * i + 1][c] << 16);
+    bf16_t *dst = Qz + ((long long)g * ntq + t) * 2048 + c * 16 + 8 * (hh ^ ((c >> 3) & 1));
+    *reinterpret_cast<u32x4 *>(dst) = u32x4{w[0], w[1], w[2], w[3]};
 }
 
 // Round 3: as k_grad_q_mfma, the four waves split the channels (wave w = channel tile w: dT[64 targets][32 ch]
-// in 32 registers, no cross-wave reduction) and every (16-query batch) is staged once per workgroup into a
-// double-buffered LDS tile: the sorted+transposed query rows Qt[128 ch][16] (one 16-byte load per thread) and
-// the 64 targets' window gradients G[64][16 queries] as bf16 hi + lo (four gathers per thread); the next
-// batch's loads fly while the current one's MFMAs run.  The 64-query chunks of the brick's origin rows are
-// dealt to the workgroups of the brick (splits).
+// in 32 registers, no cross-wave reduction) and every batch of 16 sorted queries, aligned to 8 (queries of the
+// batch outside the chunk take no gradient), is staged once per workgroup into a double-buffered LDS tile: the
+// batch's query tile (k_qt_tiles: one 16-byte load per thread) and G[64 targets][16 queries] as hi/lo pairs,
+// thread (query j, brick row r) loading the 4 z-consecutive targets of its row from query j's window in one
+// 16-byte load (the round-2 layout of this loop gathered 4-byte values from 64 windows per instruction and
+// was bound by that L2 traffic).  The 64-query chunks of the brick's origin rows are dealt to the workgroups of
+// the brick (splits).
 template <int NCT>   // channel tiles of 32 (C_pad / 32, <= 4 per launch)
-__global__ __launch_bounds__(256, 4) void k_grad_t_mfma(const bf16_t *__restrict__ Qt, long long NqPad,
+__global__ __launch_bounds__(256, 4) void k_grad_t_mfma(const bf16_t *__restrict__ Qz, long long ntq,
                                                         const unsigned long long *__restrict__ keys,
                                                         const int *__restrict__ starts, float *__restrict__ dT,
                                                         float *__restrict__ dTp, BwdArgs A, int b) {
     const GtBlock gb = gt_block(A);
     const int l = gb.l, nsplit = gb.nsplit, split = gb.split, brick = gb.brick;
     starts += A.coff[l];
-    __shared__ __attribute__((aligned(16))) bf16_t Ql[2][128][16];   // [buf][channel][query]
-    __shared__ __attribute__((aligned(16))) bf16_t Gh[2][64][16];    // [buf][target][query], hi part
-    __shared__ __attribute__((aligned(16))) bf16_t Gl[2][64][16];    // lo part
+    __shared__ __attribute__((aligned(16))) bf16_t Ql[2][2048];     // [buf] query tile [128 ch][16] (swizzled)
+    __shared__ __attribute__((aligned(16))) unsigned Gq[2][64][16];  // [buf][target][query] hi/lo pairs (swizzled)
     const int tid = threadIdx.x, lane = tid & 63, m = lane & 31, h = lane >> 5;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
@@ -991,19 +990,18 @@ __global__ __launch_bounds__(256, 4) void k_grad_t_mfma(const bf16_t *__restrict
     const int bz = t % nbz; t /= nbz;
     const int bx = t % nbx;
     const int by = t / nbx;
-    // staging roles: Q -- channel tc = tid >> 1, query half th; G -- target st = tid >> 2, query quarter sp
-    const int tc = tid >> 1, th = tid & 1;
-    const int st = tid >> 2, sp = tid & 3;
-    const bool tcok = tc < 32 * NCT;
-    const int ty = by * 4 + (st >> 4), tx = bx * 4 + ((st >> 2) & 3), tz = bz * 4 + (st & 3);
-    const bool tval = ty < Hl && tx < Wl && tz < Dl;
+    // G staging role: query j of the batch, brick row r = (ty, tx), its targets z = 4 bz .. 4 bz + 3
+    const int sj = tid & 15, sr = tid >> 4;
+    const int ty = by * 4 + (sr >> 2), tx = bx * 4 + (sr & 3);
+    const int tz0 = bz * 4;
+    const bool rval = ty < Hl && tx < Wl;
     const int CX = Wl + nu - 1, CZ = Dl + nv - 1;
     const int oy0 = by * 4, oy1 = min(by * 4 + 3, Hl - 1) + nh - 1;
     const int ox0 = bx * 4, ox1 = min(bx * 4 + 3, Wl - 1) + nu - 1;
     const int oz0 = bz * 4, oz1 = min(bz * 4 + 3, Dl - 1) + nv - 1;
     const int nox = ox1 - ox0 + 1, nrows = (oy1 - oy0 + 1) * nox;
     const unsigned *glp = reinterpret_cast<const unsigned *>(A.gwin + A.goff[l] + (long long)b * A.Nq * nw3);
-    const bf16_t *qrow = Qt + (long long)(A.cbase + tc) * NqPad;   // this thread's staged channel
+    const bf16_t *qz = Qz + (long long)(A.cbase / 128) * ntq * 2048 + 8 * tid;   // + tile * 2048: this thread's 16 B
     f32x16 acc[2];
 #pragma unroll
     for (int T = 0; T < 2; ++T)
@@ -1020,38 +1018,41 @@ __global__ __launch_bounds__(256, 4) void k_grad_t_mfma(const bf16_t *__restrict
     deal_chunks(nrows, split, nsplit, lane, range, [&](int row, int s, int e, int c1) {
         const int oy = oy0 + row / nox, ox = ox0 + row % nox;
         const long long cbase = ((long long)oy * CX + ox) * CZ + A.coff[l];   // (keys hold global cells)
-        // window position (y, x) of the staged target for a query of origin o' = (oy, ox, *)
+        // window position (y, x) of the staged brick row for a query of origin o' = (oy, ox, *)
         const int py = ty - oy + nh - 1, px = tx - ox + nu - 1;
-        const bool yxok = tval && (unsigned)py < (unsigned)nh && (unsigned)px < (unsigned)nu;
+        const bool yxok = rval && (unsigned)py < (unsigned)nh && (unsigned)px < (unsigned)nu;
         const int pyx = (py * nu + px) * nv;
         for (int base = s + 64 * c1; base < e; base += 64 * nsplit) {
             const int nk = min(64, e - base);
             const unsigned long long key = lane < nk ? keys[base + lane] : 0ull;
             const int qq_l = (int)(unsigned)(key & 0xffffffffu);
             const int oz_l = (int)((long long)(key >> 32) - cbase);
-            u32x4 qreg;
-            u32x2 ghr, glr;
+            const int p0 = base & ~7;   // batches of 16 sorted positions from 8-aligned starts
+            u32x4 qreg, gv;
             auto load = [&](int kb) {
-                qreg = u32x4{0u, 0u, 0u, 0u};
-                if (tcok) __builtin_memcpy(&qreg, qrow + base + 16 * kb + 8 * th, 16);   // (zero-padded past the keys)
-                unsigned d[4];   // bf16_hilo pairs (k_win_grad<R, true>)
+                const int p = p0 + 16 * kb;
+                __builtin_memcpy(&qreg, qz + (long long)(p >> 3) * 2048, 16);
+                const int idx = p + sj - base;
+                const bool in = (unsigned)idx < (unsigned)nk;
+                const int qq = __shfl(qq_l, in ? idx : 0);
+                const int pz0 = tz0 - __shfl(oz_l, in ? idx : 0) + nv - 1;
+                gv = u32x4{0u, 0u, 0u, 0u};
+                // (4 consecutive window z: one 16-byte load; values outside the window row are masked below, and
+                // the loads past either end of the gradient buffer fall in its 256-byte guards)
+                if (in && yxok && pz0 > -4 && pz0 < nv) __builtin_memcpy(&gv, glp + (long long)qq * nw3 + pyx + pz0, 16);
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int idx = 16 * kb + 4 * sp + k;
-                    const bool in = idx < nk;
-                    const int qq = __shfl(qq_l, in ? idx : 0);
-                    const int pz = tz - __shfl(oz_l, in ? idx : 0) + nv - 1;
-                    d[k] = in && yxok && (unsigned)pz < (unsigned)nv ? glp[(long long)qq * nw3 + pyx + pz] : 0u;
-                }
-                ghr = u32x2{(d[0] & 0xffffu) | (d[1] << 16), (d[2] & 0xffffu) | (d[3] << 16)};
-                glr = u32x2{(d[0] >> 16) | (d[1] & 0xffff0000u), (d[2] >> 16) | (d[3] & 0xffff0000u)};
+                for (int k = 0; k < 4; ++k)
+                    if (!((unsigned)(pz0 + k) < (unsigned)nv && tz0 + k < Dl)) gv[k] = 0u;
             };
             auto store = [&](int bb) {
-                *reinterpret_cast<u32x4 *>(&Ql[bb][tc][8 * th]) = qreg;
-                *reinterpret_cast<u32x2 *>(&Gh[bb][st][4 * sp]) = ghr;
-                *reinterpret_cast<u32x2 *>(&Gl[bb][st][4 * sp]) = glr;
+                *reinterpret_cast<u32x4 *>(&Ql[bb][8 * tid]) = qreg;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {   // target 4 sr + k, query sj: chunk (sj / 4) ^ (row >> 2 & 3)
+                    const int tr = 4 * sr + k;
+                    Gq[bb][tr][4 * ((sj >> 2) ^ ((tr >> 2) & 3)) + (sj & 3)] = gv[k];
+                }
             };
-            const int nb = (nk + 15) >> 4;
+            const int nb = (base + nk - p0 + 15) >> 4;
             load(0);
             __syncthreads();   // the previous chunk's last batch has been read
             store(buf);
@@ -1060,13 +1061,18 @@ __global__ __launch_bounds__(256, 4) void k_grad_t_mfma(const bf16_t *__restrict
                 const bool more = kb + 1 < nb;
                 if (more) load(kb + 1);
                 if (w < NCT) {
-                    const bf16x8 bq = *reinterpret_cast<const bf16x8 *>(&Ql[buf][32 * w + m][8 * h]);
+                    const int r = 32 * w + m, rsw = (r >> 3) & 1;
 #pragma unroll
-                    for (int T = 0; T < 2; ++T) {
-                        const bf16x8 ah = *reinterpret_cast<const bf16x8 *>(&Gh[buf][32 * T + m][8 * h]);
-                        const bf16x8 al = *reinterpret_cast<const bf16x8 *>(&Gl[buf][32 * T + m][8 * h]);
-                        acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bq, acc[T], 0, 0, 0);
-                        acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bq, acc[T], 0, 0, 0);
+                    for (int j = 0; j < 2; ++j) {   // queries 8 j .. 8 j + 7: K = 16 (query, hi/lo) pairs
+                        const u32x2 qv = *reinterpret_cast<const u32x2 *>(
+                            reinterpret_cast<const unsigned char *>(Ql[buf]) + r * 32 + 16 * (j ^ rsw) + 8 * h);
+                        const bf16x8 bq = dup_bf16x4(qv);
+#pragma unroll
+                        for (int T = 0; T < 2; ++T) {
+                            const int tr = 32 * T + m;
+                            const bf16x8 ag = *reinterpret_cast<const bf16x8 *>(&Gq[buf][tr][4 * ((2 * j + h) ^ ((tr >> 2) & 3))]);
+                            acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ag, bq, acc[T], 0, 0, 0);
+                        }
                     }
                 }
                 if (more) {
@@ -1191,7 +1197,7 @@ struct BwdPlan {
     int sp[DVC_MAX_LEVELS];               // k_grad_t splits per brick
     long long poff[DVC_MAX_LEVELS];       // split-partial offsets (floats)
     long long tz0[DVC_MAX_LEVELS + 1];   // k_tile_targets: first tile of each level
-    long long nq_pad;   // Qt row length (sorted queries + zero padding for the 16-query batches)
+    long long ntq;      // k_qt_tiles: query tiles (one per 8-aligned sorted position)
     int nw[DVC_MAX_LEVELS][3];   // window box (h, u, v) per level
     long long goff[DVC_MAX_LEVELS];
 };
@@ -1264,8 +1270,8 @@ static void bwd_plan(int B, long long Nq, const dvc_layout &lay, int radius, boo
                                    (size_t)nkeys, 0u, 64u, (hipStream_t)0);
     P.temp = al256(tb);
     P.part = al256(std::max<size_t>(part, 256));
-    P.nq_pad = ((nkeys + 16 + 63) / 64) * 64;
-    P.qt = al256((size_t)P.nq_pad * lay.c_pad * sizeof(bf16_t));   // bf16 path only (sized always)
+    P.ntq = (nkeys + 7) / 8 + 1;
+    P.qt = al256((size_t)P.ntq * ((lay.c_pad + 127) / 128) * 4096);   // bf16 path only (sized always)
     long long nt = 0;
     for (int l = 0; l < L; ++l) {
         P.tz0[l] = nt;
@@ -1382,17 +1388,16 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
         if (nblk == 0) continue;
         if constexpr (std::is_same<TT, bf16_t>::value) {
             // matrix-core path: sorted + transposed query rows, then 16-query MFMA batches
-            k_qt_sorted<<<dim3((unsigned)(P.nq_pad / 64), (unsigned)ngroups), 256, 0, s>>>(Q, kout, qt, A.Nq, nkeys,
-                                                                                       P.nq_pad, A.Cp, b);
-            if (!launched("qt_sorted")) return DVC_ERR_LAUNCH;
+            k_qt_tiles<<<dim3((unsigned)P.ntq, (unsigned)ngroups), 256, 0, s>>>(Q, kout, qt, A.Nq, nkeys, A.Cp, b);
+            if (!launched("qt_tiles")) return DVC_ERR_LAUNCH;
             for (int cg = 0; cg < ngroups; ++cg) {
                 BwdArgs Ag = A;
                 Ag.cbase = 128 * cg;
                 switch (std::min(128, A.Cp - Ag.cbase) / 32) {
-                case 1: k_grad_t_mfma<1><<<nblk, 256, 0, s>>>(qt, P.nq_pad, kout, starts, dt, dtp, Ag, b); break;
-                case 2: k_grad_t_mfma<2><<<nblk, 256, 0, s>>>(qt, P.nq_pad, kout, starts, dt, dtp, Ag, b); break;
-                case 3: k_grad_t_mfma<3><<<nblk, 256, 0, s>>>(qt, P.nq_pad, kout, starts, dt, dtp, Ag, b); break;
-                default: k_grad_t_mfma<4><<<nblk, 256, 0, s>>>(qt, P.nq_pad, kout, starts, dt, dtp, Ag, b); break;
+                case 1: k_grad_t_mfma<1><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b); break;
+                case 2: k_grad_t_mfma<2><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b); break;
+                case 3: k_grad_t_mfma<3><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b); break;
+                default: k_grad_t_mfma<4><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b); break;
                 }
             }
         } else {
