@@ -532,8 +532,11 @@ def main():
             else round(bd_bytes / (bd_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
 
     tail = flow_tail(args, coords_slab, S, B, dev, stream, _lib, dvccorr)
-    bwd = backward_timing(args, f1_slab, f2_slab, coords_slab, dims, dev, stream) \
-        if world == 1 and not shard_diag and args.convc1 is None else None
+    bwd = bwd_amp = None
+    if world == 1 and not shard_diag and args.convc1 is None:
+        bwd = backward_timing(args, f1_slab, f2_slab, coords_slab, dims, dev, stream)
+        # the reference Trainer's AMP backward (fp16 pyramid, trainer.py:249-257) on the same inputs
+        bwd_amp = backward_timing(args, f1_slab, f2_slab, coords_slab, dims, dev, stream, "fp16")
 
     detail = None
     if dist and strong and not args.no_extras:
@@ -572,6 +575,7 @@ def main():
             "lookup_avg_ms": round(lk_avg, 4),
             "flow_step": tail,
             "backward": bwd,
+            "backward_amp": bwd_amp,
             "cpu_baseline": cpu,
         }
         if detail is not None:
@@ -581,19 +585,21 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def backward_timing(args, f1, f2, coords, dims, dev, stream):
+def backward_timing(args, f1, f2, coords, dims, dev, stream, precision=None):
     """The training path's backward (dvc_corr_backward: d fmap1, d fmap2 of one lookup; autograd through
     corr.py:141-208), HIP-event timed outside the timed region on the bench's inputs and a random output
-    gradient.  Algorithmic bytes: read grad_out (fp32) + coords + the packed query/target rows, write
-    d fmap1 + d fmap2 (fp32); FLOPs: 2 x 2 C per window dot (d fmap1 and d fmap2), (2r+2)^3 window dots
-    per query and level."""
-    from dvccorr import ops
+    gradient, for the pyramid precision `precision` (default: the bench's; "fp16" = the reference Trainer's AMP
+    pyramid, trainer.py:249-257).  Algorithmic bytes: read grad_out (fp32) + coords + the packed query/target
+    rows, write d fmap1 + d fmap2 (fp32); FLOPs: 2 x 2 C per window dot (d fmap1 and d fmap2), (2r+2)^3 window
+    dots per query and level."""
+    from dvccorr import ops, _lib
+    precision = precision or args.precision
     with torch.no_grad():
         B, C = f1.shape[:2]
         S = args.size
         L, R = args.levels, args.radius
         Nq = f1[0, 0].numel()
-        dt = ops.dtype_code(args.precision)
+        dt = ops.dtype_code(precision)
         q = ops.pack_queries(f1.reshape(B, C, -1), dt)
         t = ops.pack_targets(f2, L, dt)
         g = torch.Generator(device=dev).manual_seed(99)
@@ -609,15 +615,20 @@ def backward_timing(args, f1, f2, coords, dims, dev, stream):
         b.record(stream)
         torch.cuda.synchronize()
         ms = a.elapsed_time(b) / n
-    esz = 2 if args.precision == "bf16" else 4
+    esz = 4 if precision == "fp32" else 2
     nbytes = gout.numel() * 4 + cf.numel() * 4 + (q.numel() + t.numel()) * esz + 2 * B * C * Nq * 4
     flops = 2.0 * 2 * C * (2 * R + 2) ** 3 * L * B * Nq
-    peak = BF16_PEAK_TFS if args.precision == "bf16" else F32_PEAK_TFS
-    return {"kernels": "k_win_grad + k_grad_q_mfma + radix sort + k_grad_t_mfma + k_unpack_sum (dvc_corr_backward, bf16 path)",
+    mfma = bool(_lib.lib().dvc_corr_backward_mfma(B, Nq, C, S, S, S, L, R, 0, dt))
+    kern = (f"k_win_grad + k_grad_q_mfma + radix sort + k_grad_t_mfma + k_unpack_sum (dvc_corr_backward, {precision} "
+            f"operands on v_mfma_f32_32x32x16_{'f16' if precision == 'fp16' else 'bf16'})" if mfma else
+            f"k_win_grad + k_grad_q + radix sort + k_grad_t + k_unpack_sum (dvc_corr_backward, {precision} operands, "
+            f"fp32 VALU)")
+    peak = F32_PEAK_TFS if precision == "fp32" else BF16_PEAK_TFS
+    return {"precision": precision, "kernels": kern,
             "avg_ms": round(ms, 4), "algorithmic_bytes": nbytes, "GB/s": round(nbytes / (ms * 1e-3) / 1e9, 1),
             "hbm_frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "flops": flops,
             "TFLOP/s": round(flops / (ms * 1e-3) / 1e12, 2),
-            "mfma_frac": round(flops / (ms * 1e-3) / 1e12 / peak, 4)}
+            ("mfma_frac" if mfma else "valu_frac"): round(flops / (ms * 1e-3) / 1e12 / peak, 4)}
 
 
 def flow_tail(args, coords_slab, S, B, dev, stream, _lib, dvccorr):

@@ -35,7 +35,8 @@
  *   fmap           (B, C, H, W, D) float32, channels-first, contiguous   (reference layout)
  *   coords         (B, 3, Nq) float32, channel order (h, w, d)           (corr.py:169-173)
  *   lookup out     (B, L*(2r+1)^3, Nq) float32; channel l*n^3+a*n^2+b*n+e (corr.py:188-208)
- *   packed queries [B][Nq][c_pad]         dtype (f32 or bf16), zero channel padding
+ *   packed queries [B][Nq][c_pad]         dtype (f32, bf16 or f16), zero channel padding; c_pad = 32, 64
+ *                                         or 128 for C up to 128, else C rounded up to a multiple of 128
  *   packed targets [B][row_stride][c_pad] dtype; rows = level-concatenated target voxels
  *   corr pyramid   [B][Nq][row_stride]    store dtype; row q holds every level of query q:
  *                  level l voxel (y,x,z) at offset[l] + (y*W_l + x)*Dp_l + z, Dp_l = ceil8(D_l),
@@ -56,7 +57,9 @@ extern "C" {
 #endif
 
 #define DVC_MAX_LEVELS 8
-#define DVC_ABI_VERSION 1
+/* 2 (round 4): c_pad rounds to 32 / 64 / 128 then multiples of 128 (was ceil32), DVC_F16, and
+ * dvc_corr_backward_mfma */
+#define DVC_ABI_VERSION 2
 /* The corr pyramid buffer must be allocated with DVC_CORR_GUARD_BYTES of extra
  * space before its first row and after its last row.  dvc_corr_build zeroes
  * them; dvc_corr_lookup's walk kernels load each window run from a clamped
@@ -172,6 +175,13 @@ size_t dvc_corr_backward_workspace_bytes(int B, int64_t Nq, int C, int H, int W,
 int dvc_corr_backward(const void *packed_q, const void *packed_t, const float *coords, const float *grad_out,
                       float *grad_fmap1, float *grad_fmap2, void *workspace, int B, int64_t Nq, int C, int H, int W,
                       int D, int num_levels, int radius, int convention, int dtype, void *stream);
+/* Pure host function: 1 when dvc_corr_backward runs this shape's gradient sums on the matrix cores
+ * (bf16 operands on v_mfma_f32_32x32x16_bf16, fp16 on _f16, the window gradients entering as hi/lo
+ * pairs), 0 when it takes the VALU kernels (fp32 operands, or a volume whose MFMA-kernel buffer
+ * offsets would exceed 31 bits: level-0 fmaps of about 154^3 and up).  Same results either way within
+ * the dtype's tolerance. */
+int dvc_corr_backward_mfma(int B, int64_t Nq, int C, int H, int W, int D, int num_levels, int radius, int convention,
+                           int dtype);
 
 /* Lookup with the motion encoder's convc1 (1x1x1 Conv3d L*(2r+1)^3 -> 96, + ReLU,
  * update.py:222, 246) fused into its epilogue: the L*(2r+1)^3-channel lookup output

@@ -41,13 +41,6 @@
 
 namespace dvc {
 
-// waves per SIMD the MFMA gradient kernels (k_grad_q_mfma, k_grad_t_mfma) are compiled for: at 1 their 256
-// VGPRs + 128 accumulators leave one wave per SIMD and every gather's latency exposed; at 2 they spill a few
-// dwords and run 13-18 % faster (round 3, tools/ab_bwd.py).  k_win_grad stays at one wave (2: 250 -> 368 us).
-#ifndef DVC_BWD_OCC
-#define DVC_BWD_OCC 2
-#endif
-
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -156,8 +149,6 @@ template <> __device__ __forceinline__ f32x2 load2<bf16_t>(const bf16_t *p) {
     const unsigned u = *reinterpret_cast<const unsigned *>(p);
     return f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
 }
-// fp16 operands (the AMP pyramid's packed rows) take the fp32 VALU gradient kernels: splitting the fp32
-// window gradients into fp16 hi + lo for the matrix cores would lose the small gradients to fp16's range
 template <> __device__ __forceinline__ f32x2 load2<f16_t>(const f16_t *p) {
     typedef _Float16 h2 __attribute__((ext_vector_type(2)));
     return __builtin_convertvector(*reinterpret_cast<const h2 *>(p), f32x2);
@@ -178,10 +169,31 @@ __device__ __forceinline__ unsigned bf16_hilo(float g) {
            ((unsigned)__builtin_bit_cast(unsigned short, (__bf16)(g - (float)hb)) << 16);
 }
 
-// HILO: the window gradients leave as bf16_hilo pairs (the bf16 path's MFMA kernels read them as operands
-// directly), else as fp32
-template <int R, bool HILO>
-__global__ __launch_bounds__(256) void k_win_grad(BwdArgs A) {
+// The fp16 (AMP) path's pair: f16(g) and f16(g - f16(g)), ~22 mantissa bits of g in fp16's range.  The reference's
+// own AMP backward rounds d(corr) to fp16 once (its matmul / avg_pool3d backward run in fp16 under the Trainer's
+// autocast, trainer.py:249-257, with GradScaler keeping the gradients in range), so the pair is at least as exact
+// as the reference everywhere and twice as precise wherever fp16 is normal.
+__device__ __forceinline__ unsigned f16_hilo(float g) {
+    const _Float16 hh = (_Float16)g;
+    return (unsigned)__builtin_bit_cast(unsigned short, hh) |
+           ((unsigned)__builtin_bit_cast(unsigned short, (_Float16)(g - (float)hh)) << 16);
+}
+
+// Window-gradient formats: fp32 (the VALU gradient kernels), or hi/lo pairs that ARE the MFMA kernels' A operand
+enum GwinFmt { kGwF32 = 0, kGwBf16 = 1, kGwF16 = 2 };
+template <int FMT> __device__ __forceinline__ unsigned gw_pair(float g) {
+    if constexpr (FMT == kGwF16) return f16_hilo(g);
+    else return bf16_hilo(g);
+}
+
+// Round 4 (the round-3 column-split patch): the output gradients arrive through buffer loads (the (b, l) block's
+// plane as a descriptor, the lane's query as the vector offset, the channel as a scalar one; per-lane 64-bit
+// addresses for the channels took the kernel's registers), and the window is produced in two passes over its
+// column halves [J0, J1), each holding only output columns [U0, U1] of the two rows in flight (2 x 5 x n floats at
+// r = 4, was 2 x n x n): two waves per SIMD instead of one.  The column shared by the halves is loaded twice.
+// (r = 6 keeps one wave per SIMD: its two rows of 2 x 7 x 13 floats would spill at 256 VGPRs)
+template <int R, int FMT>
+__global__ __launch_bounds__(256, R <= 5 ? 2 : 1) void k_win_grad(BwdArgs A) {
     constexpr int n = 2 * R + 1, NW = 2 * R + 2, NW3 = NW * NW * NW;
     const int lane = threadIdx.x & 63;
     const long long nqb = (A.Nq + 63) / 64;
@@ -213,81 +225,96 @@ __global__ __launch_bounds__(256) void k_win_grad(BwdArgs A) {
         wz1[t] = (unsigned)(iv + t + 1) < (unsigned)Dl ? wz1[t] : 0.0f;
     }
     const long long chu = A.legacy ? 1 : n, chv = A.legacy ? n : 1;
-    const float *g = A.gout + (long long)bl * n * n * n * A.Nq + q;
-    // Window plane i collects output row a = i (corner 0) and a = i - 1 (corner 1).  Each output row
-    // is loaded once: row i - 1 stays in registers from the previous plane (ping-pong buffers).
-    float rowA[n][n], rowB[n][n];
+    const float *gbl = A.gout + (long long)bl * n * n * n * A.Nq;
+    const int q4 = (int)(q * 4), nq4 = (int)(A.Nq * 4);
+    // Window plane i collects output row a = i (corner 0) and a = i - 1 (corner 1); row i - 1 stays in registers
+    // from the previous plane (ping-pong buffers)
+    auto pass = [&](auto j0c, auto j1c) {
+        constexpr int J0 = decltype(j0c)::value, J1 = decltype(j1c)::value;
+        constexpr int U0 = J0 > 0 ? J0 - 1 : 0, U1 = J1 - 1 < n - 1 ? J1 - 1 : n - 1, NU = U1 - U0 + 1;
+        float rowA[NU][n], rowB[NU][n];
 #pragma unroll
-    for (int j = 0; j < n; ++j)
+        for (int uu = 0; uu < NU; ++uu)
 #pragma unroll
-        for (int v = 0; v < n; ++v) rowB[j][v] = 0.0f;
-    auto plane = [&](int i, float (&cur)[n][n], const float (&prev)[n][n]) {
-        float wa0 = 0.0f, wa1 = 0.0f, t0, t1;
-        if (i < n) {
-            axis_weights(ax.ph, ax.kh, i - R, ax.hs, ax.hs, t0, t1);
-            wa0 = (unsigned)(ih + i) < (unsigned)Hl ? t0 : 0.0f;
-            const float *g0 = g + (long long)i * n * n * A.Nq;   // output row a = i
+            for (int v = 0; v < n; ++v) rowB[uu][v] = 0.0f;
+        auto plane = [&](int i, float (&cur)[NU][n], const float (&prev)[NU][n]) {
+            float wa0 = 0.0f, wa1 = 0.0f, t0, t1;
+            if (i < n) {
+                axis_weights(ax.ph, ax.kh, i - R, ax.hs, ax.hs, t0, t1);
+                wa0 = (unsigned)(ih + i) < (unsigned)Hl ? t0 : 0.0f;
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(   // output row a = i
+                    (void *)(gbl + (long long)i * n * n * A.Nq), (short)0,
+                    (int)min((long long)n * n * nq4, 0x7fffffffLL), 0x00020000);
 #pragma unroll
-            for (int j = 0; j < n; ++j)
+                for (int uu = 0; uu < NU; ++uu)
 #pragma unroll
-                for (int v = 0; v < n; ++v) cur[j][v] = g0[(j * chu + v * chv) * A.Nq];
-        }
-        if (i >= 1) {
-            axis_weights(ax.ph, ax.kh, i - 1 - R, ax.hs, ax.hs, t0, t1);
-            wa1 = (unsigned)(ih + i) < (unsigned)Hl ? t1 : 0.0f;
-        }
-        float Pp[n];
+                    for (int v = 0; v < n; ++v)
+                        cur[uu][v] = __builtin_bit_cast(
+                            float, __builtin_amdgcn_raw_buffer_load_b32(rs, q4, (int)(((U0 + uu) * chu + v * chv) * nq4), 0));
+            }
+            if (i >= 1) {
+                axis_weights(ax.ph, ax.kh, i - 1 - R, ax.hs, ax.hs, t0, t1);
+                wa1 = (unsigned)(ih + i) < (unsigned)Hl ? t1 : 0.0f;
+            }
+            float Pp[n];
 #pragma unroll
-        for (int v = 0; v < n; ++v) Pp[v] = 0.0f;
+            for (int v = 0; v < n; ++v) Pp[v] = 0.0f;
 #pragma unroll
-        for (int j = 0; j < NW; ++j) {
-            float Pc[n];
+            for (int j = U0; j < J1; ++j) {   // (j = J0 - 1 only primes Pp)
+                float Pc[n];
 #pragma unroll
-            for (int v = 0; v < n; ++v) Pc[v] = 0.0f;
-            if (j < n) {
-                if (i < n) {
+                for (int v = 0; v < n; ++v) Pc[v] = 0.0f;
+                if (j < n) {
+                    const int uu = j < n ? j - U0 : 0;
+                    if (i < n) {
 #pragma unroll
-                    for (int v = 0; v < n; ++v) Pc[v] = wa0 * cur[j < n ? j : 0][v];
+                        for (int v = 0; v < n; ++v) Pc[v] = wa0 * cur[uu][v];
+                    }
+                    if (i >= 1) {
+#pragma unroll
+                        for (int v = 0; v < n; ++v) Pc[v] = __builtin_fmaf(wa1, prev[uu][v], Pc[v]);
+                    }
                 }
-                if (i >= 1) {
+                if (j >= J0) {
+                    const float wj0 = j < n ? wx0[j < n ? j : 0] : 0.0f;
+                    const float wj1 = j >= 1 ? wx1[j >= 1 ? j - 1 : 0] : 0.0f;
+                    float o[NW];
 #pragma unroll
-                    for (int v = 0; v < n; ++v) Pc[v] = __builtin_fmaf(wa1, prev[j < n ? j : 0][v], Pc[v]);
+                    for (int k = 0; k < NW; ++k) o[k] = 0.0f;
+#pragma unroll
+                    for (int v = 0; v < n; ++v) {
+                        const float gz = __builtin_fmaf(wj0, Pc[v], wj1 * Pp[v]);
+                        o[v] = __builtin_fmaf(wz0[v], gz, o[v]);
+                        o[v + 1] = __builtin_fmaf(wz1[v], gz, o[v + 1]);
+                    }
+                    if constexpr (FMT != kGwF32) {
+                        u32x2 *dst = reinterpret_cast<u32x2 *>(gw + (i * NW + j) * NW);
+#pragma unroll
+                        for (int k = 0; k < NW / 2; ++k) dst[k] = u32x2{gw_pair<FMT>(o[2 * k]), gw_pair<FMT>(o[2 * k + 1])};
+                    } else {
+                        f32x2 *dst = reinterpret_cast<f32x2 *>(gw + (i * NW + j) * NW);
+#pragma unroll
+                        for (int k = 0; k < NW / 2; ++k) dst[k] = f32x2{o[2 * k], o[2 * k + 1]};
+                    }
                 }
+#pragma unroll
+                for (int v = 0; v < n; ++v) Pp[v] = Pc[v];
             }
-            const float wj0 = j < n ? wx0[j < n ? j : 0] : 0.0f;
-            const float wj1 = j >= 1 ? wx1[j >= 1 ? j - 1 : 0] : 0.0f;
-            float o[NW];
-#pragma unroll
-            for (int k = 0; k < NW; ++k) o[k] = 0.0f;
-#pragma unroll
-            for (int v = 0; v < n; ++v) {
-                const float gz = __builtin_fmaf(wj0, Pc[v], wj1 * Pp[v]);
-                o[v] = __builtin_fmaf(wz0[v], gz, o[v]);
-                o[v + 1] = __builtin_fmaf(wz1[v], gz, o[v + 1]);
-            }
-            if constexpr (HILO) {
-                u32x2 *dst = reinterpret_cast<u32x2 *>(gw + (i * NW + j) * NW);
-#pragma unroll
-                for (int k = 0; k < NW / 2; ++k) dst[k] = u32x2{bf16_hilo(o[2 * k]), bf16_hilo(o[2 * k + 1])};
-            } else {
-                f32x2 *dst = reinterpret_cast<f32x2 *>(gw + (i * NW + j) * NW);
-#pragma unroll
-                for (int k = 0; k < NW / 2; ++k) dst[k] = f32x2{o[2 * k], o[2 * k + 1]};
-            }
-#pragma unroll
-            for (int v = 0; v < n; ++v) Pp[v] = Pc[v];
+        };
+#pragma unroll 1
+        for (int i = 0; i < NW; i += 2) {   // NW is even
+            plane(i, rowA, rowB);
+            plane(i + 1, rowB, rowA);
         }
     };
-    for (int i = 0; i < NW; i += 2) {   // NW is even
-        plane(i, rowA, rowB);
-        plane(i + 1, rowB, rowA);
-    }
+    pass(std::integral_constant<int, 0>{}, std::integral_constant<int, NW / 2>{});
+    pass(std::integral_constant<int, NW / 2>{}, std::integral_constant<int, NW>{});
 }
 
 // Generic (legacy W != D) levels: lane = query; the window box is zeroed, then every output's
 // (up to) 8 in-range corners are added in output order with grid_sample's weights
 // (tri_sample in common.h).  The box is private to the lane: no atomics, fixed order.
-template <int R, bool HILO>
+template <int R, int FMT>
 __global__ __launch_bounds__(256) void k_win_grad_generic(BwdArgs A) {
     constexpr int n = 2 * R + 1;
     const int lane = threadIdx.x & 63;
@@ -357,8 +384,8 @@ __global__ __launch_bounds__(256) void k_win_grad_generic(BwdArgs A) {
             }
         }
     }
-    if constexpr (HILO) {   // the lane's finished box into bf16_hilo pairs, in place
-        for (long long i = 0; i < nw3; ++i) reinterpret_cast<unsigned *>(gw)[i] = bf16_hilo(gw[i]);
+    if constexpr (FMT != kGwF32) {   // the lane's finished box into hi/lo pairs, in place
+        for (long long i = 0; i < nw3; ++i) reinterpret_cast<unsigned *>(gw)[i] = gw_pair<FMT>(gw[i]);
     }
 }
 
@@ -568,6 +595,18 @@ __device__ __forceinline__ void blds(u32x4 rs, unsigned voff, unsigned soff, uns
 using W16 = std::integral_constant<int, 16>;
 using W4 = std::integral_constant<int, 4>;
 
+// D += A x B on the 32x32x16 matrix cores, bf16 or (the fp16 / AMP path) fp16 operands: the operand images and
+// the hi/lo pairing are the same 16-bit layouts for both
+template <bool F16>
+__device__ __forceinline__ f32x16 mma32(bf16x8 a, bf16x8 b, f32x16 c) {
+    if constexpr (F16) {
+        typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b), c, 0, 0, 0);
+    } else {
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+    }
+}
+
 // {a.lo, a.lo, a.hi, a.hi, b.lo, ...}: four bf16 each repeated (the B operand over K = (z, hi/lo))
 __device__ __forceinline__ bf16x8 dup_bf16x4(u32x2 v) {
     u32x4 r;
@@ -578,7 +617,7 @@ __device__ __forceinline__ bf16x8 dup_bf16x4(u32x2 v) {
     return __builtin_bit_cast(bf16x8, r);
 }
 
-template <int NCT>   // channel tiles of 32 (C_pad / 32, <= 4 per launch)
+template <int NCT, bool F16>   // channel tiles of 32 (C_pad / 32, <= 4 per launch); fp16 operands
 __global__ __launch_bounds__(256, 4) void k_grad_q_mfma(const bf16_t *__restrict__ Tz, float *__restrict__ dQp,
                                                         long long part_stride, BwdArgs A) {
     constexpr int STAGE = 8192;                      // bytes: T tile (4 KB, bf16) + G tile (4 KB, hi/lo pairs)
@@ -720,7 +759,7 @@ __global__ __launch_bounds__(256, 4) void k_grad_q_mfma(const bf16_t *__restrict
                             const int gq = 32 * T + m, sw = (gq >> 2) & 3;
                             const bf16x8 ag =
                                 *reinterpret_cast<const bf16x8 *>(sb + 4096 + gq * 64 + 16 * ((2 * j + h) ^ sw));
-                            acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ag, bt, acc[T], 0, 0, 0);
+                            acc[T] = mma32<F16>(ag, bt, acc[T]);
                         }
                     }
                 }
@@ -970,7 +1009,7 @@ __global__ __launch_bounds__(256) void k_qt_tiles(const bf16_t *__restrict__ Q, 
 // 16-byte load (the round-2 layout of this loop gathered 4-byte values from 64 windows per instruction and
 // was bound by that L2 traffic).  The 64-query chunks of the brick's origin rows are dealt to the workgroups of
 // the brick (splits).
-template <int NCT>   // channel tiles of 32 (C_pad / 32, <= 4 per launch)
+template <int NCT, bool F16>   // channel tiles of 32 (C_pad / 32, <= 4 per launch); fp16 operands
 __global__ __launch_bounds__(256, 4) void k_grad_t_mfma(const bf16_t *__restrict__ Qz, long long ntq,
                                                         const unsigned long long *__restrict__ keys,
                                                         const int *__restrict__ starts, float *__restrict__ dT,
@@ -1071,7 +1110,7 @@ __global__ __launch_bounds__(256, 4) void k_grad_t_mfma(const bf16_t *__restrict
                         for (int T = 0; T < 2; ++T) {
                             const int tr = 32 * T + m;
                             const bf16x8 ag = *reinterpret_cast<const bf16x8 *>(&Gq[buf][tr][4 * ((2 * j + h) ^ ((tr >> 2) & 3))]);
-                            acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ag, bq, acc[T], 0, 0, 0);
+                            acc[T] = mma32<F16>(ag, bq, acc[T]);
                         }
                     }
                 }
@@ -1261,6 +1300,8 @@ static void bwd_plan(int B, long long Nq, const dvc_layout &lay, int radius, boo
     // the target-gradient pass sorts the keys of all L levels of one batch element at once
     const long long nkeys = (long long)L * Nq;
     P.gwin = al256(gw) + 512;   // + 256-byte guards before and after (k_grad_q_mfma's 8-float loads)
+    // partial dQ per k_grad_q_mfma level group; the workspace query has no dtype, so this covers the MFMA path
+    // (the VALU kernels of fp32 blocks use the first part only)
     P.dq = al256((size_t)grad_q_parts(L) * B * Nq * lay.c_pad * sizeof(float));
     P.dt = al256((size_t)B * lay.row_stride * lay.c_pad * sizeof(float));
     P.keys = al256((size_t)nkeys * sizeof(unsigned long long));
@@ -1288,6 +1329,31 @@ size_t backward_workspace_bytes(int B, long long Nq, const dvc_layout &lay, int 
     bwd_plan(B, Nq, lay, radius, false, P);
     bwd_plan(B, Nq, lay, radius, true, Q);
     return std::max(P.total, Q.total);
+}
+
+// k_grad_q_mfma addresses its target tiles and the window gradients of a query box through buffer descriptors
+// with 32-bit byte offsets (num_records <= 2^31 - 1): the tiles of one (batch element, 128-channel group) -- every
+// level's (row, 8-aligned z start) tile, 4 KB each -- and, per level, the window gradients from the box's first
+// query to the last of the < 4 (W, D) planes it spans.  Larger volumes (level-0 fmaps of ~154^3 and up) take the
+// VALU gradient kernels, which address with 64 bits, instead of reading zeros past the descriptor's range.
+static bool mfma_offsets_fit(const BwdArgs &A, const BwdPlan &P) {
+    const long long lim = 0x7fffffffLL;
+    if (P.tz0[A.L] * 4096 > lim) return false;
+    const long long span = 3LL * A.Wq * A.Dq + 3LL * A.Dq + 4;
+    for (int l = 0; l < A.L; ++l)
+        if (span * ((long long)A.nwh[l] * A.nwu[l] * A.nwv[l]) * 4 > lim) return false;
+    return true;
+}
+
+// dtype codes of the packed operands whose gradient sums can run on the matrix cores (the rest: VALU)
+int backward_uses_mfma(int B, long long Nq, const dvc_layout &lay, int radius, int convention, int dtype) {
+    if (dtype != DVC_BF16 && dtype != DVC_F16) return 0;
+    BwdPlan P;
+    bwd_plan(B, Nq, lay, radius, convention == DVC_LEGACY, P);
+    BwdArgs A{};
+    A.L = lay.num_levels; A.Wq = lay.W[0]; A.Dq = lay.D[0];
+    for (int l = 0; l < lay.num_levels; ++l) { A.nwh[l] = P.nw[l][0]; A.nwu[l] = P.nw[l][1]; A.nwv[l] = P.nw[l][2]; }
+    return mfma_offsets_fit(A, P) ? 1 : 0;
 }
 
 template <typename TT, int R>
@@ -1318,34 +1384,55 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     };
     const long long nqb = (A.Nq + 63) / 64;
     const int ngroups = (A.Cp + 127) / 128;   // 128-channel groups: one launch of each gradient kernel per group
-    k_win_grad<R, std::is_same<TT, bf16_t>::value><<<(unsigned)((A.B * A.L * nqb + 3) / 4), 256, 0, s>>>(A);
+    // Matrix-core path for 16-bit operands (bf16; fp16 = the AMP pyramid) whenever its LDS-DMA buffer offsets fit
+    // 32 bits (mfma_offsets_fit); otherwise, and for fp32 blocks, the VALU gradient kernels (64-bit addressing)
+    constexpr bool k16 = !std::is_same<TT, float>::value;
+    constexpr bool F16 = std::is_same<TT, f16_t>::value;
+    const bool mfma = k16 && mfma_offsets_fit(A, P);
+    const int fmt = mfma ? (F16 ? kGwF16 : kGwBf16) : kGwF32;
+    const unsigned wgrid = (unsigned)((A.B * A.L * nqb + 3) / 4);
+    switch (fmt) {
+    case kGwF16: k_win_grad<R, kGwF16><<<wgrid, 256, 0, s>>>(A); break;
+    case kGwBf16: k_win_grad<R, kGwBf16><<<wgrid, 256, 0, s>>>(A); break;
+    default: k_win_grad<R, kGwF32><<<wgrid, 256, 0, s>>>(A); break;
+    }
     if (!launched("win_grad")) return DVC_ERR_LAUNCH;
     bool any_generic = false;
     for (int l = 0; l < A.L; ++l) any_generic |= A.generic[l] != 0;
     if (any_generic) {
-        k_win_grad_generic<R, std::is_same<TT, bf16_t>::value><<<(unsigned)((A.B * A.L * nqb + 3) / 4), 256, 0, s>>>(A);
+        switch (fmt) {
+        case kGwF16: k_win_grad_generic<R, kGwF16><<<wgrid, 256, 0, s>>>(A); break;
+        case kGwBf16: k_win_grad_generic<R, kGwBf16><<<wgrid, 256, 0, s>>>(A); break;
+        default: k_win_grad_generic<R, kGwF32><<<wgrid, 256, 0, s>>>(A); break;
+        }
         if (!launched("win_grad_generic")) return DVC_ERR_LAUNCH;
     }
     const long long boxes = (long long)A.B * ((A.Hq + 3) / 4) * ((A.Wq + 3) / 4) * ((A.Dq + 3) / 4);
     // partial dQ per level group of the MFMA path (qparts of them, qstride floats apart)
-    const int qparts = std::is_same<TT, bf16_t>::value ? grad_q_parts(A.L) : 1;
+    const int qparts = mfma ? grad_q_parts(A.L) : 1;
     const long long qstride = (long long)A.B * A.Nq * A.Cp;
-    if constexpr (std::is_same<TT, bf16_t>::value) {
-        for (int l = 0; l <= A.L; ++l) A.tz0[l] = P.tz0[l];
-        k_tile_targets<<<dim3((unsigned)P.tz0[A.L], (unsigned)ngroups, (unsigned)A.B), 256, 0, s>>>(Tt, ttr, A);
-        if (!launched("tile_targets")) return DVC_ERR_LAUNCH;
-        const dim3 qg((unsigned)boxes, (unsigned)qparts);   // level groups: {0}, {1 .. L-1}
-        for (int g = 0; g < ngroups; ++g) {
-            BwdArgs Ag = A;
-            Ag.cbase = 128 * g;
-            switch (std::min(128, A.Cp - Ag.cbase) / 32) {
-            case 1: k_grad_q_mfma<1><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag); break;
-            case 2: k_grad_q_mfma<2><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag); break;
-            case 3: k_grad_q_mfma<3><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag); break;
-            default: k_grad_q_mfma<4><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag); break;
+    bool done_q = false;
+    if constexpr (k16) {
+        if (mfma) {
+            for (int l = 0; l <= A.L; ++l) A.tz0[l] = P.tz0[l];
+            k_tile_targets<<<dim3((unsigned)P.tz0[A.L], (unsigned)ngroups, (unsigned)A.B), 256, 0, s>>>(
+                reinterpret_cast<const bf16_t *>(Tt), ttr, A);
+            if (!launched("tile_targets")) return DVC_ERR_LAUNCH;
+            const dim3 qg((unsigned)boxes, (unsigned)qparts);   // level groups: {0}, {1 .. L-1}
+            for (int g = 0; g < ngroups; ++g) {
+                BwdArgs Ag = A;
+                Ag.cbase = 128 * g;
+                switch (std::min(128, A.Cp - Ag.cbase) / 32) {
+                case 1: k_grad_q_mfma<1, F16><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag); break;
+                case 2: k_grad_q_mfma<2, F16><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag); break;
+                case 3: k_grad_q_mfma<3, F16><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag); break;
+                default: k_grad_q_mfma<4, F16><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag); break;
+                }
             }
+            done_q = true;
         }
-    } else {
+    }
+    if (!done_q) {
         for (int g = 0; g < ngroups; ++g) {
             BwdArgs Ag = A;
             Ag.cbase = 128 * g;
@@ -1386,21 +1473,27 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
         k_cell_starts<<<(unsigned)((ncell + 1 + 255) / 256), 256, 0, s>>>(kout, nkeys, ncell, starts);
         if (!launched("cell_starts")) return DVC_ERR_LAUNCH;
         if (nblk == 0) continue;
-        if constexpr (std::is_same<TT, bf16_t>::value) {
-            // matrix-core path: sorted + transposed query rows, then 16-query MFMA batches
-            k_qt_tiles<<<dim3((unsigned)P.ntq, (unsigned)ngroups), 256, 0, s>>>(Q, kout, qt, A.Nq, nkeys, A.Cp, b);
-            if (!launched("qt_tiles")) return DVC_ERR_LAUNCH;
-            for (int cg = 0; cg < ngroups; ++cg) {
-                BwdArgs Ag = A;
-                Ag.cbase = 128 * cg;
-                switch (std::min(128, A.Cp - Ag.cbase) / 32) {
-                case 1: k_grad_t_mfma<1><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b); break;
-                case 2: k_grad_t_mfma<2><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b); break;
-                case 3: k_grad_t_mfma<3><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b); break;
-                default: k_grad_t_mfma<4><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b); break;
+        bool done_t = false;
+        if constexpr (k16) {
+            if (mfma) {
+                // matrix-core path: sorted + transposed query rows, then 16-query MFMA batches
+                k_qt_tiles<<<dim3((unsigned)P.ntq, (unsigned)ngroups), 256, 0, s>>>(
+                    reinterpret_cast<const bf16_t *>(Q), kout, qt, A.Nq, nkeys, A.Cp, b);
+                if (!launched("qt_tiles")) return DVC_ERR_LAUNCH;
+                for (int cg = 0; cg < ngroups; ++cg) {
+                    BwdArgs Ag = A;
+                    Ag.cbase = 128 * cg;
+                    switch (std::min(128, A.Cp - Ag.cbase) / 32) {
+                    case 1: k_grad_t_mfma<1, F16><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b); break;
+                    case 2: k_grad_t_mfma<2, F16><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b); break;
+                    case 3: k_grad_t_mfma<3, F16><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b); break;
+                    default: k_grad_t_mfma<4, F16><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b); break;
+                    }
                 }
+                done_t = true;
             }
-        } else {
+        }
+        if (!done_t) {
             for (int cg = 0; cg < ngroups; ++cg) {
                 BwdArgs Ag = A;
                 Ag.cbase = 128 * cg;

@@ -837,9 +837,11 @@ template __global__ void k_build_bf16_2b<32, f16_t>(const f16_t *, const f16_t *
                                             long long, long long, long long, int, float, int);
 template __global__ void k_build_bf16_2b<32, bf16_t>(const bf16_t *, const bf16_t *, bf16_t *, long long, int, long long,
                                              long long, long long, long long, int, float, int);
+#if DVC_DIAG   // diagnostics (build_ablate): 1 no global stores, 2 no MFMAs
 template __global__ void k_build_bf16<16, false, 1>(const bf16_t *, const bf16_t *, bf16_t *, long long, int,
                                                     long long, long long, long long, long long, int, float);
 template __global__ void k_build_bf16<16, false, 2>(const bf16_t *, const bf16_t *, bf16_t *, long long, int,
                                                     long long, long long, long long, long long, int, float);
+#endif
 
 }  // namespace dvc

@@ -60,6 +60,7 @@ int corr_backward(const void *packed_q, const void *packed_t, const float *coord
                   const dvc_layout &lay, int radius, int convention, int dtype, hipStream_t s, char *err,
                   size_t errlen);
 size_t backward_workspace_bytes(int B, long long Nq, const dvc_layout &lay, int radius);
+int backward_uses_mfma(int B, long long Nq, const dvc_layout &lay, int radius, int convention, int dtype);
 __global__ void k_coords_grid(float *, long long, int, int, int);
 template <bool DELTA, bool SUBGRID, int VEC, bool STAGED>
 __global__ void k_upflow(const float *, const float *, float *, float *, long long, int, int, int, int, int, int, int,
@@ -166,9 +167,10 @@ static bool tile_ok(const LookupArgs &A, size_t esz) {
 // four rounds, so the hardware dispatcher rebalances the uneven workgroup times (88-136 us with one
 // workgroup per slot, tools/trace_lookup.py); tools/ab_lookup.py, bitwise equal, 149.2 -> 145.2 us median.
 static constexpr long long kSplitTiles = 1024, kSplitRows = 512;
+// rows per chunk of the row split (0 = no row split; 2, 3, 5; tuning "split_ach")
 static thread_local int g_split_ach = 5;
 // launches with fewer query tiles than this take one (tile, level) pair per workgroup (tuning "split_tiles")
-static thread_local long long g_split_tiles = kSplitTiles;          // rows per chunk of the row split (0 = no row split; 2, 3, 5)
+static thread_local long long g_split_tiles = kSplitTiles;
 // r = 4 tile kernel: 4 = four waves of 3 + 2 + 2 + 2 output columns (default: two workgroups put two waves
 // on every SIMD), 0 = three 3-column waves.  Round 2 A/B (tools/ab_waves.py, bitwise-equal outputs, median
 // of 40 calls): config #3 bf16 151.8 -> 150.0 us, fp32 220.7 -> 213.9; one rank's slab of an 8 / 4 / 2-way
@@ -203,6 +205,7 @@ static void launch_tile_nt(const LookupArgs &A0, hipStream_t s) {
                       split_rows ? (unsigned)((n + ach - 1) / ach) : 1u);
     const bool bal = NT && A.r == 4 && g_lookup_waves == 4 && (ach == 5 || !split_rows);
     const unsigned threads = 64u * (bal ? 4u : (unsigned)((2 * A.r + 3) / 3));
+#if DVC_DIAG
     if constexpr (std::is_same<T, bf16_t>::value && NT) {
         if (A.r == 4 && A.ablate >= 1 && A.ablate <= 4) {   // diagnostics only
             const dim3 b1((unsigned)tiles, blocks.y);
@@ -213,8 +216,10 @@ static void launch_tile_nt(const LookupArgs &A0, hipStream_t s) {
             return;
         }
     }
+#endif
     if constexpr (NT) {
         if (bal) {
+#if DVC_DIAG
             if constexpr (std::is_same<T, bf16_t>::value) {
                 if (A.trace) {   // diagnostics only: timeline stamps
                     if (split_rows) k_lookup_tile<T, 4, true, 8, false, 5, 4><<<blocks, threads, 0, s>>>(A);
@@ -222,10 +227,12 @@ static void launch_tile_nt(const LookupArgs &A0, hipStream_t s) {
                     return;
                 }
             }
+#endif
             if (split_rows) {
                 k_lookup_tile<T, 4, true, 0, false, 5, 4><<<blocks, threads, 0, s>>>(A);
                 return;
             }
+#if DVC_DIAG
             if constexpr (std::is_same<T, bf16_t>::value) {
                 switch (g_lookup_stpol) {   // diagnostics only
                 case 0: k_lookup_tile<T, 4, true, 0, false, 0, 4, 0><<<blocks, threads, 0, s>>>(A); return;
@@ -235,6 +242,7 @@ static void launch_tile_nt(const LookupArgs &A0, hipStream_t s) {
                 default: break;
                 }
             }
+#endif
             k_lookup_tile<T, 4, true, 0, false, 0, 4><<<blocks, threads, 0, s>>>(A);
             return;
         }
@@ -280,6 +288,14 @@ const char *dvc_last_error(void) { return g_err; }
 
 int dvc_set_tuning(const char *key, int value) {
     if (!key) return fail(DVC_ERR_INVALID, "set_tuning: null key");
+#if !DVC_DIAG
+    // ablations, timeline stamps and store-policy variants live in the diagnostics library only
+    for (const char *d : {"lookup_ablate", "build_ablate", "fused_ablate", "lookup_trace_lo", "lookup_trace_hi",
+                          "lookup_stpol"})
+        if (!strcmp(key, d))
+            return fail(DVC_ERR_UNSUPPORTED, "set_tuning: '%s' is a diagnostics knob: load libdvccorr_diag.so "
+                        "(make -C raft-dvc_amd/csrc diag; DVCCORR_LIB=.../libdvccorr_diag.so)", key);
+#endif
     if (!strcmp(key, "lookup_variant")) {
         if (value < 0 || value > 2) return fail(DVC_ERR_INVALID, "set_tuning: lookup_variant %d", value);
         g_lookup_variant = value;
@@ -599,11 +615,13 @@ int dvc_corr_build(const void *packed_q, const void *packed_t, void *corr, int B
             }
             return check_launch("corr_build");
         }
+#if DVC_DIAG
         if (g_build_ablate && Cp == 128 && !f32s) {   // diagnostics only
             if (g_build_ablate == 1) launch(k_build_bf16<16, false, 1>);
             else launch(k_build_bf16<16, false, 2>);
             return check_launch("corr_build");
         }
+#endif
         switch (Cp / 8) {
         case 4: f32s ? launch(k_build_bf16<4, true, 0>) : launch(k_build_bf16<4, false, 0>); break;
         case 8: f32s ? launch(k_build_bf16<8, true, 0>) : launch(k_build_bf16<8, false, 0>); break;
@@ -832,6 +850,14 @@ int dvc_corr_backward(const void *packed_q, const void *packed_t, const float *c
         return fail(DVC_ERR_INVALID, "corr_backward: bad dtype %d", dtype);
     return corr_backward(packed_q, packed_t, coords, grad_out, grad_fmap1, grad_fmap2, workspace, B, Nq, C, lay, radius,
                          convention, dtype, (hipStream_t)stream, g_err, sizeof(g_err));
+}
+
+int dvc_corr_backward_mfma(int B, int64_t Nq, int C, int H, int W, int D, int num_levels, int radius, int convention,
+                           int dtype) {
+    dvc_layout lay;
+    if (dvc_layout_init(H, W, D, num_levels, C, &lay)) return 0;
+    if (B < 1 || Nq < 1 || radius < 1 || radius > 6) return 0;
+    return backward_uses_mfma(B, Nq, lay, radius, convention, dtype);
 }
 
 int dvc_sample3d(const float *vol, const float *pts, float *out, int B, int C, int Hv, int Wv, int Dv, int64_t Nq,

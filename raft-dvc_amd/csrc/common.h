@@ -6,6 +6,13 @@
 
 #include "dvccorr.h"
 
+// DVC_DIAG = 1: the diagnostics library (libdvccorr_diag.so, `make diag`) -- ablation, timeline and store-policy
+// kernel instances reachable through dvc_set_tuning, for A/B tools only (DVCCORR_LIB selects it).  The product
+// library (libdvccorr.so) is built with DVC_DIAG = 0 and carries only product kernels.
+#ifndef DVC_DIAG
+#define DVC_DIAG 0
+#endif
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));

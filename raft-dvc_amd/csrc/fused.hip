@@ -224,6 +224,7 @@ static void launch_fused_box(const bf16_t *Q, const bf16_t *Tt, const LookupArgs
                     ngz = ((Dq + TZ - 1) / TZ + 1) / 2;
     const long long tiles = (long long)A.B * ngy * ngx * ngz * 32;
     const unsigned grid = (unsigned)(8 * ((tiles + 7) / 8));
+#if DVC_DIAG
     if constexpr (R == 4 && NWV == 8 && TY == 2 && TX == 2 && TZ == 16) {   // diagnostics (fused_ablate)
         if (A.ablate && Cp == 128) {
 #define DVC_FBOX_ABL(V) \
@@ -236,6 +237,7 @@ static void launch_fused_box(const bf16_t *Q, const bf16_t *Tt, const LookupArgs
 #undef DVC_FBOX_ABL
         }
     }
+#endif
     switch (Cp / 32) {
     case 1: k_fused_box<R, 1, NWV, TY, TX, TZ, 0><<<grid, 64 * NWV, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;
     case 2: k_fused_box<R, 2, NWV, TY, TX, TZ, 0><<<grid, 64 * NWV, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;

@@ -406,10 +406,12 @@ DVC_FBOX_ALLR(8, 2, 2, 16)
 DVC_FBOX_ALLR(4, 2, 2, 16)
 DVC_FBOX_ALLR(8, 4, 4, 4)
 
+#if DVC_DIAG
 // diagnostics instances (fused_ablate) of the default configuration
 #define DVC_FBOX_ABL(V) \
     template __global__ void k_fused_box<4, 4, 8, 2, 2, 16, V>(const bf16_t *, const bf16_t *, LookupArgs, int, \
                                                                long long, int, int, int, float);
 DVC_FBOX_ABL(1) DVC_FBOX_ABL(2) DVC_FBOX_ABL(3) DVC_FBOX_ABL(4) DVC_FBOX_ABL(8) DVC_FBOX_ABL(12) DVC_FBOX_ABL(13)
+#endif
 
 }  // namespace dvc

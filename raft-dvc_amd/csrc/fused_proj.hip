@@ -500,6 +500,7 @@ static void launch_fused_proj(const bf16_t *Q, const bf16_t *Tt, const LookupArg
                               int b, int Cp, long long t_rows, float scale, float *rows, hipStream_t s) {
     const long long nchunks = (A.Nq + 63) / 64;
     const unsigned grid = (unsigned)(8 * ((nchunks + 7) / 8));
+#if DVC_DIAG
     if constexpr (R == 4) {   // diagnostics instances (C_pad 128 only)
         if (A.ablate && Cp == 128) {
 #define DVC_FPROJ_ABL(V) \
@@ -512,6 +513,7 @@ static void launch_fused_proj(const bf16_t *Q, const bf16_t *Tt, const LookupArg
 #undef DVC_FPROJ_ABL
         }
     }
+#endif
     switch (Cp / 32) {
     case 1: k_fused_proj<R, 1, 0><<<grid, 512, 0, s>>>(Q, Tt, A, keys, b, Cp, t_rows, scale, rows); break;
     case 2: k_fused_proj<R, 2, 0><<<grid, 512, 0, s>>>(Q, Tt, A, keys, b, Cp, t_rows, scale, rows); break;

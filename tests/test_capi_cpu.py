@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol():
     for name in declared:
         assert hasattr(L, name), name
     assert set(declared) == set(_lib.EXPORTED)
-    assert L.dvc_abi_version() == 1
+    assert L.dvc_abi_version() == 2
     assert b"gfx950" in L.dvc_version()
 
 
@@ -137,6 +137,23 @@ def test_backward_validation_without_gpu():
     # rows) -- ~177 MB above the window gradients at #3
     nws = L.dvc_corr_backward_workspace_bytes(1, 32768, 128, 32, 32, 32, 4, 4)
     assert nws >= 4 * 32768 * 1000 * 4 and nws < 4 * 32768 * 1000 * 4 + 200 * 2 ** 20
+
+
+def test_backward_path_selection_without_gpu():
+    """Which gradient kernels dvc_corr_backward runs (pure host): 16-bit operands (bf16, and fp16 = the AMP pyramid)
+    on the matrix cores while k_grad_q_mfma's 32-bit buffer offsets cover the volume; fp32 operands, and volumes
+    past that range (a 160^3 level-0 fmap: 160 * 160 * 20 target tiles of 4 KB per (batch, channel group) exceed
+    2^31 bytes), on the 64-bit-addressed VALU kernels -- never a descriptor read past its range."""
+    from dvccorr import _lib
+    L = _lib.lib()
+    for dt in (_lib.DVC_BF16, _lib.DVC_F16):
+        assert L.dvc_corr_backward_mfma(1, 32768, 128, 32, 32, 32, 4, 4, 0, dt) == 1    # config #3
+        assert L.dvc_corr_backward_mfma(1, 4096, 128, 16, 16, 16, 4, 4, 1, dt) == 1     # config #2, legacy
+        assert L.dvc_corr_backward_mfma(1, 160 ** 3, 128, 160, 160, 160, 4, 4, 0, dt) == 0
+        assert L.dvc_corr_backward_mfma(1, 128 * 128 * 256, 128, 128, 128, 256, 4, 4, 0, dt) == 0
+        assert L.dvc_corr_backward_mfma(1, 64 ** 3, 128, 64, 64, 64, 4, 4, 0, dt) == 1   # config #4's fmaps
+    assert L.dvc_corr_backward_mfma(1, 32768, 128, 32, 32, 32, 4, 4, 0, _lib.DVC_F32) == 0
+    assert L.dvc_corr_backward_mfma(1, 32768, 128, 32, 32, 32, 4, 9, 0, _lib.DVC_BF16) == 0   # radius outside 1..6
 
 
 def test_coords_grid_matches_reference_fixture():

@@ -29,6 +29,7 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
 GRAD_TOL = 1e-5
 BF16_TOL = 1e-2
+FP16_TOL = 5e-3     # the reference's AMP tolerance, test_corr_equivalence.py:156-186
 CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "grad_*.npz")))
 
 
@@ -45,9 +46,23 @@ def _gpu_grads(kind, f1, f2, coords, G, L, r, legacy, precision="fp32"):
 @pytest.mark.parametrize("kind", ["gemm", "fused"])
 @pytest.mark.parametrize("case", CASES)
 def test_grad_golden(case, kind):
+    _check_golden(case, kind, "fp32", GRAD_TOL)
+
+
+# The matrix-core gradient kernels (bf16 and, for the materialised block, fp16 operands) against the reference's
+# own gradients at the production channel count and pyramid depth: grad_cfg2 is config #2's 16^3, C = 128, L = 4,
+# r = 4 (the shapes k_grad_q_mfma / k_grad_t_mfma are benchmarked at, with more than one split per level).
+@pytest.mark.parametrize("kind", ["gemm", "fused"])
+@pytest.mark.parametrize("precision,tol", [("bf16", BF16_TOL), ("fp16", FP16_TOL)])
+@pytest.mark.parametrize("case", ["grad_cfg2", "grad_edge_888_L4_r4", "grad_legacy_cube_L3_r2"])
+def test_grad_golden_low_precision(case, kind, precision, tol):
+    _check_golden(case, kind, precision, tol)
+
+
+def _check_golden(case, kind, precision, tol):
     g = load_golden(case + ".npz")
     f1, f2, coords, G, L, r, legacy = grad_inputs(g)
-    d1, d2 = _gpu_grads(kind, f1, f2, coords, G, L, r, legacy)
+    d1, d2 = _gpu_grads(kind, f1, f2, coords, G, L, r, legacy, precision=precision)
     assert np.isfinite(d1).all() and np.isfinite(d2).all()
     if "grad_f1" in g:
         e1, e2 = orc.rel_err(d1, g["grad_f1"]), orc.rel_err(d2, g["grad_f2"])
@@ -57,8 +72,8 @@ def test_grad_golden(case, kind):
         e2 = orc.rel_err(d2.reshape(-1)[idx], g["grad_f2_s"])
         for d, cs in ((d1, g["checksum_f1"]), (d2, g["checksum_f2"])):
             dd = d.astype(np.float64)
-            assert abs((dd * dd).sum() - cs[2]) / cs[2] < 1e-5
-    assert e1 <= GRAD_TOL and e2 <= GRAD_TOL, (case, kind, e1, e2)
+            assert abs((dd * dd).sum() - cs[2]) / cs[2] < tol
+    assert e1 <= tol and e2 <= tol, (case, kind, precision, e1, e2)
 
 
 @pytest.mark.parametrize("shape,C,L,r,legacy", [((9, 7, 5), 32, 2, 1, False), ((12, 10, 16), 64, 3, 2, False),
@@ -185,3 +200,44 @@ def test_grad_legacy_w_ne_d(shape, C, L, r):
     a1, a2 = _gpu_grads("gemm", f1, f2, coords, G, L, r, True)
     b1, b2 = _gpu_grads("gemm", f1, f2, coords, G, L, r, True)
     assert np.array_equal(a1, b1) and np.array_equal(a2, b2)
+
+
+@pytest.mark.parametrize("precision,tol", [("bf16", BF16_TOL), ("fp16", FP16_TOL), ("fp32", GRAD_TOL)])
+def test_grad_cfg3_slab(precision, tol):
+    """Config #3 at full size (32^3, C = 128, L = 4, r = 4, +-2-voxel flows: the shape the backward is benchmarked
+    at, so every size-dependent choice of the gradient kernels -- split counts sized by query count, the three-way
+    level group of k_grad_q_mfma, the 8-aligned tile starts of k_tile_targets / k_qt_tiles -- runs as in the bench)
+    with an output gradient that is nonzero on one ragged 512-row query slab only.  Against autograd through
+    oracle/torch_cpu.py's build_rows / lookup_rows on that slab (corr.py:141-208 restated; rows are independent):
+    d fmap1 on the slab rows, exact zeros elsewhere, d fmap2 in full."""
+    import dvccorr
+    from oracle import torch_cpu
+    B, C, S, L, r = 1, 128, 32, 4, 4
+    N, n3 = S ** 3, (2 * r + 1) ** 3
+    q0, q1 = 12345, 12345 + 512
+    f1 = prng.normal(7001, (B, C, S, S, S))
+    f2 = prng.normal(7002, (B, C, S, S, S))
+    coords = prng.flow_coords(7003, B, S, S, S, 2.0)
+    Gs = prng.normal(7004, (B, L * n3, q1 - q0))
+    # oracle: the slab's rows of every level, its lookup, autograd
+    t1 = torch.from_numpy(f1).requires_grad_(True)
+    t2 = torch.from_numpy(f2).requires_grad_(True)
+    pyr = torch_cpu.build_rows(t1, t2, L, q0, q1)
+    out = torch_cpu.lookup_rows(pyr, torch.from_numpy(coords), r, False, q0, q1)
+    (out * torch.from_numpy(Gs)).sum().backward()
+    ref1 = t1.grad.numpy().reshape(B, C, N)
+    ref2 = t2.grad.numpy()
+    # GPU: the whole block, G zero outside the slab
+    g1 = torch.from_numpy(f1).to(DEV).requires_grad_(True)
+    g2 = torch.from_numpy(f2).to(DEV).requires_grad_(True)
+    blk = dvccorr.CorrBlock(g1, g2, L, r, precision=precision)
+    G = torch.zeros((B, L * n3, N), device=DEV)
+    G[:, :, q0:q1] = torch.from_numpy(Gs).to(DEV)
+    (blk(torch.from_numpy(coords).to(DEV)) * G.view(B, L * n3, S, S, S)).sum().backward()
+    d1 = g1.grad.reshape(B, C, N).cpu().numpy()
+    d2 = g2.grad.cpu().numpy()
+    assert np.isfinite(d1).all() and np.isfinite(d2).all()
+    assert not d1[:, :, :q0].any() and not d1[:, :, q1:].any()
+    e1 = orc.rel_err(d1[:, :, q0:q1], ref1[:, :, q0:q1])
+    e2 = orc.rel_err(d2, ref2)
+    assert e1 <= tol and e2 <= tol, (precision, e1, e2)

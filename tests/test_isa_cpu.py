@@ -36,3 +36,38 @@ def test_no_packed_fp32_opsel_beside_mfma():
     assert any(v[2] for v in res.values())
     bad = {f"{b}:{k}": v[0] for b, (pk, _mf, _q, _m) in res.items() for k, v in pk.items()}
     assert not bad, bad
+
+
+def test_hidden_load_kernels_do_not_spill():
+    """k_build_f32r and the k_build_bf16 / k_build_bf16_2b instances with NCH <= 16 issue their operand loads from
+    inline asm, out of the compiler's s_waitcnt bookkeeping (build_gemm.hip, Hidden<NCH>).  That is only correct
+    while none of those destination registers is ever spilled or reassigned before its load lands (the round-1
+    fault: k_build_bf16_2b<32> spilled them).  The AMDGPU metadata of the shipped code objects must show no
+    private segment and no VGPR / SGPR spills for every such kernel."""
+    import isa_check
+    res = isa_check.kernel_resources(LIB)
+    hidden = [k for k in res if isa_check.HIDDEN_LOAD_KERNELS.search(k)]
+    assert len(hidden) >= 12, hidden     # k_build_f32r x 6, k_build_bf16 x 6+, k_build_bf16_2b x 6
+    assert any("k_build_f32r" in k for k in hidden) and any("k_build_bf16_2b" in k for k in hidden)
+    assert not isa_check.spill_violations(res), isa_check.spill_violations(res)
+    # the pattern recognises spills where they exist (the compiler-tracked NCH = 32 instances do spill)
+    assert any(v.get(".vgpr_spill_count", 0) for k, v in res.items() if "k_build_bf16_2bILi32E" in k)
+
+
+def test_product_library_has_no_diagnostics_instances():
+    """The ablation / timeline / store-policy instances are built only into libdvccorr_diag.so (make diag,
+    common.h DVC_DIAG); the shipped libdvccorr.so refuses their tuning knobs and carries none of them."""
+    import ctypes
+    import isa_check
+    names = list(isa_check.kernel_resources(LIB))
+    assert any("k_lookup_tile" in k for k in names) and any("k_fused_box" in k for k in names)
+    # ablation template arguments: k_lookup_tile<bf16, 4, true, ABL != 0, ...>, k_fused_box<..., ABL != 0>,
+    # k_build_bf16<16, false, ABL != 0>, k_fused_proj<4, 4, ABL != 0>
+    diag = [k for k in names if "k_lookup_tileItLi4ELb1ELi1E" in k or "k_lookup_tileItLi4ELb1ELi8E" in k
+            or "k_build_bf16ILi16ELb0ELi1E" in k or "k_fused_boxILi4ELi4ELi8ELi2ELi2ELi16ELi1E" in k
+            or "k_fused_projILi4ELi4ELi1E" in k or "k_lookup_tileItLi4ELb1ELi0ELb0ELi0ELi4ELi16E" in k]
+    assert not diag, diag
+    lib = ctypes.CDLL(LIB)
+    for key in (b"lookup_ablate", b"build_ablate", b"fused_ablate", b"lookup_stpol", b"lookup_trace_lo"):
+        assert lib.dvc_set_tuning(key, 1) == 2, key   # DVC_ERR_UNSUPPORTED
+    assert lib.dvc_set_tuning(b"lookup_variant", 2) == 0

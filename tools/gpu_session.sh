@@ -4,6 +4,10 @@
 #   bench   bench.py default line (config #3, the BASELINE metric) + the secondary lines in BENCH_SET
 #   prof    rocprofv3 --kernel-trace --stats of the default bench line
 #   pmc     rocprofv3 --pmc passes of the default lookup (tools/pmc_groups.sh; PMC_GROUPS overrides)
+#   bwd     rocprofv3 kernel stats of the backward (tools/prof_bwd.sh), then its PMC passes (tools/pmc_bwd.sh,
+#           groups in BWD_PMC_GROUPS; skipped when empty)
+#   diag    build nothing; checks that libdvccorr_diag.so (make -C raft-dvc_amd/csrc diag) is present for the
+#           A/B tools that need diagnostics knobs
 #   cmd     an arbitrary command in $CMD (A/B scripts), under its own timeout
 # Never retries a GPU step; a fault / abort / timeout ends the session.
 #   TAG=r3a STEPS="tests bench" bash tools/gpu_session.sh
@@ -57,6 +61,11 @@ for s in ${STEPS:-tests bench}; do
   pmc)
     TAG=$T VARIANT=2 PMC_GROUPS="${PMC_GROUPS:-FETCH_SIZE;WRITE_SIZE;SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_BUSY_CYCLES;TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE GRBM_COUNT}" \
         EXTRA="${PMC_EXTRA:---reps 2}" bash tools/pmc_groups.sh || exit 3 ;;
+  bwd)
+    TAG=${T}_bwd bash tools/prof_bwd.sh || exit 3
+    if [ -n "${BWD_PMC_GROUPS:-}" ]; then TAG=${T}_bwdpmc PMC_GROUPS="$BWD_PMC_GROUPS" bash tools/pmc_bwd.sh || exit 3; fi ;;
+  diag)
+    [ -f raft-dvc_amd/dvccorr/libdvccorr_diag.so ] || { echo "libdvccorr_diag.so missing (make -C raft-dvc_amd/csrc diag)"; exit 3; } ;;
   cmd)
     timeout -k 10 ${CMD_TIMEOUT:-600} bash -c "$CMD" > "$OUT/cmd.log" 2>&1; rc=$?
     echo "cmd rc=$rc"; tail -${CMD_TAIL:-40} "$OUT/cmd.log"

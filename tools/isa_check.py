@@ -8,7 +8,13 @@
     the broadcasts materialised by splat2() 0 of 220 poisoned runs differ, against ~4 % before).
     Round 3: SGPR-pair broadcasts (the epilogue scale of the build and fused kernels) are held to the
     same rule -- they were bit-exact in every test, but the guard no longer rests on that;
-  * MFMAs whose destination overlaps their own A or B source registers (reported, not fatal).
+  * MFMAs whose destination overlaps their own A or B source registers (reported, not fatal);
+  * (round 4, the library scan) scratch use in the kernels whose operand loads are hidden from the compiler's
+    s_waitcnt bookkeeping (inline-asm loads into VGPRs, waited for by counted s_waitcnt: k_build_f32r,
+    k_build_bf16_2b, k_build_bf16).  Those are correct only while the destination registers are never spilled:
+    a spill would store a register before its load has landed (the round-1 fault of k_build_bf16_2b<32>).  A
+    non-zero private segment, VGPR or SGPR spill count there fails the check; `--resources` lists every
+    kernel's VGPRs / AGPRs / LDS / scratch.
 
     python tools/isa_check.py                 the shipped dvccorr/libdvccorr.so (seconds: its gfx950 code
                                               objects are unbundled and disassembled)
@@ -81,6 +87,50 @@ def check_library(lib=LIB):
         return {f"bundle{i}": scan(d) for i, d in enumerate(disassemble_library(lib, tmp))}
 
 
+# kernels whose VGPR operand loads are issued from inline asm (invisible to the compiler's waitcnt insertion):
+# every k_build_f32r, and k_build_bf16 / k_build_bf16_2b with NCH <= 16 (build_gemm.hip Hidden<NCH>; the NCH = 32
+# instances load through the compiler and may spill)
+HIDDEN_LOAD_KERNELS = re.compile(r'k_build_f32r|k_build_bf16_2bILi(?:4|8|16)E|k_build_bf16ILi(?:4|8|16)E')
+RES_KEYS = (".vgpr_count", ".agpr_count", ".sgpr_count", ".vgpr_spill_count", ".sgpr_spill_count",
+            ".private_segment_fixed_size", ".group_segment_fixed_size")
+
+
+def kernel_resources(lib=LIB):
+    """{kernel symbol: {key: int}} from the AMDGPU metadata notes of every gfx950 code object in the library."""
+    res = {}
+    with tempfile.TemporaryDirectory() as tmp:
+        fb = os.path.join(tmp, "fatbin")
+        subprocess.run([LLVM + "/llvm-objcopy", "--dump-section", ".hip_fatbin=" + fb, lib, os.path.join(tmp, "c")],
+                       check=True)
+        data = open(fb, "rb").read()
+        offs = [m.start() for m in re.finditer(b"__CLANG_OFFLOAD_BUNDLE__", data)] + [len(data)]
+        for i in range(len(offs) - 1):
+            b, co = os.path.join(tmp, f"b{i}.bin"), os.path.join(tmp, f"b{i}.co")
+            open(b, "wb").write(data[offs[i]:offs[i + 1]])
+            subprocess.run([LLVM + "/clang-offload-bundler", "--unbundle", "--type=o", "--input=" + b,
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--output=" + co], check=True)
+            notes = subprocess.run([LLVM + "/llvm-readelf", "--notes", co], check=True, capture_output=True,
+                                   text=True).stdout
+            cur = {}
+            for line in notes.splitlines():
+                t = line.strip().lstrip("- ").strip()
+                for k in RES_KEYS:
+                    if t.startswith(k + ":"):
+                        cur[k] = int(t.split(":", 1)[1])
+                if t.startswith(".name:"):
+                    cur["name"] = t.split(":", 1)[1].strip()
+                if t.startswith(".wavefront_size:") and "name" in cur:   # last key of a kernel's record
+                    res[cur.pop("name")] = cur
+                    cur = {}
+    return res
+
+
+def spill_violations(res):
+    """Hidden-load kernels with scratch, VGPR or SGPR spills."""
+    return {k: v for k, v in res.items() if HIDDEN_LOAD_KERNELS.search(k) and
+            (v.get(".private_segment_fixed_size", 0) or v.get(".vgpr_spill_count", 0) or v.get(".sgpr_spill_count", 0))}
+
+
 def scan(asm):
     """(op_sel reads in kernels that also run MFMAs, MFMA overlaps, op_sel reads in MFMA-free kernels,
     names of the kernels that run MFMAs)"""
@@ -113,7 +163,22 @@ def check(files):
 
 
 if __name__ == "__main__":
+    if sys.argv[1:2] == ["--resources"]:
+        for k, v in sorted(kernel_resources().items(), key=lambda kv: kv[0]):
+            print(f"{k[:90]:90s} vgpr {v.get('.vgpr_count')} agpr {v.get('.agpr_count')} "
+                  f"lds {v.get('.group_segment_fixed_size')} scratch {v.get('.private_segment_fixed_size')} "
+                  f"spill {v.get('.vgpr_spill_count')}/{v.get('.sgpr_spill_count')}")
+        sys.exit(0)
     res = check(sys.argv[1:]) if sys.argv[1:] else check_library()
+    if not sys.argv[1:]:
+        rv = kernel_resources()
+        bad = spill_violations(rv)
+        hidden = [k for k in rv if HIDDEN_LOAD_KERNELS.search(k)]
+        print(f"hidden-load kernels checked for spills: {len(hidden)}; with scratch / spills: {len(bad)}")
+        for k, v in bad.items():
+            print(f"  SPILL in hidden-load kernel {k[:80]}: {v}")
+        if bad:
+            sys.exit(1)
     npk = 0
     for f, (pk, mf, quiet, _) in res.items():
         for k, v in pk.items():
