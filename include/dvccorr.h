@@ -77,7 +77,9 @@ typedef enum {
 
 /* DVC_F16: the reference's AMP pyramid (torch.amp.autocast('cuda') in its Trainer, trainer.py:249-252,
  * makes CorrBlock's matmul and pyramid float16, corr.py:155-167): pack, build (v_mfma_f32_32x32x16_f16),
- * pool, lookup (also convc1-fused) and backward; the on-the-fly entry points take F32 / BF16 only. */
+ * pool, lookup (also convc1-fused) and backward; the on-the-fly entry points (dvc_corr_lookup_fused,
+ * dvc_corr_lookup_fused_proj) take it too (round 4): the reference's CorrBlockOnTheFly einsum runs in fp16 under
+ * the same autocast (corr_otf.py:198-237), and the window dots are rounded to fp16 like the fp16 pyramid. */
 typedef enum { DVC_F32 = 0, DVC_BF16 = 1, DVC_F16 = 2 } dvc_dtype;
 
 /* Layout flag ORed into the dtype of dvc_pack_targets and the store_dtype of dvc_corr_lookup /
@@ -205,12 +207,12 @@ int dvc_corr_lookup_proj(const void *corr, const float *coords, const void *pack
 
 /* The same composition on the on-the-fly path (CorrBlockOnTheFly.__call__ followed by
  * F.relu(self.convc1(corr)), src/core/corr_otf.py:96-237 + src/core/update.py:246):
- * packed_q / packed_t as for dvc_corr_lookup_fused (bf16), packed_w from dvc_proj_pack,
+ * packed_q / packed_t as for dvc_corr_lookup_fused (bf16 or f16), packed_w from dvc_proj_pack,
  * out (B, 96, Nq) float32.  Queries are processed in order of their level-0 window
  * origin (a radix sort per call), so each workgroup's union of windows is small; the
  * per-query 96-channel rows are transposed to (B, 96, Nq) at the end.  Workspace:
  * dvc_lookup_fused_proj_workspace_bytes (sort keys + the [B][Nq][96] rows).
- * Supported: bf16, radius 1..4, C_pad in {32, 64, 128}, and for the legacy convention
+ * Supported: bf16 / f16, radius 1..4, C_pad in {32, 64, 128}, and for the legacy convention
  * W == D at every non-zero level (DVC_ERR_UNSUPPORTED otherwise). */
 size_t dvc_lookup_fused_proj_workspace_bytes(int B, int64_t Nq);
 int dvc_corr_lookup_fused_proj(const void *packed_q, const void *packed_t, const float *coords, const void *packed_w,

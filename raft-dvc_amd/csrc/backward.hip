@@ -191,9 +191,13 @@ template <int FMT> __device__ __forceinline__ unsigned gw_pair(float g) {
 // addresses for the channels took the kernel's registers), and the window is produced in two passes over its
 // column halves [J0, J1), each holding only output columns [U0, U1] of the two rows in flight (2 x 5 x n floats at
 // r = 4, was 2 x n x n): two waves per SIMD instead of one.  The column shared by the halves is loaded twice.
-// (r = 6 keeps one wave per SIMD: its two rows of 2 x 7 x 13 floats would spill at 256 VGPRs)
+// (r = 6 keeps one wave per SIMD: its two rows of 2 x 7 x 13 floats would spill at 256 VGPRs.)
+// DVC_WG_SPLIT=0 (A/B builds, tools/build_variant.sh): one pass over all columns at one wave per SIMD.
+#ifndef DVC_WG_SPLIT
+#define DVC_WG_SPLIT 1
+#endif
 template <int R, int FMT>
-__global__ __launch_bounds__(256, R <= 5 ? 2 : 1) void k_win_grad(BwdArgs A) {
+__global__ __launch_bounds__(256, (R <= 5 && DVC_WG_SPLIT) ? 2 : 1) void k_win_grad(BwdArgs A) {
     constexpr int n = 2 * R + 1, NW = 2 * R + 2, NW3 = NW * NW * NW;
     const int lane = threadIdx.x & 63;
     const long long nqb = (A.Nq + 63) / 64;
@@ -307,8 +311,12 @@ __global__ __launch_bounds__(256, R <= 5 ? 2 : 1) void k_win_grad(BwdArgs A) {
             plane(i + 1, rowB, rowA);
         }
     };
-    pass(std::integral_constant<int, 0>{}, std::integral_constant<int, NW / 2>{});
-    pass(std::integral_constant<int, NW / 2>{}, std::integral_constant<int, NW>{});
+    if constexpr (DVC_WG_SPLIT) {
+        pass(std::integral_constant<int, 0>{}, std::integral_constant<int, NW / 2>{});
+        pass(std::integral_constant<int, NW / 2>{}, std::integral_constant<int, NW>{});
+    } else {
+        pass(std::integral_constant<int, 0>{}, std::integral_constant<int, NW>{});
+    }
 }
 
 // Generic (legacy W != D) levels: lane = query; the window box is zeroed, then every output's

@@ -85,6 +85,9 @@ static thread_local int g_build_ablate = 0;       // diagnostics only: k_build_b
 // build output stores: 1 = nontemporal (default; round 2 A/B, bench n1 twice each: build 0.545 -> 0.506 ms,
 // step 2.20 -> 2.11 ms -- the 2.46 GB pyramid never fits the caches it would otherwise sweep), 0 = default policy
 static thread_local int g_build_stpol = 1;
+// column chunks per query tile are doubled while the build grid has fewer workgroups than this (tuning
+// "build_wgs"; 1024 = four per CU)
+static thread_local int g_build_wgs = 1024;
 static thread_local int g_build_variant = 1;      // 1 = two-barrier bf16-store kernel (k_build_bf16_2b), 0 = k_build_bf16
 static thread_local int g_build_f32_variant = 2;  // 2 = k_build_f32r, wave-private staging (default); 1 = k_build_f32r, workgroup staging; 0 = k_build_f32
 // fused lookup kernel where the MFMA path applies: 2 = k_fused_box 2x2x16, 8 waves (default),
@@ -350,6 +353,11 @@ int dvc_set_tuning(const char *key, int value) {
         g_build_f32_variant = value;
         return DVC_OK;
     }
+    if (!strcmp(key, "build_wgs")) {
+        if (value < 1) return fail(DVC_ERR_INVALID, "set_tuning: build_wgs %d < 1", value);
+        g_build_wgs = value;
+        return DVC_OK;
+    }
     if (!strcmp(key, "build_variant")) {
         if (value < 0 || value > 1) return fail(DVC_ERR_INVALID, "set_tuning: build_variant %d", value);
         g_build_variant = value;
@@ -567,7 +575,7 @@ int dvc_corr_build(const void *packed_q, const void *packed_t, void *corr, int B
     // rank's slab: 32 query tiles at config #3 / 8 GPUs) and every chunk keeps >= 2 column tiles
     const long long qtiles = ceil_div(Nq, in_dtype == DVC_F32 ? 64 : 128) * B;
     long long nch = 8;
-    while (qtiles * nch < 1024 && nch * 4 <= ncol_tiles && nch < 64) nch *= 2;
+    while (qtiles * nch < g_build_wgs && nch * 4 <= ncol_tiles && nch < 64) nch *= 2;
     const int nchunk = (int)std::min<long long>(nch, ncol_tiles);
     if (in_dtype == DVC_F16) {   // the AMP pyramid: fp16 operands on v_mfma_f32_32x32x16_f16, fp16 store
         if (store_dtype != DVC_F16) return fail(DVC_ERR_UNSUPPORTED, "build: float16 inputs need a float16 store");
@@ -823,7 +831,8 @@ int dvc_corr_lookup_fused(const void *packed_q, const void *packed_t, const floa
     if (radius < 0 || radius > 16) return fail(DVC_ERR_INVALID, "lookup_fused: radius %d outside [0, 16]", radius);
     if (convention != DVC_FIXED && convention != DVC_LEGACY)
         return fail(DVC_ERR_INVALID, "lookup_fused: bad convention %d", convention);
-    if (dtype != DVC_BF16 && dtype != DVC_F32) return fail(DVC_ERR_INVALID, "lookup_fused: bad dtype %d", dtype);
+    if (dtype != DVC_BF16 && dtype != DVC_F32 && dtype != DVC_F16)
+        return fail(DVC_ERR_INVALID, "lookup_fused: bad dtype %d", dtype);
     return fused_lookup(packed_q, packed_t, coords, out, workspace, B, Nq, C, lay, radius, convention, dtype,
                         g_fused_variant | (g_fused_ablate << 8), (hipStream_t)stream, g_err, sizeof(g_err));
 }
@@ -973,7 +982,8 @@ int dvc_corr_lookup_fused_proj(const void *packed_q, const void *packed_t, const
     if (B < 1 || Nq < 1) return fail(DVC_ERR_INVALID, "lookup_fused_proj: B=%d Nq=%lld", B, (long long)Nq);
     if (convention != DVC_FIXED && convention != DVC_LEGACY)
         return fail(DVC_ERR_INVALID, "lookup_fused_proj: bad convention %d", convention);
-    if (dtype != DVC_BF16 && dtype != DVC_F32) return fail(DVC_ERR_INVALID, "lookup_fused_proj: bad dtype %d", dtype);
+    if (dtype != DVC_BF16 && dtype != DVC_F32 && dtype != DVC_F16)
+        return fail(DVC_ERR_INVALID, "lookup_fused_proj: bad dtype %d", dtype);
     return fused_lookup_proj(packed_q, packed_t, coords, packed_w, bias, out, workspace, B, Nq, C, lay, radius,
                              convention, dtype, g_fused_ablate, (hipStream_t)stream, g_err, sizeof(g_err));
 }

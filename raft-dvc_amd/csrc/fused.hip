@@ -17,6 +17,8 @@
 #include <algorithm>
 #include <stdio.h>
 
+#include <type_traits>
+
 #include "common.h"
 #include "lookup_common.h"
 
@@ -40,6 +42,17 @@ template <> struct Dot<bf16_t> {
         for (int i = 0; i < 4; ++i) {
             acc = __builtin_fmaf(__uint_as_float(a[i] << 16), __uint_as_float(b[i] << 16), acc);
             acc = __builtin_fmaf(__uint_as_float(a[i] & 0xffff0000u), __uint_as_float(b[i] & 0xffff0000u), acc);
+        }
+        return acc;
+    }
+    static constexpr int kPerChunk = 8;
+};
+template <> struct Dot<f16_t> {   // fp16 operands (the AMP block): same FMA order as Dot<bf16_t>
+    static __device__ __forceinline__ float chunk(const u32x4 &a, const u32x4 &b, float acc) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            acc = __builtin_fmaf(bits16_to_f32<f16_t>(a[i]), bits16_to_f32<f16_t>(b[i]), acc);
+            acc = __builtin_fmaf(bits16_to_f32<f16_t>(a[i] >> 16), bits16_to_f32<f16_t>(b[i] >> 16), acc);
         }
         return acc;
     }
@@ -188,12 +201,13 @@ static void fused_level(int R, const T *Q, const T *Tt, LookupArgs &A, float *ws
 template <int R, int NCH>
 __global__ void k_fused_tile(const bf16_t *, const bf16_t *, LookupArgs, int, long long, int, int, int, float);
 
-// The MFMA tile kernel (fused_tile.hip) covers bf16, r <= 4, C_pad in {32, 64, 128}, whole (y, x)
-// planes of queries (Nq a multiple of W*D: the full grid or an H-slab of it) and
-// packed targets addressable with 32-bit byte offsets.
+// The MFMA kernels (fused_box.hip, fused_tile.hip) cover 16-bit operands, r <= 4, C_pad in {32, 64, 128},
+// whole (y, x) planes of queries (Nq a multiple of W*D: the full grid or an H-slab of it) and packed targets
+// addressable with 32-bit byte offsets.  fp16 (the AMP block) runs on the box kernels; the round-1 tile kernel
+// (variant 1) is bf16 only, so an fp16 request for it takes the default box kernel.
 static bool fused_tile_ok(long long Nq, int W, int D, int Cp, long long t_rows, int radius, int dtype) {
-    return dtype == DVC_BF16 && radius >= 1 && radius <= 4 && (Cp == 32 || Cp == 64 || Cp == 128) &&
-           Nq % ((long long)W * D) == 0 &&
+    return (dtype == DVC_BF16 || dtype == DVC_F16) && radius >= 1 && radius <= 4 &&
+           (Cp == 32 || Cp == 64 || Cp == 128) && Nq % ((long long)W * D) == 0 &&
            t_rows * Cp * 2 < (1LL << 31) - 65536;
 }
 
@@ -213,10 +227,10 @@ static void launch_fused_tile(const bf16_t *Q, const bf16_t *Tt, const LookupArg
     }
 }
 
-template <int R, int KS, int NWAVES, int TY, int TX, int TZ, int ABL>
+template <int R, int KS, int NWAVES, int TY, int TX, int TZ, int ABL, typename E>
 __global__ void k_fused_box(const bf16_t *, const bf16_t *, LookupArgs, int, long long, int, int, int, float);
 
-template <int R, int NWV, int TY, int TX, int TZ>
+template <int R, int NWV, int TY, int TX, int TZ, typename E>
 static void launch_fused_box(const bf16_t *Q, const bf16_t *Tt, const LookupArgs &A, int Cp, long long t_rows,
                              int Hq, int Wq, int Dq, float scale, hipStream_t s) {
     // boxes in 4 x 4 x 2 groups, padded to a multiple of 8 workgroups (one range per XCD)
@@ -225,10 +239,11 @@ static void launch_fused_box(const bf16_t *Q, const bf16_t *Tt, const LookupArgs
     const long long tiles = (long long)A.B * ngy * ngx * ngz * 32;
     const unsigned grid = (unsigned)(8 * ((tiles + 7) / 8));
 #if DVC_DIAG
-    if constexpr (R == 4 && NWV == 8 && TY == 2 && TX == 2 && TZ == 16) {   // diagnostics (fused_ablate)
+    if constexpr (R == 4 && NWV == 8 && TY == 2 && TX == 2 && TZ == 16 && std::is_same<E, bf16_t>::value) {
         if (A.ablate && Cp == 128) {
 #define DVC_FBOX_ABL(V) \
-    case V: k_fused_box<4, 4, 8, 2, 2, 16, V><<<grid, 512, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); return;
+    case V: k_fused_box<4, 4, 8, 2, 2, 16, V, bf16_t><<<grid, 512, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); \
+        return;
             switch (A.ablate) {
                 DVC_FBOX_ABL(1) DVC_FBOX_ABL(2) DVC_FBOX_ABL(3) DVC_FBOX_ABL(4) DVC_FBOX_ABL(8) DVC_FBOX_ABL(12)
                 DVC_FBOX_ABL(13)
@@ -239,19 +254,25 @@ static void launch_fused_box(const bf16_t *Q, const bf16_t *Tt, const LookupArgs
     }
 #endif
     switch (Cp / 32) {
-    case 1: k_fused_box<R, 1, NWV, TY, TX, TZ, 0><<<grid, 64 * NWV, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;
-    case 2: k_fused_box<R, 2, NWV, TY, TX, TZ, 0><<<grid, 64 * NWV, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;
-    default: k_fused_box<R, 4, NWV, TY, TX, TZ, 0><<<grid, 64 * NWV, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;
+    case 1: k_fused_box<R, 1, NWV, TY, TX, TZ, 0, E><<<grid, 64 * NWV, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;
+    case 2: k_fused_box<R, 2, NWV, TY, TX, TZ, 0, E><<<grid, 64 * NWV, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;
+    default: k_fused_box<R, 4, NWV, TY, TX, TZ, 0, E><<<grid, 64 * NWV, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;
     }
 }
 
-template <int R>
+template <int R, typename E>
 static void launch_fused_mfma(int variant, const bf16_t *Q, const bf16_t *Tt, const LookupArgs &A, int Cp,
                               long long t_rows, int Hq, int Wq, int Dq, float scale, hipStream_t s) {
-    if (variant == 1) launch_fused_tile<R>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale, s);
-    else if (variant == 3) launch_fused_box<R, 8, 4, 4, 4>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale, s);
-    else if (variant == 4) launch_fused_box<R, 4, 2, 2, 16>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale, s);
-    else launch_fused_box<R, 8, 2, 2, 16>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale, s);
+    if (variant == 1 && std::is_same<E, bf16_t>::value) launch_fused_tile<R>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale, s);
+    else if (variant == 3) launch_fused_box<R, 8, 4, 4, 4, E>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale, s);
+    else if (variant == 4) launch_fused_box<R, 4, 2, 2, 16, E>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale, s);
+    else launch_fused_box<R, 8, 2, 2, 16, E>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale, s);
+}
+template <int R>
+static void launch_fused_mfma_dt(int dtype, int variant, const bf16_t *Q, const bf16_t *Tt, const LookupArgs &A, int Cp,
+                                 long long t_rows, int Hq, int Wq, int Dq, float scale, hipStream_t s) {
+    if (dtype == DVC_F16) launch_fused_mfma<R, f16_t>(variant, Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale, s);
+    else launch_fused_mfma<R, bf16_t>(variant, Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale, s);
 }
 
 int fused_lookup(const void *packed_q, const void *packed_t, const float *coords, float *out, void *workspace, int B,
@@ -260,7 +281,7 @@ int fused_lookup(const void *packed_q, const void *packed_t, const float *coords
     const int Cp = lay.c_pad;
     const int ablate = variant >> 8;   // diagnostics knob (capi fused_ablate)
     variant &= 0xff;
-    if ((dtype == DVC_BF16 && Cp > 512) || (dtype == DVC_F32 && Cp > 256)) {
+    if ((dtype != DVC_F32 && Cp > 512) || (dtype == DVC_F32 && Cp > 256)) {
         snprintf(err, errlen, "lookup_fused: C=%d too large", C);
         return DVC_ERR_UNSUPPORTED;
     }
@@ -301,10 +322,10 @@ int fused_lookup(const void *packed_q, const void *packed_t, const float *coords
         const int Hq = (int)(Nq / ((long long)Wq * Dq));
         const bf16_t *Q = (const bf16_t *)packed_q, *Tt = (const bf16_t *)packed_t;
         switch (radius) {
-        case 1: launch_fused_mfma<1>(variant, Q, Tt, T, Cp, lay.row_stride, Hq, Wq, Dq, scale, s); break;
-        case 2: launch_fused_mfma<2>(variant, Q, Tt, T, Cp, lay.row_stride, Hq, Wq, Dq, scale, s); break;
-        case 3: launch_fused_mfma<3>(variant, Q, Tt, T, Cp, lay.row_stride, Hq, Wq, Dq, scale, s); break;
-        default: launch_fused_mfma<4>(variant, Q, Tt, T, Cp, lay.row_stride, Hq, Wq, Dq, scale, s); break;
+        case 1: launch_fused_mfma_dt<1>(dtype, variant, Q, Tt, T, Cp, lay.row_stride, Hq, Wq, Dq, scale, s); break;
+        case 2: launch_fused_mfma_dt<2>(dtype, variant, Q, Tt, T, Cp, lay.row_stride, Hq, Wq, Dq, scale, s); break;
+        case 3: launch_fused_mfma_dt<3>(dtype, variant, Q, Tt, T, Cp, lay.row_stride, Hq, Wq, Dq, scale, s); break;
+        default: launch_fused_mfma_dt<4>(dtype, variant, Q, Tt, T, Cp, lay.row_stride, Hq, Wq, Dq, scale, s); break;
         }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) {
@@ -326,12 +347,18 @@ int fused_lookup(const void *packed_q, const void *packed_t, const float *coords
                 if (dtype == DVC_BF16)
                     k_fused_generic<bf16_t><<<(unsigned)((total + 255) / 256), 256, 0, s>>>(
                         (const bf16_t *)packed_q, (const bf16_t *)packed_t, A, Cp, lay.row_stride, scale);
+                else if (dtype == DVC_F16)
+                    k_fused_generic<f16_t><<<(unsigned)((total + 255) / 256), 256, 0, s>>>(
+                        (const f16_t *)packed_q, (const f16_t *)packed_t, A, Cp, lay.row_stride, scale);
                 else
                     k_fused_generic<float><<<(unsigned)((total + 255) / 256), 256, 0, s>>>(
                         (const float *)packed_q, (const float *)packed_t, A, Cp, lay.row_stride, scale);
             } else if (dtype == DVC_BF16) {
                 fused_level<bf16_t>(radius, (const bf16_t *)packed_q, (const bf16_t *)packed_t, A, (float *)workspace,
                                     Cp, lay.row_stride, scale, s);
+            } else if (dtype == DVC_F16) {
+                fused_level<f16_t>(radius, (const f16_t *)packed_q, (const f16_t *)packed_t, A, (float *)workspace,
+                                   Cp, lay.row_stride, scale, s);
             } else {
                 fused_level<float>(radius, (const float *)packed_q, (const float *)packed_t, A, (float *)workspace,
                                    Cp, lay.row_stride, scale, s);

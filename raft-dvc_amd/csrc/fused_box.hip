@@ -55,7 +55,8 @@ template <int R, int NWAVES> struct BoxCfg {
 
 // ABL (diagnostics only, never the product path; capi "fused_ablate"): 1 no output stores, 2 no window
 // dots, 4 no target loads, 8 no window writes
-template <int R, int KS, int NWAVES, int TY, int TX, int TZ, int ABL>
+// E: bf16_t or f16_t operands (E16 in fused_common.h); the buffers hold E bits either way
+template <int R, int KS, int NWAVES, int TY, int TX, int TZ, int ABL, typename E = bf16_t>
 __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__restrict__ Q,
                                                               const bf16_t *__restrict__ Tt, LookupArgs A,
                                                               int Cp, long long t_rows, int Hq, int Wq, int Dq,
@@ -241,7 +242,7 @@ __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__re
                 for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], bq[j][ks], acc[j], 0, 0, 0);
+                        acc[j] = E16<E>::mma(a[ks], bq[j][ks], acc[j]);
             };
             auto epilogue = [&](const f32x4 (&acc)[4]) {
                 const int z0 = zs + 16 * pe.zb;
@@ -252,8 +253,8 @@ __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__re
                 for (int j = 0; j < 4; ++j) {
                     const f32x2 lo = f32x2{acc[j][0], acc[j][1]} * sc2;
                     const f32x2 hi = f32x2{acc[j][2], acc[j][3]} * sc2;
-                    const unsigned p01 = __builtin_bit_cast(unsigned, __builtin_convertvector(lo, bf16x2));
-                    const unsigned p23 = __builtin_bit_cast(unsigned, __builtin_convertvector(hi, bf16x2));
+                    const unsigned p01 = E16<E>::pack2(lo);
+                    const unsigned p23 = E16<E>::pack2(hi);
                     if constexpr ((ABL & 8) != 0) {   // diagnostics: no window writes (keep the values live)
                         sink ^= p01 ^ p23;
                         continue;
@@ -328,8 +329,8 @@ __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__re
 #pragma unroll
             for (int i = 0; i < NW / 2; ++i) {
                 const unsigned w = __builtin_amdgcn_alignbit(dw[i + 1], dw[i], rsh);
-                r[2 * i] = __uint_as_float(w << 16);
-                r[2 * i + 1] = __uint_as_float(w & 0xffff0000u);
+                r[2 * i] = E16<E>::lo(w);
+                r[2 * i + 1] = E16<E>::hi(w);
             }
 #pragma unroll
             for (int i = 0; i < NP; ++i)
@@ -396,7 +397,10 @@ __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__re
 
 #define DVC_FBOX_INST1(R, KS, NWV, TY, TX, TZ)                                                                    \
     template __global__ void k_fused_box<R, KS, NWV, TY, TX, TZ, 0>(const bf16_t *, const bf16_t *, LookupArgs, int, \
-                                                                    long long, int, int, int, float);
+                                                                    long long, int, int, int, float);                \
+    template __global__ void k_fused_box<R, KS, NWV, TY, TX, TZ, 0, f16_t>(const bf16_t *, const bf16_t *,            \
+                                                                           LookupArgs, int, long long, int, int, int, \
+                                                                           float);
 #define DVC_FBOX_INST(R, NWV, TY, TX, TZ)                                                                      \
     DVC_FBOX_INST1(R, 1, NWV, TY, TX, TZ) DVC_FBOX_INST1(R, 2, NWV, TY, TX, TZ) DVC_FBOX_INST1(R, 4, NWV, TY, TX, TZ)
 #define DVC_FBOX_ALLR(NWV, TY, TX, TZ)                                                                         \

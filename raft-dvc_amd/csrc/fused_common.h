@@ -28,6 +28,34 @@ __device__ __forceinline__ int bwave_max(int v) {
     return buni(v);
 }
 
+// 16-bit operand policy of the MFMA on-the-fly kernels: bf16, or fp16 -- the reference's CorrBlockOnTheFly under
+// its Trainer's autocast runs the einsum in fp16 (corr_otf.py:198-237, trainer.py:249-257).  The window dots are
+// rounded to E exactly as the materialised build rounds its E pyramid (build_gemm.hip Mma16<E>: the same
+// f32x2 -> E x 2 conversion), so the on-the-fly lookup equals the materialised E path.
+template <typename E> struct E16;
+template <> struct E16<bf16_t> {
+    static __device__ __forceinline__ f32x4 mma(bf16x8 a, bf16x8 b, f32x4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ unsigned pack2(f32x2 v) {
+        return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
+    }
+    static __device__ __forceinline__ float lo(unsigned w) { return __uint_as_float(w << 16); }
+    static __device__ __forceinline__ float hi(unsigned w) { return __uint_as_float(w & 0xffff0000u); }
+};
+template <> struct E16<f16_t> {
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    static __device__ __forceinline__ f32x4 mma(bf16x8 a, bf16x8 b, f32x4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b), c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ unsigned pack2(f32x2 v) {
+        return __builtin_bit_cast(unsigned, __builtin_convertvector(v, h2));
+    }
+    static __device__ __forceinline__ float lo(unsigned w) { return bits16_to_f32<f16_t>(w); }
+    static __device__ __forceinline__ float hi(unsigned w) { return bits16_to_f32<f16_t>(w >> 16); }
+};
+
 template <int n> struct BRun {
     f32x2 p[n / 2];
     float t;

@@ -99,7 +99,8 @@ __global__ __launch_bounds__(256) void k_otf_keys(LookupArgs A, int b, int ncx, 
 
 // ABL (diagnostics only, never the product path; capi "fused_ablate"): 1 no phase 1, 2 no producers,
 // 4 no convc1 MFMA, 8 no window writes, 16 no target loads
-template <int R, int KS, int ABL>
+// E: bf16_t, or f16_t for the AMP block (E16 in fused_common.h: the dots rounded to fp16 like the fp16 pyramid)
+template <int R, int KS, int ABL, typename E = bf16_t>
 __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict__ Q, const bf16_t *__restrict__ Tt,
                                                        LookupArgs A, const unsigned long long *__restrict__ keys,
                                                        int b, int Cp, long long t_rows, float scale,
@@ -243,7 +244,7 @@ __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict_
                 for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                        d[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], bq[j][ks], d[j], 0, 0, 0);
+                        d[j] = E16<E>::mma(a[ks], bq[j][ks], d[j]);
             };
             auto epilogue = [&](const f32x4 (&d)[4]) {
                 const int z0 = zs + 16 * pe.zb;
@@ -254,8 +255,8 @@ __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict_
                 for (int j = 0; j < 4; ++j) {
                     const f32x2 lo = f32x2{d[j][0], d[j][1]} * sc2;
                     const f32x2 hi = f32x2{d[j][2], d[j][3]} * sc2;
-                    const unsigned p01 = __builtin_bit_cast(unsigned, __builtin_convertvector(lo, bf16x2));
-                    const unsigned p23 = __builtin_bit_cast(unsigned, __builtin_convertvector(hi, bf16x2));
+                    const unsigned p01 = E16<E>::pack2(lo);
+                    const unsigned p23 = E16<E>::pack2(hi);
                     if constexpr ((ABL & 8) != 0) {
                         sink ^= p01 ^ p23;
                         continue;
@@ -335,8 +336,8 @@ __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict_
 #pragma unroll
             for (int i = 0; i < NW / 2; ++i) {
                 const unsigned w = __builtin_amdgcn_alignbit(dw[i + 1], dw[i], rsh);
-                r[2 * i] = __uint_as_float(w << 16);
-                r[2 * i + 1] = __uint_as_float(w & 0xffff0000u);
+                r[2 * i] = E16<E>::lo(w);
+                r[2 * i + 1] = E16<E>::hi(w);
             }
 #pragma unroll
             for (int i = 0; i < NP; ++i)
@@ -495,13 +496,13 @@ size_t fused_proj_workspace_bytes(int B, long long Nq) {
     return P.total;
 }
 
-template <int R>
+template <int R, typename E>
 static void launch_fused_proj(const bf16_t *Q, const bf16_t *Tt, const LookupArgs &A, const unsigned long long *keys,
                               int b, int Cp, long long t_rows, float scale, float *rows, hipStream_t s) {
     const long long nchunks = (A.Nq + 63) / 64;
     const unsigned grid = (unsigned)(8 * ((nchunks + 7) / 8));
 #if DVC_DIAG
-    if constexpr (R == 4) {   // diagnostics instances (C_pad 128 only)
+    if constexpr (R == 4 && std::is_same<E, bf16_t>::value) {   // diagnostics instances (C_pad 128 only)
         if (A.ablate && Cp == 128) {
 #define DVC_FPROJ_ABL(V) \
     case V: k_fused_proj<4, 4, V><<<grid, 512, 0, s>>>(Q, Tt, A, keys, b, Cp, t_rows, scale, rows); return;
@@ -515,9 +516,9 @@ static void launch_fused_proj(const bf16_t *Q, const bf16_t *Tt, const LookupArg
     }
 #endif
     switch (Cp / 32) {
-    case 1: k_fused_proj<R, 1, 0><<<grid, 512, 0, s>>>(Q, Tt, A, keys, b, Cp, t_rows, scale, rows); break;
-    case 2: k_fused_proj<R, 2, 0><<<grid, 512, 0, s>>>(Q, Tt, A, keys, b, Cp, t_rows, scale, rows); break;
-    default: k_fused_proj<R, 4, 0><<<grid, 512, 0, s>>>(Q, Tt, A, keys, b, Cp, t_rows, scale, rows); break;
+    case 1: k_fused_proj<R, 1, 0, E><<<grid, 512, 0, s>>>(Q, Tt, A, keys, b, Cp, t_rows, scale, rows); break;
+    case 2: k_fused_proj<R, 2, 0, E><<<grid, 512, 0, s>>>(Q, Tt, A, keys, b, Cp, t_rows, scale, rows); break;
+    default: k_fused_proj<R, 4, 0, E><<<grid, 512, 0, s>>>(Q, Tt, A, keys, b, Cp, t_rows, scale, rows); break;
     }
 }
 
@@ -526,8 +527,8 @@ int fused_lookup_proj(const void *packed_q, const void *packed_t, const float *c
                       const dvc_layout &lay, int radius, int convention, int dtype, int ablate, hipStream_t s,
                       char *err, size_t errlen) {
     const int Cp = lay.c_pad;
-    if (dtype != DVC_BF16) {
-        snprintf(err, errlen, "lookup_fused_proj: the bf16 path only (an fp32 block takes relu(conv3d(lookup)))");
+    if (dtype != DVC_BF16 && dtype != DVC_F16) {
+        snprintf(err, errlen, "lookup_fused_proj: 16-bit operands only (an fp32 block takes relu(conv3d(lookup)))");
         return DVC_ERR_UNSUPPORTED;
     }
     if (radius < 1 || radius > DVC_PROJ_MAX_RADIUS) {
@@ -596,11 +597,20 @@ int fused_lookup_proj(const void *packed_q, const void *packed_t, const float *c
             snprintf(err, errlen, "lookup_fused_proj: radix sort failed");
             return DVC_ERR_RUNTIME;
         }
-        switch (radius) {
-        case 1: launch_fused_proj<1>(Q, Tt, A, kout, b, Cp, lay.row_stride, scale, rows, s); break;
-        case 2: launch_fused_proj<2>(Q, Tt, A, kout, b, Cp, lay.row_stride, scale, rows, s); break;
-        case 3: launch_fused_proj<3>(Q, Tt, A, kout, b, Cp, lay.row_stride, scale, rows, s); break;
-        default: launch_fused_proj<4>(Q, Tt, A, kout, b, Cp, lay.row_stride, scale, rows, s); break;
+        if (dtype == DVC_F16) {
+            switch (radius) {
+            case 1: launch_fused_proj<1, f16_t>(Q, Tt, A, kout, b, Cp, lay.row_stride, scale, rows, s); break;
+            case 2: launch_fused_proj<2, f16_t>(Q, Tt, A, kout, b, Cp, lay.row_stride, scale, rows, s); break;
+            case 3: launch_fused_proj<3, f16_t>(Q, Tt, A, kout, b, Cp, lay.row_stride, scale, rows, s); break;
+            default: launch_fused_proj<4, f16_t>(Q, Tt, A, kout, b, Cp, lay.row_stride, scale, rows, s); break;
+            }
+        } else {
+            switch (radius) {
+            case 1: launch_fused_proj<1, bf16_t>(Q, Tt, A, kout, b, Cp, lay.row_stride, scale, rows, s); break;
+            case 2: launch_fused_proj<2, bf16_t>(Q, Tt, A, kout, b, Cp, lay.row_stride, scale, rows, s); break;
+            case 3: launch_fused_proj<3, bf16_t>(Q, Tt, A, kout, b, Cp, lay.row_stride, scale, rows, s); break;
+            default: launch_fused_proj<4, bf16_t>(Q, Tt, A, kout, b, Cp, lay.row_stride, scale, rows, s); break;
+            }
         }
         if (!launched("fused_proj")) return DVC_ERR_LAUNCH;
     }

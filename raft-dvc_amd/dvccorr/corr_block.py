@@ -59,7 +59,7 @@ __all__ = ["CorrBlock", "CorrBlockFused", "CorrBlockOnTheFly", "bilinear_sampler
 _CANON = {ops.DVC_F32: "fp32", ops.DVC_BF16: "bf16", ops.DVC_F16: "fp16"}
 
 
-def resolve_precision(fmap: torch.Tensor, precision: Optional[str], fp16_ok: bool = True) -> str:
+def resolve_precision(fmap: torch.Tensor, precision: Optional[str]) -> str:
     """Storage/MFMA precision of the pyramid.  Explicit argument > DVCCORR_PRECISION >
     AMP policy > input dtype.
 
@@ -70,18 +70,17 @@ def resolve_precision(fmap: torch.Tensor, precision: Optional[str], fp16_ok: boo
     float32.  Inside an enabled CUDA autocast region (the float16 one: the reference's
     trainer uses autocast's default dtype) this block likewise packs, builds and stores
     fp16 (v_mfma_f32_32x32x16_f16) and returns float32 lookups; an autocast region set to
-    bfloat16 gives bf16.  Outside autocast, float32 fmaps build in exact f32.
-
-    fp16_ok=False (the on-the-fly block, whose kernels take fp32 / bf16 operands): an fp16
-    request or policy resolves to bf16 (same storage width, fp32's exponent range)."""
+    bfloat16 gives bf16.  Outside autocast, float32 fmaps build in exact f32.  The on-the-fly
+    block follows the same policy: under autocast its window dots run on fp16 MFMA
+    (v_mfma_f32_16x16x32_f16), as the reference's CorrBlockOnTheFly einsum runs in fp16
+    (corr_otf.py:198-237)."""
     if precision is None:
         precision = os.environ.get("DVCCORR_PRECISION") or None
     if precision is None and fmap.is_cuda and torch.is_autocast_enabled("cuda"):
         precision = "bf16" if torch.get_autocast_dtype("cuda") == torch.bfloat16 else "fp16"
     if precision is None:
         precision = {torch.float32: "fp32", torch.float16: "fp16"}.get(fmap.dtype, "bf16")
-    p = _CANON[ops.dtype_code(precision)]
-    return "bf16" if p == "fp16" and not fp16_ok else p
+    return _CANON[ops.dtype_code(precision)]
 
 
 def _wants_grad(*ts: torch.Tensor) -> bool:
@@ -279,7 +278,7 @@ class CorrBlockFused(_Block):
         B, C, H, W, D = fmap1.shape
         self.shape = (B, C, H, W, D)
         self._lay = layout(H, W, D, num_levels, C)
-        self.precision = resolve_precision(fmap1, precision, fp16_ok=False)
+        self.precision = resolve_precision(fmap1, precision)
         self._dt = ops.dtype_code(self.precision)
         self._grad_fmaps = (fmap1, fmap2) if _wants_grad(fmap1, fmap2) else None
         if self._grad_fmaps is not None:

@@ -191,8 +191,7 @@ class ShardedCorrBlock:
         self.shape = (B, C, Hs, W, D)
         self.num_levels, self.radius, self.legacy_wd_swap = num_levels, radius, legacy_wd_swap
         self.gather_output = gather_output
-        # (the on-the-fly rows take fp32 / bf16 operands only: fp16 resolves to bf16 there)
-        precision = resolve_precision(fmap1_slab, precision, fp16_ok=impl == "materialised")
+        precision = resolve_precision(fmap1_slab, precision)
         stream = torch.cuda.current_stream(fmap1_slab.device) if fmap1_slab.is_cuda else None
         if build_events is not None and stream is not None:
             e0 = torch.cuda.Event(enable_timing=True)

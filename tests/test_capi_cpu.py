@@ -174,7 +174,6 @@ def test_precision_policy_host_logic(monkeypatch):
     assert dvccorr.resolve_precision(torch.zeros(1, dtype=torch.float16), None) == "fp16"
     assert dvccorr.resolve_precision(f32, "bf16") == "bf16"
     assert dvccorr.resolve_precision(f32, "float16") == "fp16"
-    assert dvccorr.resolve_precision(f32, "fp16", fp16_ok=False) == "bf16"   # the on-the-fly block's operands
     monkeypatch.setenv("DVCCORR_PRECISION", "bf16")
     assert dvccorr.resolve_precision(f32, None) == "bf16"
     assert dvccorr.resolve_precision(b16, "fp32") == "fp32"

@@ -83,9 +83,13 @@ def test_autocast_default_is_fp16_and_closer_than_bf16():
     assert blk.precision == "fp16" and out.dtype == torch.float32
     e16, ebf = _compare(out.cpu().numpy(), g), _compare(bf.cpu().numpy(), g)
     assert e16 <= AMP_TOL and e16 < ebf, (e16, ebf)
-    # fp16 inputs default to fp16, the on-the-fly block keeps bf16 operands
+    # fp16 inputs default to fp16; the on-the-fly block follows the same policy (round 4: fp16 MFMA operands,
+    # as the reference's CorrBlockOnTheFly einsum under autocast, corr_otf.py:198-237)
     assert dvccorr.CorrBlock(t1.half(), t2.half(), L, r).precision == "fp16"
-    assert dvccorr.CorrBlockFused(t1, t2, L, r, precision="fp16").precision == "bf16"
+    assert dvccorr.CorrBlockFused(t1, t2, L, r, precision="fp16").precision == "fp16"
+    with torch.amp.autocast("cuda"):
+        assert dvccorr.CorrBlockFused(t1, t2, L, r).precision == "fp16"
+        assert dvccorr.CorrBlockOnTheFly(t1, t2, L, r).precision == "fp16"
 
 
 def test_fp16_bricked_equals_linear_and_walk():
@@ -128,8 +132,8 @@ def test_fp16_convc1_fused(name):
 
 
 def test_fp16_backward():
-    """Gradients of an fp16 block (fp32 VALU gradient kernels over fp16 operands) against autograd through the
-    fp32 CPU restatement, at the AMP tolerance (the operands carry fp16 rounding)."""
+    """Gradients of an fp16 block (round 4: the fp16 MFMA gradient kernels, window gradients as fp16 hi/lo pairs)
+    against autograd through the fp32 CPU restatement, at the AMP tolerance (the operands carry fp16 rounding)."""
     import dvccorr
     H, W, D, C, L, r = 8, 12, 10, 32, 3, 3
     f1, f2 = prng.normal(801, (1, C, H, W, D)), prng.normal(802, (1, C, H, W, D))
@@ -140,5 +144,106 @@ def test_fp16_backward():
     t2 = torch.from_numpy(f2).to(DEV).requires_grad_(True)
     out = dvccorr.CorrBlock(t1, t2, L, r, precision="fp16")(torch.from_numpy(coords).to(DEV))
     (out * torch.from_numpy(G).to(DEV)).sum().backward()
+    e1, e2 = orc.rel_err(t1.grad.cpu().numpy(), ref1), orc.rel_err(t2.grad.cpu().numpy(), ref2)
+    assert e1 <= AMP_TOL and e2 <= AMP_TOL, (e1, e2)
+
+
+# ---- the on-the-fly block in fp16 (round 4): the reference's CorrBlockOnTheFly under autocast runs its einsum in
+# fp16 (corr_otf.py:198-237); k_fused_box / k_fused_proj take fp16 operands on v_mfma_f32_16x16x32_f16 and round
+# the window dots to fp16 exactly as the fp16 build rounds its pyramid.
+
+
+@pytest.mark.parametrize("shape,C,L,r", [((9, 7, 20), 32, 2, 4), ((16, 12, 40), 64, 3, 3), ((8, 8, 24), 128, 2, 2),
+                                         ((12, 10, 17), 32, 2, 1)])
+def test_fp16_fused_matches_materialised(shape, C, L, r):
+    """The fp16 on-the-fly kernels reproduce the fp16 materialised pyramid + lookup bit for bit (box kernel
+    variants 2, 3, 4; variant 1, the bf16-only tile kernel, falls back to the default box), ragged boxes, NaN /
+    huge coordinates, both conventions (legacy W != D levels: per-output kernel, AMP tolerance)."""
+    import dvccorr
+    from dvccorr import _lib
+    H, W, D = shape
+    g = torch.Generator(device="cpu").manual_seed(H * 1000 + W * 10 + D + r + C + 16)
+    f1 = torch.randn(1, C, H, W, D, generator=g).to(DEV)
+    f2 = torch.randn(1, C, H, W, D, generator=g).to(DEV)
+    base = dvccorr.coords_grid_3d(1, H, W, D, torch.device("cpu"))
+    c = base + (torch.rand(1, 3, H, W, D, generator=g) * 2 - 1) * (r + 4)
+    c.view(3, -1)[:, 5] = float("nan")
+    c.view(3, -1)[1, 17] = 1e30
+    c = c.to(DEV)
+    lay = dvccorr.layout(H, W, D, L, C)
+    n3 = (2 * r + 1) ** 3
+    with torch.no_grad():
+        for legacy in (False, True):
+            ref = dvccorr.CorrBlock(f1, f2, L, r, legacy_wd_swap=legacy, precision="fp16")(c)
+            fz = dvccorr.CorrBlockFused(f1, f2, L, r, legacy_wd_swap=legacy, precision="fp16")
+            assert fz.precision == "fp16"
+            try:
+                _lib.set_tuning("fused_variant", 0)
+                two_stage = fz(c)
+                for variant in (1, 2, 3, 4):
+                    _lib.set_tuning("fused_variant", variant)
+                    out = fz(c)
+                    assert torch.isfinite(out).all(), variant
+                    for l, (h, w, d) in enumerate(lay.levels()):
+                        sl = slice(l * n3, (l + 1) * n3)
+                        if legacy and w != d and min(h, w, d) > 1:
+                            assert orc.rel_err(out[:, sl].cpu().numpy(), ref[:, sl].cpu().numpy()) <= AMP_TOL
+                        else:
+                            assert torch.equal(out[:, sl], ref[:, sl]), (variant, shape, l, legacy)
+                    assert orc.rel_err(out.cpu().numpy(), two_stage.cpu().numpy()) <= AMP_TOL, variant
+            finally:
+                _lib.set_tuning("fused_variant", 2)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_fp16_fused_against_reference_amp(case):
+    """The on-the-fly block in fp16 against the reference's own AMP output (tests/golden/amp_*.npz) at 5e-3."""
+    import dvccorr
+    g, f1, f2, coords, L, r, legacy = amp_case(case)
+    t1, t2, tc = (torch.from_numpy(a).to(DEV) for a in (f1, f2, coords))
+    with torch.no_grad():
+        with torch.amp.autocast("cuda"):
+            blk = dvccorr.CorrBlockFused(t1, t2, L, r, legacy_wd_swap=legacy)
+            out = blk(tc)
+    assert blk.precision == "fp16" and out.dtype == torch.float32
+    e = _compare(out.cpu().numpy(), g)
+    assert e <= AMP_TOL, (case, e)
+
+
+@pytest.mark.parametrize("name", ["proj_888_L2_r4", "proj_888_L2_r4_legacy", "proj_978_L3_r3", "proj_888_L4_r1"])
+def test_fp16_fused_convc1(name):
+    """convc1 fused into the fp16 on-the-fly lookup (k_fused_proj with fp16 dots): against the reference's
+    CorrBlock + MotionEncoder.convc1 + ReLU (tests/golden/proj_*.npz) at 1e-2, and within 1e-5 of the fp16
+    materialised block's fused convc1 (same dots, same fp16 X operands, sorted query order)."""
+    import dvccorr
+    g = load_golden(name + ".npz")
+    f1, f2, coords, w, b, L, r, legacy = proj_inputs(g)
+    t = lambda a: torch.from_numpy(a).to(DEV)
+    with torch.no_grad():
+        fz = dvccorr.CorrBlockFused(t(f1), t(f2), L, r, legacy_wd_swap=legacy, precision="fp16")
+        out = fz.lookup_convc1(t(coords), t(w), t(b))
+        mat = dvccorr.CorrBlock(t(f1), t(f2), L, r, legacy_wd_swap=legacy, precision="fp16").lookup_convc1(
+            t(coords), t(w), t(b))
+    assert orc.rel_err(out.cpu().numpy(), g["out"]) <= 1e-2
+    assert orc.rel_err(out.cpu().numpy(), mat.cpu().numpy()) <= 1e-5
+
+
+def test_fp16_fused_backward():
+    """Gradients of the fp16 on-the-fly block (dvc_corr_backward over its fp16 packed operands, MFMA path)
+    against autograd through the fp32 CPU restatement at the AMP tolerance."""
+    import dvccorr
+    H, W, D, C, L, r = 10, 8, 12, 64, 3, 4
+    f1, f2 = prng.normal(811, (1, C, H, W, D)), prng.normal(812, (1, C, H, W, D))
+    coords = prng.flow_coords(813, 1, H, W, D, 2.5)
+    G = prng.normal(814, (1, L * (2 * r + 1) ** 3, H, W, D))
+    ref1, ref2 = oracle_grads(f1, f2, coords, G, L, r, False)
+    t1 = torch.from_numpy(f1).to(DEV).requires_grad_(True)
+    t2 = torch.from_numpy(f2).to(DEV).requires_grad_(True)
+    with torch.amp.autocast("cuda"):
+        blk = dvccorr.CorrBlockFused(t1, t2, L, r)
+        out = blk(torch.from_numpy(coords).to(DEV))
+        loss = (out * torch.from_numpy(G).to(DEV)).sum()
+    assert blk.precision == "fp16"
+    loss.backward()
     e1, e2 = orc.rel_err(t1.grad.cpu().numpy(), ref1), orc.rel_err(t2.grad.cpu().numpy(), ref2)
     assert e1 <= AMP_TOL and e2 <= AMP_TOL, (e1, e2)
