@@ -62,7 +62,9 @@ def parse(argv=None):
     ap.add_argument("--levels", type=int, default=4)
     ap.add_argument("--radius", type=int, default=4)
     ap.add_argument("--iters", type=int, default=12)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"],
+                    help="pyramid / operand precision: bf16 (BASELINE config #3), fp16 (the reference Trainer's AMP), "
+                         "fp32 (exact)")
     ap.add_argument("--impl", default="materialised", choices=["materialised", "fused"])
     ap.add_argument("--max-flow", type=float, default=2.0)
     ap.add_argument("--flow", default="random", choices=["random", "smooth"],
@@ -416,7 +418,8 @@ def main():
     nq_total = S * S * S * (1 if strong else world) if not shard_diag else nq_local
     lay = dvccorr.layout(S, S, S, L, C)
     dims = lay.levels()
-    store_bytes = 2 if args.precision == "bf16" else 4
+    sixteen = args.precision in ("bf16", "fp16")
+    store_bytes = 2 if sixteen else 4
     stream = torch.cuda.current_stream(dev)
     group = None if (strong and dist) else LOCAL
 
@@ -476,10 +479,10 @@ def main():
             kname = {"fused": "k_lookup_tile<PROJ> (dvc_corr_lookup_proj, convc1 fused)",
                      "unfused": "k_lookup_tile (dvc_corr_lookup) + torch conv/relu (timed together)"}.get(
                          args.convc1, "k_lookup_tile (dvc_corr_lookup)")
-        elif args.convc1 == "fused" and args.precision == "bf16" and 1 <= R <= 4:
+        elif args.convc1 == "fused" and sixteen and 1 <= R <= 4:
             kname = ("k_otf_keys + radix sort + k_fused_proj + k_rows_to_channels "
                      "(dvc_corr_lookup_fused_proj, convc1 fused, timed together)")
-        elif args.precision == "bf16" and 1 <= R <= 4:
+        elif sixteen and 1 <= R <= 4:
             kname = "k_fused_box (dvc_corr_lookup_fused)"
         else:
             kname = "k_fused_dots + k_lookup_win (dvc_corr_lookup_fused)"
@@ -490,7 +493,7 @@ def main():
         if args.impl == "fused":
             # the reference OTF dot count 2 C (2r+1)^3 L per voxel-query, against the dtype's MFMA peak
             fl = 2.0 * C * (2 * R + 1) ** 3 * L * nq_local
-            peak = BF16_PEAK_TFS if args.precision == "bf16" else F32_PEAK_TFS
+            peak = BF16_PEAK_TFS if sixteen else F32_PEAK_TFS   # (fp16 MFMA: the bf16 rate)
             if args.convc1 == "fused":   # + convc1: 2 x 96 x L (2r+1)^3 per voxel-query
                 fl += 2.0 * 96 * (2 * R + 1) ** 3 * L * nq_local
             roof["mfma"] = {"achieved": round(fl / (lk_avg * 1e-3) / 1e12, 1), "peak": peak, "unit": "TFLOP/s",
@@ -518,7 +521,7 @@ def main():
                             "algorithmic_bytes_per_launch": bd_bytes},
                     "lookup": lk}
         else:
-            roof = {"kernel": "build (pack + k_build_bf16_2b)", "bound": "hbm", "achieved": round(gbs, 1),
+            roof = {"kernel": f"build (pack + k_build_bf16_2b, {args.precision})", "bound": "hbm", "achieved": round(gbs, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
                     "algorithmic_bytes_per_launch": bd_bytes, "avg_launch_ms": round(bd_avg, 4),
                     "mfma": {"achieved": round(tfs, 1), "peak": BF16_PEAK_TFS,
@@ -557,7 +560,7 @@ def main():
             "value": value, "unit": "voxel-queries/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
             "scaling": "strong" if strong else "weak", "vs_baseline": None,
-            "dtype": "bf16" if args.precision == "bf16" else "f32",
+            "dtype": {"bf16": "bf16", "fp16": "f16"}.get(args.precision, "f32"),
             "data": (f"synthetic: N(0,1) feature maps, coords = identity + "
                      + (f"U(-{args.max_flow:g},{args.max_flow:g}) i.i.d. per voxel" if args.flow == "random" else
                         f"a smooth field (3 sinusoids per axis, |flow| <= {args.max_flow:g})")

@@ -186,18 +186,13 @@ template <int FMT> __device__ __forceinline__ unsigned gw_pair(float g) {
     else return bf16_hilo(g);
 }
 
-// Round 4 (the round-3 column-split patch): the output gradients arrive through buffer loads (the (b, l) block's
-// plane as a descriptor, the lane's query as the vector offset, the channel as a scalar one; per-lane 64-bit
-// addresses for the channels took the kernel's registers), and the window is produced in two passes over its
-// column halves [J0, J1), each holding only output columns [U0, U1] of the two rows in flight (2 x 5 x n floats at
-// r = 4, was 2 x n x n): two waves per SIMD instead of one.  The column shared by the halves is loaded twice.
-// (r = 6 keeps one wave per SIMD: its two rows of 2 x 7 x 13 floats would spill at 256 VGPRs.)
-// DVC_WG_SPLIT=0 (A/B builds, tools/build_variant.sh): one pass over all columns at one wave per SIMD.
-#ifndef DVC_WG_SPLIT
-#define DVC_WG_SPLIT 1
-#endif
+// Round 4: the output gradients arrive through buffer loads (the (b, l) block's plane as a descriptor, the lane's
+// query as the vector offset, the channel as a scalar one) instead of per-lane 64-bit addresses: 330 -> 292 us at
+// config #3.  The round-3 column-split patch (two passes over the window's column halves, half the rows in
+// registers, two waves per SIMD) was measured and dropped: 426 us (gpurun_out/r4c_bwd_*, rocprof) -- the
+// shared column loaded twice and the second pass's re-derived weights cost more than the occupancy bought.
 template <int R, int FMT>
-__global__ __launch_bounds__(256, (R <= 5 && DVC_WG_SPLIT) ? 2 : 1) void k_win_grad(BwdArgs A) {
+__global__ __launch_bounds__(256) void k_win_grad(BwdArgs A) {
     constexpr int n = 2 * R + 1, NW = 2 * R + 2, NW3 = NW * NW * NW;
     const int lane = threadIdx.x & 63;
     const long long nqb = (A.Nq + 63) / 64;
@@ -311,12 +306,7 @@ __global__ __launch_bounds__(256, (R <= 5 && DVC_WG_SPLIT) ? 2 : 1) void k_win_g
             plane(i + 1, rowB, rowA);
         }
     };
-    if constexpr (DVC_WG_SPLIT) {
-        pass(std::integral_constant<int, 0>{}, std::integral_constant<int, NW / 2>{});
-        pass(std::integral_constant<int, NW / 2>{}, std::integral_constant<int, NW>{});
-    } else {
-        pass(std::integral_constant<int, 0>{}, std::integral_constant<int, NW>{});
-    }
+    pass(std::integral_constant<int, 0>{}, std::integral_constant<int, NW>{});
 }
 
 // Generic (legacy W != D) levels: lane = query; the window box is zeroed, then every output's
@@ -535,8 +525,18 @@ __global__ __launch_bounds__(256) void k_grad_q(const TT *__restrict__ Tt, float
 // 16-byte halves of channel c swapped when (c >> 3) & 1 (the dQ kernel's bank-conflict-free B reads).  A batch's
 // target operand is then one contiguous 4 KB LDS-DMA (the channel-major rows of round 2 cost one 128-byte line
 // per 32 bytes used, and the dQ kernel was bound by that L2 traffic).
-__global__ __launch_bounds__(256) void k_tile_targets(const bf16_t *__restrict__ Tt, bf16_t *__restrict__ Tz, BwdArgs A) {
-    __shared__ __attribute__((aligned(16))) bf16_t tile[16][128 + 8];
+// fp32 operands (TT = float, round 4): the tile is written twice, bf16(T) into Tz and bf16(T - bf16(T)) into Tz + lo
+// (elements), so the MFMA kernels take T as a hi/lo pair too (the fp32 block's gradient sums on the matrix cores).
+__device__ __forceinline__ void split_bf16(float v, bf16_t &hi, bf16_t &lo) {
+    const __bf16 h = (__bf16)v;
+    hi = __builtin_bit_cast(bf16_t, h);
+    lo = __builtin_bit_cast(bf16_t, (__bf16)(v - (float)h));
+}
+template <typename TT>
+__global__ __launch_bounds__(256) void k_tile_targets(const TT *__restrict__ Tt, bf16_t *__restrict__ Tz, BwdArgs A,
+                                                      long long lo) {
+    constexpr bool SPLIT = std::is_same<TT, float>::value;
+    __shared__ __attribute__((aligned(16))) bf16_t tile[SPLIT ? 2 : 1][16][128 + 8];
     const long long t = blockIdx.x;
     const int g = blockIdx.y, b = blockIdx.z, ng = gridDim.y;
     int l = 0;
@@ -546,20 +546,38 @@ __global__ __launch_bounds__(256) void k_tile_targets(const bf16_t *__restrict__
     const long long row = local / kb;
     const int z0 = 8 * (int)(local - row * kb);
     const int cb = 128 * g, cg = min(128, A.Cp - cb);
-    const bf16_t *src = Tt + ((long long)b * A.row_stride + A.off[l] + row * A.Dp[l]) * A.Cp + cb;
+    const TT *src = Tt + ((long long)b * A.row_stride + A.off[l] + row * A.Dp[l]) * A.Cp + cb;
     {
         const int z = threadIdx.x >> 4, ch = threadIdx.x & 15;   // 16 z x 16 chunks of 8 channels
-        u32x4 v = {0u, 0u, 0u, 0u};
-        if (z0 + z < A.Dp[l] && 8 * ch < cg) v = *reinterpret_cast<const u32x4 *>(src + (long long)(z0 + z) * A.Cp + 8 * ch);
-        *reinterpret_cast<u32x4 *>(&tile[z][8 * ch]) = v;
+        const bool in = z0 + z < A.Dp[l] && 8 * ch < cg;
+        if constexpr (SPLIT) {
+            f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = v0;
+            if (in) {
+                v0 = *reinterpret_cast<const f32x4 *>(src + (long long)(z0 + z) * A.Cp + 8 * ch);
+                v1 = *reinterpret_cast<const f32x4 *>(src + (long long)(z0 + z) * A.Cp + 8 * ch + 4);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                split_bf16(v0[i], tile[0][z][8 * ch + i], tile[1][z][8 * ch + i]);
+                split_bf16(v1[i], tile[0][z][8 * ch + 4 + i], tile[1][z][8 * ch + 4 + i]);
+            }
+        } else {
+            u32x4 v = {0u, 0u, 0u, 0u};
+            if (in) v = *reinterpret_cast<const u32x4 *>(src + (long long)(z0 + z) * A.Cp + 8 * ch);
+            *reinterpret_cast<u32x4 *>(&tile[0][z][8 * ch]) = v;
+        }
     }
     __syncthreads();
     const int c = threadIdx.x >> 1, hh = threadIdx.x & 1;   // channel, logical z half
-    unsigned w[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = (unsigned)tile[8 * hh + 2 * i][c] | ((unsigned)tile[8 * hh + 2 * i + 1][c] << 16);
     bf16_t *dst = Tz + (((long long)b * ng + g) * A.tz0[A.L] + t) * 2048 + c * 16 + 8 * (hh ^ ((c >> 3) & 1));
-    *reinterpret_cast<u32x4 *>(dst) = u32x4{w[0], w[1], w[2], w[3]};
+#pragma unroll
+    for (int s = 0; s < (SPLIT ? 2 : 1); ++s) {
+        unsigned w[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            w[i] = (unsigned)tile[s][8 * hh + 2 * i][c] | ((unsigned)tile[s][8 * hh + 2 * i + 1][c] << 16);
+        *reinterpret_cast<u32x4 *>(dst + s * lo) = u32x4{w[0], w[1], w[2], w[3]};
+    }
 }
 
 // Round 3: the workgroup's four waves split the CHANNELS (wave w = channel tile w of 32), so a wave accumulates
@@ -625,10 +643,14 @@ __device__ __forceinline__ bf16x8 dup_bf16x4(u32x2 v) {
     return __builtin_bit_cast(bf16x8, r);
 }
 
-template <int NCT, bool F16>   // channel tiles of 32 (C_pad / 32, <= 4 per launch); fp16 operands
-__global__ __launch_bounds__(256, 4) void k_grad_q_mfma(const bf16_t *__restrict__ Tz, float *__restrict__ dQp,
-                                                        long long part_stride, BwdArgs A) {
-    constexpr int STAGE = 8192;                      // bytes: T tile (4 KB, bf16) + G tile (4 KB, hi/lo pairs)
+// SPLIT (fp32 blocks, round 4): the targets as bf16 hi/lo tiles (k_tile_targets<float>, the lo tiles tz_lo elements
+// after the hi ones); every batch stages both and runs the MFMAs on each, so dQ = sum (G_hi + G_lo) (T_hi + T_lo):
+// every product of the 16-bit pieces, ~2^-17 of each operand left out (the fp32 tolerance, 1e-5, holds with room).
+template <int NCT, bool F16, bool SPLIT = false>   // channel tiles of 32 (C_pad / 32, <= 4 per launch); fp16 operands
+__global__ __launch_bounds__(256, SPLIT ? 3 : 4) void k_grad_q_mfma(const bf16_t *__restrict__ Tz, float *__restrict__ dQp,
+                                                        long long part_stride, BwdArgs A, long long tz_lo) {
+    // bytes per stage: T tile (4 KB, 16-bit) + G tile (4 KB, hi/lo pairs) [+ T lo tile (4 KB)]
+    constexpr int STAGE = SPLIT ? 12288 : 8192;
     __shared__ __attribute__((aligned(16))) unsigned char stg[kQStages * STAGE];
     __shared__ unsigned qrows[kQRows + 2];           // batches (y | x << 11 | z0 << 22), count, next row
     const int tid = threadIdx.x, lane = tid & 63, m = lane & 31, h = lane >> 5;
@@ -656,6 +678,8 @@ __global__ __launch_bounds__(256, 4) void k_grad_q_mfma(const bf16_t *__restrict
     const long long ntz = A.tz0[A.L];
     const u32x4 rs_t = sgpr_rsrc(Tz + (((long long)b * ((A.Cp + 127) / 128) + A.cbase / 128) * ntz) * 2048,
                                  (unsigned)min(ntz * 4096, 0x7fffffffLL));
+    const u32x4 rs_tl = sgpr_rsrc(Tz + tz_lo + (((long long)b * ((A.Cp + 127) / 128) + A.cbase / 128) * ntz) * 2048,
+                                  (unsigned)min(ntz * 4096, 0x7fffffffLL));
     const unsigned tvo = 16u * (unsigned)tid;
     // G DMA role, instruction k: query gq = 16 w + 4 k + lane / 16, physical dword lane & 15 of its 64-byte row =
     // logical z 4 ((lane >> 2 & 3) ^ (gq >> 2 & 3)) + (lane & 3)
@@ -707,8 +731,11 @@ __global__ __launch_bounds__(256, 4) void k_grad_q_mfma(const bf16_t *__restrict
             const unsigned e = __builtin_amdgcn_readfirstlane(qrows[it]);
             const int y = (int)(e & 2047u), x = (int)((e >> 11) & 2047u), z0 = (int)(e >> 22);
             const unsigned sb = sbase + st * STAGE;
-            if (!(DVC_GQ_ABL & 4))   // (the batch's row: a scalar offset)
-                blds(rs_t, tvo, (unsigned)((tzl + (long long)(y * Wl + x) * kbl + (z0 >> 3)) * 4096), sb + 1024 * w, W16{});
+            if (!(DVC_GQ_ABL & 4)) {   // (the batch's row: a scalar offset)
+                const unsigned toff = (unsigned)((tzl + (long long)(y * Wl + x) * kbl + (z0 >> 3)) * 4096);
+                blds(rs_t, tvo, toff, sb + 1024 * w, W16{});
+                if constexpr (SPLIT) blds(rs_tl, tvo, toff, sb + 8192 + 1024 * w, W16{});
+            }
 #pragma unroll
             for (int k = 0; k < 4 && !(DVC_GQ_ABL & 2); ++k) {
                 const int wy = y - goh[k], wx = x - gou[k], wz = z0 - gov[k];
@@ -749,7 +776,7 @@ __global__ __launch_bounds__(256, 4) void k_grad_q_mfma(const bf16_t *__restrict
             for (int it = 0; it < nit; ++it) {
                 // batch it has landed (this thread's DMAs; kQStages - 2 newer batches may fly), then every thread's
                 // has, and every wave is done with batch it - 1, whose stage the next DMA refills
-                constexpr int kDma = ((DVC_GQ_ABL & 4) ? 0 : 1) + ((DVC_GQ_ABL & 2) ? 0 : 4);   // DMAs per batch
+                constexpr int kDma = ((DVC_GQ_ABL & 4) ? 0 : (SPLIT ? 2 : 1)) + ((DVC_GQ_ABL & 2) ? 0 : 4);   // DMAs per batch
                 asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kDma * (kQStages - 2)) : "memory");
                 __builtin_amdgcn_s_barrier();
                 asm volatile("" ::: "memory");
@@ -762,12 +789,16 @@ __global__ __launch_bounds__(256, 4) void k_grad_q_mfma(const bf16_t *__restrict
                         // B: this lane's 4 targets z = 8 j + 4 h .. + 3 of channel r, each twice
                         const u32x2 tv = *reinterpret_cast<const u32x2 *>(sb + r * 32 + 16 * (j ^ rsw) + 8 * h);
                         const bf16x8 bt = dup_bf16x4(tv);
+                        bf16x8 btl = bt;
+                        if constexpr (SPLIT)
+                            btl = dup_bf16x4(*reinterpret_cast<const u32x2 *>(sb + 8192 + r * 32 + 16 * (j ^ rsw) + 8 * h));
 #pragma unroll
                         for (int T = 0; T < 2; ++T) {
                             const int gq = 32 * T + m, sw = (gq >> 2) & 3;
                             const bf16x8 ag =
                                 *reinterpret_cast<const bf16x8 *>(sb + 4096 + gq * 64 + 16 * ((2 * j + h) ^ sw));
                             acc[T] = mma32<F16>(ag, bt, acc[T]);
+                            if constexpr (SPLIT) acc[T] = mma32<F16>(ag, btl, acc[T]);
                         }
                     }
                 }
@@ -985,28 +1016,48 @@ __global__ __launch_bounds__(256) void k_grad_t(const TT *__restrict__ Qp, const
 // positions from every 8-aligned start, [128 ch][16] bf16 = 4 KB (the halves of channel c swapped when
 // (c >> 3) & 1), so a batch's B operand is one contiguous tile.
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_qt_tiles(const bf16_t *__restrict__ Q, const unsigned long long *__restrict__ keys,
-                                                  bf16_t *__restrict__ Qz, long long Nq, long long nkeys, int Cp, int b) {
-    __shared__ __attribute__((aligned(16))) bf16_t tile[16][128 + 8];
+// fp32 queries (TT = float): hi tiles into Qz, lo tiles into Qz + lo (elements), as k_tile_targets<float>
+template <typename TT>
+__global__ __launch_bounds__(256) void k_qt_tiles(const TT *__restrict__ Q, const unsigned long long *__restrict__ keys,
+                                                  bf16_t *__restrict__ Qz, long long Nq, long long nkeys, int Cp, int b,
+                                                  long long lo) {
+    constexpr bool SPLIT = std::is_same<TT, float>::value;
+    __shared__ __attribute__((aligned(16))) bf16_t tile[SPLIT ? 2 : 1][16][128 + 8];
     const long long t = blockIdx.x, ntq = gridDim.x;
     const int g = blockIdx.y, cb = 128 * g, cg = min(128, Cp - cb);
     {
         const int r = threadIdx.x >> 4, ch = threadIdx.x & 15;   // 16 sorted positions x 16 chunks of 8 channels
         const long long i = 8 * t + r;
-        u32x4 v = {0u, 0u, 0u, 0u};
-        if (i < nkeys && 8 * ch < cg) {
-            const long long q = (long long)(keys[i] & 0xffffffffull);
-            v = *reinterpret_cast<const u32x4 *>(Q + ((long long)b * Nq + q) * Cp + cb + 8 * ch);
+        const bool in = i < nkeys && 8 * ch < cg;
+        const TT *row = Q + ((long long)b * Nq + (in ? (long long)(keys[i] & 0xffffffffull) : 0)) * Cp + cb + 8 * ch;
+        if constexpr (SPLIT) {
+            f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = v0;
+            if (in) {
+                v0 = *reinterpret_cast<const f32x4 *>(row);
+                v1 = *reinterpret_cast<const f32x4 *>(row + 4);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                split_bf16(v0[k], tile[0][r][8 * ch + k], tile[1][r][8 * ch + k]);
+                split_bf16(v1[k], tile[0][r][8 * ch + 4 + k], tile[1][r][8 * ch + 4 + k]);
+            }
+        } else {
+            u32x4 v = {0u, 0u, 0u, 0u};
+            if (in) v = *reinterpret_cast<const u32x4 *>(row);
+            *reinterpret_cast<u32x4 *>(&tile[0][r][8 * ch]) = v;
         }
-        *reinterpret_cast<u32x4 *>(&tile[r][8 * ch]) = v;
     }
     __syncthreads();
     const int c = threadIdx.x >> 1, hh = threadIdx.x & 1;
-    unsigned w[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = (unsigned)tile[8 * hh + 2 * i][c] | ((unsigned)tile[8 * hh + 2 * i + 1][c] << 16);
     bf16_t *dst = Qz + ((long long)g * ntq + t) * 2048 + c * 16 + 8 * (hh ^ ((c >> 3) & 1));
-    *reinterpret_cast<u32x4 *>(dst) = u32x4{w[0], w[1], w[2], w[3]};
+#pragma unroll
+    for (int s = 0; s < (SPLIT ? 2 : 1); ++s) {
+        unsigned w[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            w[i] = (unsigned)tile[s][8 * hh + 2 * i][c] | ((unsigned)tile[s][8 * hh + 2 * i + 1][c] << 16);
+        *reinterpret_cast<u32x4 *>(dst + s * lo) = u32x4{w[0], w[1], w[2], w[3]};
+    }
 }
 
 // Round 3: as k_grad_q_mfma, the four waves split the channels (wave w = channel tile w: dT[64 targets][32 ch]
@@ -1017,15 +1068,18 @@ __global__ __launch_bounds__(256) void k_qt_tiles(const bf16_t *__restrict__ Q, 
 // 16-byte load (the round-2 layout of this loop gathered 4-byte values from 64 windows per instruction and
 // was bound by that L2 traffic).  The 64-query chunks of the brick's origin rows are dealt to the workgroups of
 // the brick (splits).
-template <int NCT, bool F16>   // channel tiles of 32 (C_pad / 32, <= 4 per launch); fp16 operands
+// SPLIT (fp32 blocks): the query tiles as bf16 hi/lo (k_qt_tiles<float>, lo tiles qz_lo elements on), both staged
+// per batch and both multiplied (as k_grad_q_mfma<.., SPLIT>)
+template <int NCT, bool F16, bool SPLIT = false>   // channel tiles of 32 (C_pad / 32, <= 4 per launch); fp16 operands
 __global__ __launch_bounds__(256, 4) void k_grad_t_mfma(const bf16_t *__restrict__ Qz, long long ntq,
                                                         const unsigned long long *__restrict__ keys,
                                                         const int *__restrict__ starts, float *__restrict__ dT,
-                                                        float *__restrict__ dTp, BwdArgs A, int b) {
+                                                        float *__restrict__ dTp, BwdArgs A, int b, long long qz_lo) {
     const GtBlock gb = gt_block(A);
     const int l = gb.l, nsplit = gb.nsplit, split = gb.split, brick = gb.brick;
     starts += A.coff[l];
     __shared__ __attribute__((aligned(16))) bf16_t Ql[2][2048];     // [buf] query tile [128 ch][16] (swizzled)
+    __shared__ __attribute__((aligned(16))) bf16_t Qll[SPLIT ? 2 : 1][SPLIT ? 2048 : 8];   // [buf] its lo tile
     __shared__ __attribute__((aligned(16))) unsigned Gq[2][64][16];  // [buf][target][query] hi/lo pairs (swizzled)
     const int tid = threadIdx.x, lane = tid & 63, m = lane & 31, h = lane >> 5;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1075,10 +1129,11 @@ __global__ __launch_bounds__(256, 4) void k_grad_t_mfma(const bf16_t *__restrict
             const int qq_l = (int)(unsigned)(key & 0xffffffffu);
             const int oz_l = (int)((long long)(key >> 32) - cbase);
             const int p0 = base & ~7;   // batches of 16 sorted positions from 8-aligned starts
-            u32x4 qreg, gv;
+            u32x4 qreg, qregl, gv;
             auto load = [&](int kb) {
                 const int p = p0 + 16 * kb;
                 __builtin_memcpy(&qreg, qz + (long long)(p >> 3) * 2048, 16);
+                if constexpr (SPLIT) __builtin_memcpy(&qregl, qz + qz_lo + (long long)(p >> 3) * 2048, 16);
                 const int idx = p + sj - base;
                 const bool in = (unsigned)idx < (unsigned)nk;
                 const int qq = __shfl(qq_l, in ? idx : 0);
@@ -1093,6 +1148,7 @@ __global__ __launch_bounds__(256, 4) void k_grad_t_mfma(const bf16_t *__restrict
             };
             auto store = [&](int bb) {
                 *reinterpret_cast<u32x4 *>(&Ql[bb][8 * tid]) = qreg;
+                if constexpr (SPLIT) *reinterpret_cast<u32x4 *>(&Qll[bb][8 * tid]) = qregl;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {   // target 4 sr + k, query sj: chunk (sj / 4) ^ (row >> 2 & 3)
                     const int tr = 4 * sr + k;
@@ -1114,11 +1170,16 @@ __global__ __launch_bounds__(256, 4) void k_grad_t_mfma(const bf16_t *__restrict
                         const u32x2 qv = *reinterpret_cast<const u32x2 *>(
                             reinterpret_cast<const unsigned char *>(Ql[buf]) + r * 32 + 16 * (j ^ rsw) + 8 * h);
                         const bf16x8 bq = dup_bf16x4(qv);
+                        bf16x8 bql = bq;
+                        if constexpr (SPLIT)
+                            bql = dup_bf16x4(*reinterpret_cast<const u32x2 *>(
+                                reinterpret_cast<const unsigned char *>(Qll[buf]) + r * 32 + 16 * (j ^ rsw) + 8 * h));
 #pragma unroll
                         for (int T = 0; T < 2; ++T) {
                             const int tr = 32 * T + m;
                             const bf16x8 ag = *reinterpret_cast<const bf16x8 *>(&Gq[buf][tr][4 * ((2 * j + h) ^ ((tr >> 2) & 3))]);
                             acc[T] = mma32<F16>(ag, bq, acc[T]);
+                            if constexpr (SPLIT) acc[T] = mma32<F16>(ag, bql, acc[T]);
                         }
                     }
                 }
@@ -1320,14 +1381,16 @@ static void bwd_plan(int B, long long Nq, const dvc_layout &lay, int radius, boo
     P.temp = al256(tb);
     P.part = al256(std::max<size_t>(part, 256));
     P.ntq = (nkeys + 7) / 8 + 1;
-    P.qt = al256((size_t)P.ntq * ((lay.c_pad + 127) / 128) * 4096);   // bf16 path only (sized always)
+    // the MFMA path's query / target tiles, sized always (the workspace query has no dtype): twice, for the fp32
+    // blocks' hi and lo tiles
+    P.qt = al256(2 * (size_t)P.ntq * ((lay.c_pad + 127) / 128) * 4096);
     long long nt = 0;
     for (int l = 0; l < L; ++l) {
         P.tz0[l] = nt;
         nt += (long long)lay.H[l] * lay.W[l] * (lay.Dp[l] / 8);
     }
     P.tz0[L] = nt;
-    P.ttr = al256((size_t)B * ((lay.c_pad + 127) / 128) * nt * 4096);   // bf16 path only (sized always)
+    P.ttr = al256(2 * (size_t)B * ((lay.c_pad + 127) / 128) * nt * 4096);
     P.total = P.gwin + P.dq + P.dt + 2 * P.keys + P.starts + P.temp + P.part + P.qt + P.ttr;
 }
 
@@ -1353,9 +1416,14 @@ static bool mfma_offsets_fit(const BwdArgs &A, const BwdPlan &P) {
     return true;
 }
 
-// dtype codes of the packed operands whose gradient sums can run on the matrix cores (the rest: VALU)
+// fp32 blocks on the matrix cores (operands split into bf16 hi/lo pairs; round 4) -- 0 keeps them on the fp32 VALU
+// kernels (tuning "bwd_f32_mfma", thread-local like every dvc_set_tuning knob)
+static thread_local int g_bwd_f32_mfma = 1;
+void set_backward_f32_mfma(int v) { g_bwd_f32_mfma = v; }
+
+// dtype codes of the packed operands whose gradient sums run on the matrix cores (the rest: VALU)
 int backward_uses_mfma(int B, long long Nq, const dvc_layout &lay, int radius, int convention, int dtype) {
-    if (dtype != DVC_BF16 && dtype != DVC_F16) return 0;
+    if (dtype != DVC_BF16 && dtype != DVC_F16 && !(dtype == DVC_F32 && g_bwd_f32_mfma)) return 0;
     BwdPlan P;
     bwd_plan(B, Nq, lay, radius, convention == DVC_LEGACY, P);
     BwdArgs A{};
@@ -1392,11 +1460,15 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     };
     const long long nqb = (A.Nq + 63) / 64;
     const int ngroups = (A.Cp + 127) / 128;   // 128-channel groups: one launch of each gradient kernel per group
-    // Matrix-core path for 16-bit operands (bf16; fp16 = the AMP pyramid) whenever its LDS-DMA buffer offsets fit
-    // 32 bits (mfma_offsets_fit); otherwise, and for fp32 blocks, the VALU gradient kernels (64-bit addressing)
-    constexpr bool k16 = !std::is_same<TT, float>::value;
+    // Matrix-core path whenever its LDS-DMA buffer offsets fit 32 bits (mfma_offsets_fit): 16-bit operands (bf16;
+    // fp16 = the AMP pyramid) as they are, fp32 operands split into bf16 hi/lo tiles (SPLIT); otherwise the VALU
+    // gradient kernels (64-bit addressing)
+    constexpr bool k16 = true;   // (every operand type has a matrix-core path)
     constexpr bool F16 = std::is_same<TT, f16_t>::value;
-    const bool mfma = k16 && mfma_offsets_fit(A, P);
+    constexpr bool SPLIT = std::is_same<TT, float>::value;
+    const bool mfma = (!SPLIT || g_bwd_f32_mfma) && mfma_offsets_fit(A, P);
+    const long long tz_lo = (long long)A.B * ngroups * P.tz0[A.L] * 2048;   // lo tiles: elements after the hi ones
+    const long long qz_lo = (long long)P.ntq * ngroups * 2048;
     const int fmt = mfma ? (F16 ? kGwF16 : kGwBf16) : kGwF32;
     const unsigned wgrid = (unsigned)((A.B * A.L * nqb + 3) / 4);
     switch (fmt) {
@@ -1423,18 +1495,22 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     if constexpr (k16) {
         if (mfma) {
             for (int l = 0; l <= A.L; ++l) A.tz0[l] = P.tz0[l];
-            k_tile_targets<<<dim3((unsigned)P.tz0[A.L], (unsigned)ngroups, (unsigned)A.B), 256, 0, s>>>(
-                reinterpret_cast<const bf16_t *>(Tt), ttr, A);
+            if constexpr (SPLIT)
+                k_tile_targets<float><<<dim3((unsigned)P.tz0[A.L], (unsigned)ngroups, (unsigned)A.B), 256, 0, s>>>(
+                    Tt, ttr, A, tz_lo);
+            else
+                k_tile_targets<bf16_t><<<dim3((unsigned)P.tz0[A.L], (unsigned)ngroups, (unsigned)A.B), 256, 0, s>>>(
+                    reinterpret_cast<const bf16_t *>(Tt), ttr, A, 0);
             if (!launched("tile_targets")) return DVC_ERR_LAUNCH;
             const dim3 qg((unsigned)boxes, (unsigned)qparts);   // level groups: {0}, {1 .. L-1}
             for (int g = 0; g < ngroups; ++g) {
                 BwdArgs Ag = A;
                 Ag.cbase = 128 * g;
                 switch (std::min(128, A.Cp - Ag.cbase) / 32) {
-                case 1: k_grad_q_mfma<1, F16><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag); break;
-                case 2: k_grad_q_mfma<2, F16><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag); break;
-                case 3: k_grad_q_mfma<3, F16><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag); break;
-                default: k_grad_q_mfma<4, F16><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag); break;
+                case 1: k_grad_q_mfma<1, F16, SPLIT><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo); break;
+                case 2: k_grad_q_mfma<2, F16, SPLIT><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo); break;
+                case 3: k_grad_q_mfma<3, F16, SPLIT><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo); break;
+                default: k_grad_q_mfma<4, F16, SPLIT><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo); break;
                 }
             }
             done_q = true;
@@ -1485,17 +1561,21 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
         if constexpr (k16) {
             if (mfma) {
                 // matrix-core path: sorted + transposed query rows, then 16-query MFMA batches
-                k_qt_tiles<<<dim3((unsigned)P.ntq, (unsigned)ngroups), 256, 0, s>>>(
-                    reinterpret_cast<const bf16_t *>(Q), kout, qt, A.Nq, nkeys, A.Cp, b);
+                if constexpr (SPLIT)
+                    k_qt_tiles<float><<<dim3((unsigned)P.ntq, (unsigned)ngroups), 256, 0, s>>>(
+                        Q, kout, qt, A.Nq, nkeys, A.Cp, b, qz_lo);
+                else
+                    k_qt_tiles<bf16_t><<<dim3((unsigned)P.ntq, (unsigned)ngroups), 256, 0, s>>>(
+                        reinterpret_cast<const bf16_t *>(Q), kout, qt, A.Nq, nkeys, A.Cp, b, 0);
                 if (!launched("qt_tiles")) return DVC_ERR_LAUNCH;
                 for (int cg = 0; cg < ngroups; ++cg) {
                     BwdArgs Ag = A;
                     Ag.cbase = 128 * cg;
                     switch (std::min(128, A.Cp - Ag.cbase) / 32) {
-                    case 1: k_grad_t_mfma<1, F16><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b); break;
-                    case 2: k_grad_t_mfma<2, F16><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b); break;
-                    case 3: k_grad_t_mfma<3, F16><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b); break;
-                    default: k_grad_t_mfma<4, F16><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b); break;
+                    case 1: k_grad_t_mfma<1, F16, SPLIT><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b, qz_lo); break;
+                    case 2: k_grad_t_mfma<2, F16, SPLIT><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b, qz_lo); break;
+                    case 3: k_grad_t_mfma<3, F16, SPLIT><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b, qz_lo); break;
+                    default: k_grad_t_mfma<4, F16, SPLIT><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b, qz_lo); break;
                     }
                 }
                 done_t = true;

@@ -221,10 +221,18 @@ __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__re
                 pl.bx = blk - pl.by * nx;
             }
             Pos pe = pl;   // position of the next epilogue
+            // Every iteration issues its loads, past the wave's last block with an out-of-range offset (zeros, no
+            // memory traffic): loads under a branch leave hipcc's waitcnt pass unsure how many younger loads
+            // are in flight at the MFMAs, and it then waits for ALL of them (vmcnt(3..0) before each block's
+            // MFMAs, draining the other operand set's prefetch; round 4, ISA of k_fused_box).  With the loads
+            // unconditional the counts are exact and one whole block of loads stays in flight under the MFMAs.
+            int nload = 0;   // loads issued so far
             auto load_a = [&](bf16x8 (&dst)[KS]) {
                 const int z0 = zs + 16 * pl.zb;
                 const long long rowbase = offl + ((long long)(ys + pl.by) * Wl + (xs + pl.bx)) * Dpl;
-                const int off = z0 + m16 <= ze ? (int)(((rowbase + z0 + m16) * Cp + 8 * h4) * 2) : 0x7fff0000;
+                const int off = nload < nit && z0 + m16 <= ze ? (int)(((rowbase + z0 + m16) * Cp + 8 * h4) * 2)
+                                                              : 0x7fff0000;
+                ++nload;
                 advance(pl);
                 if constexpr ((ABL & 4) != 0) {   // diagnostics: no target loads
 #pragma unroll
@@ -272,24 +280,19 @@ __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__re
             // epilogue of iteration k
             bf16x8 a0[KS], a1[KS];
             f32x4 c0[4], c1[4];
-            if (nit > 0) load_a(a0);
-            if (nit > 1) load_a(a1);
-            if (nit > 0) {
+            if (nit > 0) {   // (the loop inside the branch: its entry sees exactly these loads in flight)
+                load_a(a0);
+                load_a(a1);
+                __builtin_amdgcn_sched_barrier(0);   // (keep a1's loads older than a0's next ones)
                 mfma(a0, c0);
-                if (nit > 2) load_a(a0);
-            }
-            for (int k = 0; k < nit; k += 2) {
-                if (k + 1 < nit) {
-                    mfma(a1, c1);
-                    if (k + 3 < nit) load_a(a1);
-                }
-                epilogue(c0);
-                if (k + 1 < nit) {
-                    if (k + 2 < nit) {
-                        mfma(a0, c0);
-                        if (k + 4 < nit) load_a(a0);
-                    }
-                    epilogue(c1);
+                load_a(a0);
+                for (int k = 0; k < nit; k += 2) {
+                    mfma(a1, c1);    // (past the last block: dots of zeros, never written)
+                    load_a(a1);
+                    epilogue(c0);
+                    mfma(a0, c0);
+                    load_a(a0);
+                    if (k + 1 < nit) epilogue(c1);   // (LDS writes only: the branch leaves the load counts exact)
                 }
             }
         }

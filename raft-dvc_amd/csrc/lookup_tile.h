@@ -270,11 +270,11 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
         }
     };
     stamp(0);
-    // zero the LDS once: guards and strip padding are read (with zero weight) and must be finite
-    for (int i = tid * 16; i < C::LDS; i += C::THREADS * 16) *reinterpret_cast<u32x4 *>(smem + i) = u32x4{0, 0, 0, 0};
-
+    // the coordinates first (the workgroup's first dependent memory round trip), the LDS clear under it
     float cy = 0.f, cx = 0.f, cz = 0.f;
     if (active) load_coords(A.coords, b, Nq, q, cy, cx, cz);
+    // zero the LDS once: guards and strip padding are read (with zero weight) and must be finite
+    for (int i = tid * 16; i < C::LDS; i += C::THREADS * 16) *reinterpret_cast<u32x4 *>(smem + i) = u32x4{0, 0, 0, 0};
 
     // the tile's rows as one buffer: offsets past its valid rows (or negative) read 0
     const T *tile_rows = reinterpret_cast<const T *>(A.corr) + ((long long)b * Nq + A.q0 + qt) * A.row_stride;

@@ -134,15 +134,15 @@ def test_backward_validation_without_gpu():
     assert nws_wd >= 256 * (11 * 22 * 7) * 4
     # workspace: window gradients (B*L*Nq*(2r+2)^3 x 4 bytes) + two partial dQ + dT + every level's keys + cell
     # starts + sort scratch + the MFMA path's query and target tiles (4 KB per 8-aligned start: twice the bf16
-    # rows) -- ~177 MB above the window gradients at #3
+    # rows; twice again for the fp32 blocks' hi and lo tiles, round 4) -- ~265 MB above the window gradients at #3
     nws = L.dvc_corr_backward_workspace_bytes(1, 32768, 128, 32, 32, 32, 4, 4)
-    assert nws >= 4 * 32768 * 1000 * 4 and nws < 4 * 32768 * 1000 * 4 + 200 * 2 ** 20
+    assert nws >= 4 * 32768 * 1000 * 4 and nws < 4 * 32768 * 1000 * 4 + 300 * 2 ** 20
 
 
 def test_backward_path_selection_without_gpu():
-    """Which gradient kernels dvc_corr_backward runs (pure host): 16-bit operands (bf16, and fp16 = the AMP pyramid)
-    on the matrix cores while k_grad_q_mfma's 32-bit buffer offsets cover the volume; fp32 operands, and volumes
-    past that range (a 160^3 level-0 fmap: 160 * 160 * 20 target tiles of 4 KB per (batch, channel group) exceed
+    """Which gradient kernels dvc_corr_backward runs (pure host): every operand dtype (bf16, fp16 = the AMP pyramid,
+    fp32 as bf16 hi/lo pairs) on the matrix cores while k_grad_q_mfma's 32-bit buffer offsets cover the volume;
+    volumes past that range (a 160^3 level-0 fmap: 160 * 160 * 20 target tiles of 4 KB per (batch, channel group) exceed
     2^31 bytes), on the 64-bit-addressed VALU kernels -- never a descriptor read past its range."""
     from dvccorr import _lib
     L = _lib.lib()
@@ -152,7 +152,13 @@ def test_backward_path_selection_without_gpu():
         assert L.dvc_corr_backward_mfma(1, 160 ** 3, 128, 160, 160, 160, 4, 4, 0, dt) == 0
         assert L.dvc_corr_backward_mfma(1, 128 * 128 * 256, 128, 128, 128, 256, 4, 4, 0, dt) == 0
         assert L.dvc_corr_backward_mfma(1, 64 ** 3, 128, 64, 64, 64, 4, 4, 0, dt) == 1   # config #4's fmaps
-    assert L.dvc_corr_backward_mfma(1, 32768, 128, 32, 32, 32, 4, 4, 0, _lib.DVC_F32) == 0
+    # fp32 operands (round 4): split into bf16 hi/lo tiles on the same kernels; tuning "bwd_f32_mfma" 0 = VALU
+    assert L.dvc_corr_backward_mfma(1, 32768, 128, 32, 32, 32, 4, 4, 0, _lib.DVC_F32) == 1
+    assert L.dvc_set_tuning(b"bwd_f32_mfma", 0) == 0
+    try:
+        assert L.dvc_corr_backward_mfma(1, 32768, 128, 32, 32, 32, 4, 4, 0, _lib.DVC_F32) == 0
+    finally:
+        L.dvc_set_tuning(b"bwd_f32_mfma", 1)
     assert L.dvc_corr_backward_mfma(1, 32768, 128, 32, 32, 32, 4, 9, 0, _lib.DVC_BF16) == 0   # radius outside 1..6
 
 
