@@ -1416,14 +1416,15 @@ static bool mfma_offsets_fit(const BwdArgs &A, const BwdPlan &P) {
     return true;
 }
 
-// fp32 blocks on the matrix cores (operands split into bf16 hi/lo pairs; round 4) -- 0 keeps them on the fp32 VALU
-// kernels (tuning "bwd_f32_mfma", thread-local like every dvc_set_tuning knob)
-static thread_local int g_bwd_f32_mfma = 1;
-void set_backward_f32_mfma(int v) { g_bwd_f32_mfma = v; }
+// 1: the gradient sums on the matrix cores wherever the offsets fit (fp32 operands split into bf16 hi/lo pairs,
+// round 4); 0: the VALU kernels for every dtype -- the large-volume fallback, kept testable at any size (tuning
+// "bwd_mfma", thread-local like every dvc_set_tuning knob)
+static thread_local int g_bwd_mfma = 1;
+void set_backward_mfma(int v) { g_bwd_mfma = v; }
 
 // dtype codes of the packed operands whose gradient sums run on the matrix cores (the rest: VALU)
 int backward_uses_mfma(int B, long long Nq, const dvc_layout &lay, int radius, int convention, int dtype) {
-    if (dtype != DVC_BF16 && dtype != DVC_F16 && !(dtype == DVC_F32 && g_bwd_f32_mfma)) return 0;
+    if (!g_bwd_mfma || (dtype != DVC_BF16 && dtype != DVC_F16 && dtype != DVC_F32)) return 0;
     BwdPlan P;
     bwd_plan(B, Nq, lay, radius, convention == DVC_LEGACY, P);
     BwdArgs A{};
@@ -1466,7 +1467,7 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     constexpr bool k16 = true;   // (every operand type has a matrix-core path)
     constexpr bool F16 = std::is_same<TT, f16_t>::value;
     constexpr bool SPLIT = std::is_same<TT, float>::value;
-    const bool mfma = (!SPLIT || g_bwd_f32_mfma) && mfma_offsets_fit(A, P);
+    const bool mfma = g_bwd_mfma && mfma_offsets_fit(A, P);
     const long long tz_lo = (long long)A.B * ngroups * P.tz0[A.L] * 2048;   // lo tiles: elements after the hi ones
     const long long qz_lo = (long long)P.ntq * ngroups * 2048;
     const int fmt = mfma ? (F16 ? kGwF16 : kGwBf16) : kGwF32;

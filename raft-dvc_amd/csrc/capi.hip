@@ -61,7 +61,7 @@ int corr_backward(const void *packed_q, const void *packed_t, const float *coord
                   size_t errlen);
 size_t backward_workspace_bytes(int B, long long Nq, const dvc_layout &lay, int radius);
 int backward_uses_mfma(int B, long long Nq, const dvc_layout &lay, int radius, int convention, int dtype);
-void set_backward_f32_mfma(int v);
+void set_backward_mfma(int v);
 __global__ void k_coords_grid(float *, long long, int, int, int);
 template <bool DELTA, bool SUBGRID, int VEC, bool STAGED>
 __global__ void k_upflow(const float *, const float *, float *, float *, long long, int, int, int, int, int, int, int,
@@ -354,9 +354,9 @@ int dvc_set_tuning(const char *key, int value) {
         g_build_f32_variant = value;
         return DVC_OK;
     }
-    if (!strcmp(key, "bwd_f32_mfma")) {   // 1 = fp32 blocks' gradient sums on the matrix cores (default), 0 = VALU
-        if (value < 0 || value > 1) return fail(DVC_ERR_INVALID, "set_tuning: bwd_f32_mfma %d", value);
-        set_backward_f32_mfma(value);
+    if (!strcmp(key, "bwd_mfma")) {   // 1 = gradient sums on the matrix cores (default), 0 = the VALU kernels
+        if (value < 0 || value > 1) return fail(DVC_ERR_INVALID, "set_tuning: bwd_mfma %d", value);
+        set_backward_mfma(value);
         return DVC_OK;
     }
     if (!strcmp(key, "build_wgs")) {

@@ -41,11 +41,25 @@ namespace dvc {
 // Staged chunks are 16 bytes for 16-bit pyramids and 8 bytes for fp32 ones (round 3): a run of 2r+2 fp32
 // values then spans at most 2r+4 staged values instead of 2r+8, so the fp32 plane strips shrink from
 // 41.5 KB to 31 KB and two workgroups fit a CU (one did before: 83 KB of LDS).
+// Round 4 A/B (build-time, DVC_TILE_CB16=8 DVC_TILE_PD16=3): 16-bit pyramids staging 8-byte chunks (strips of
+// 328 instead of 488 bytes, 20 instead of 32 VGPRs per plane) with THREE planes in flight in registers, a plane
+// loaded ~3 output rows before its LDS write (the workgroup timelines, tools/trace_lookup.py, show rows 0-6
+// waiting ~1 us each on their plane, rows 7-8 with nothing to wait for at 0.9 us).  Bitwise equal, and slower:
+// config #3 154.4 vs 146.6 us median, one rank's 8-way slab step 0.39 vs 0.372 ms (gpurun_out/r4f, alternating
+// processes): the extra load and LDS-write instructions cost more than the deeper prefetch returned.  The
+// product keeps 16-byte chunks and two planes in flight.
+#ifndef DVC_TILE_CB16
+#define DVC_TILE_CB16 16
+#endif
+#ifndef DVC_TILE_PD16
+#define DVC_TILE_PD16 2
+#endif
 template <typename T, int R, int NWV = 0> struct TileCfg {
     static constexpr int n = 2 * R + 1;
     static constexpr int NW = 2 * R + 2;                        // window planes / columns / run length
     static constexpr int ES = (int)sizeof(T);
-    static constexpr int CB = ES == 4 ? 8 : 16;                 // bytes per staged chunk
+    // bytes per staged chunk (16-bit radii 5-6 keep 16-byte chunks: their strips' register staging would spill)
+    static constexpr int CB = ES == 4 ? 8 : (R <= 4 ? DVC_TILE_CB16 : 16);
     static constexpr int CE = CB / ES;                          // elements per chunk
     static constexpr int ZWMAX = (NW + CE - 1 + CE - 1) / CE * CE;   // z-chunk span covering any run
     static constexpr int NWAVES = NWV > 0 ? NWV : (n + 2) / 3;
@@ -55,6 +69,9 @@ template <typename T, int R, int NWV = 0> struct TileCfg {
     static constexpr int SLOT = 64 * SQMAX;
     static constexpr int GUARD = 64;                            // >= NW*ES + 4 bytes either side
     static constexpr int MAXCH = (64 * NW * (ZWMAX / CE) + THREADS - 1) / THREADS;
+    // planes staged in registers (pipeline depth): three where the staging costs <= 64 VGPRs (16-bit pyramids,
+    // the four-wave r <= 4 instances: 10 chunks x 2 VGPRs), else two
+    static constexpr int PD = (ES == 2 && MAXCH * (CB / 4) * DVC_TILE_PD16 <= 64) ? DVC_TILE_PD16 : 2;
     static constexpr int LDS = GUARD + 2 * SLOT + GUARD;
     static_assert(SLOT / 8 < 0xffff, "chunk LDS offsets are packed as 16-bit multiples of 8 bytes");
     static_assert(SQMAX % 8 == 0, "strips must stay 8-byte aligned");
@@ -473,27 +490,31 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
             z.t = __builtin_fmaf(r[n], wv1[n - 1], r[n - 1] * wv0[n - 1]);
         };
 
-        // staged planes (relative index p = plane - a0): plane p + 2 is loaded into st[p & 1]
-        // two rows before it is written
+        // staged planes (relative index p = plane - a0) live in st[p % PD]: plane p is written to LDS at the end of
+        // row p - 2 (into the slot of plane p - 2, read by rows p - 3 and p - 2), and its register set then takes
+        // plane p + PD, loaded PD - 1 rows ahead of its own write
         constexpr int NPL = NA + 1;   // window planes this workgroup reads
-        Chunk st[2][C::MAXCH];
+        constexpr int PD = PROJ ? 2 : C::PD;   // (the convc1 consumer's 96 accumulators: keep the registers)
+        Chunk st[PD][C::MAXCH];
         ZRun<n> zp[NU + 1];       // z-lerped columns of the lower plane of the current row
-        load_plane(a0, st[0]);
-        load_plane(a0 + 1, st[1]);
+#pragma unroll
+        for (int p = 0; p < PD; ++p)
+            if (p < NPL) load_plane(a0 + p, st[p]);
         write_plane(0, a0, st[0]);
-        if (2 < NPL) load_plane(a0 + 2, st[0]);
+        if (PD < NPL) load_plane(a0 + PD, st[0]);
         stamp(3);
         __syncthreads();          // plane a0 in slot 0
         stamp(4);
 #pragma unroll
         for (int k = 0; k <= NU; ++k) lerp_col(0, k, zp[k]);
-        write_plane(1, a0 + 1, st[1]);
+        write_plane(1, a0 + 1, st[1 % PD]);
+        if (PD > 2 && PD + 1 < NPL) load_plane(a0 + PD + 1, st[1 % PD]);
         __syncthreads();          // plane a0 + 1 in slot 1
         stamp(5);
 #pragma unroll
         for (int ia = 0; ia < NA; ++ia) {
             const int a = a0 + ia;
-            if (ia + 3 < NPL) load_plane(a + 3, st[(ia + 1) & 1]);   // in flight for two rows
+            if (PD == 2 && ia + 3 < NPL) load_plane(a + 3, st[(ia + 1) & 1]);   // in flight for two rows
             float wy0, wy1;
             axis_weights(ax.ph, ax.kh, a - R, ax.hs, ax.hs, wy0, wy1);
             wy0 = (unsigned)(ih + a) < (unsigned)Hl ? wy0 : 0.0f;
@@ -572,7 +593,10 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
                 for (int j = 0; j < ProjCfg::KW / 8; ++j)
                     dst[j] = u32x4{xw[4 * j], xw[4 * j + 1], xw[4 * j + 2], xw[4 * j + 3]};
             }
-            if (ia + 2 < NPL) write_plane(ia & 1, a + 2, st[ia & 1]);   // plane a+2 into the slot of plane a (read in row a-1)
+            if (ia + 2 < NPL) {   // plane a+2 into the slot of plane a (read in row a-1)
+                write_plane(ia & 1, a + 2, st[(ia + 2) % PD]);
+                if (PD > 2 && ia + 2 + PD < NPL) load_plane(a + 2 + PD, st[(ia + 2) % PD]);
+            }
             __syncthreads();
             stamp(6 + ia);
         }

@@ -152,13 +152,14 @@ def test_backward_path_selection_without_gpu():
         assert L.dvc_corr_backward_mfma(1, 160 ** 3, 128, 160, 160, 160, 4, 4, 0, dt) == 0
         assert L.dvc_corr_backward_mfma(1, 128 * 128 * 256, 128, 128, 128, 256, 4, 4, 0, dt) == 0
         assert L.dvc_corr_backward_mfma(1, 64 ** 3, 128, 64, 64, 64, 4, 4, 0, dt) == 1   # config #4's fmaps
-    # fp32 operands (round 4): split into bf16 hi/lo tiles on the same kernels; tuning "bwd_f32_mfma" 0 = VALU
+    # fp32 operands (round 4): split into bf16 hi/lo tiles on the same kernels; tuning "bwd_mfma" 0 = VALU for all
     assert L.dvc_corr_backward_mfma(1, 32768, 128, 32, 32, 32, 4, 4, 0, _lib.DVC_F32) == 1
-    assert L.dvc_set_tuning(b"bwd_f32_mfma", 0) == 0
+    assert L.dvc_set_tuning(b"bwd_mfma", 0) == 0
     try:
-        assert L.dvc_corr_backward_mfma(1, 32768, 128, 32, 32, 32, 4, 4, 0, _lib.DVC_F32) == 0
+        for dt in (_lib.DVC_F32, _lib.DVC_BF16, _lib.DVC_F16):
+            assert L.dvc_corr_backward_mfma(1, 32768, 128, 32, 32, 32, 4, 4, 0, dt) == 0
     finally:
-        L.dvc_set_tuning(b"bwd_f32_mfma", 1)
+        L.dvc_set_tuning(b"bwd_mfma", 1)
     assert L.dvc_corr_backward_mfma(1, 32768, 128, 32, 32, 32, 4, 9, 0, _lib.DVC_BF16) == 0   # radius outside 1..6
 
 

@@ -241,3 +241,16 @@ def test_grad_cfg3_slab(precision, tol):
     e1 = orc.rel_err(d1[:, :, q0:q1], ref1[:, :, q0:q1])
     e2 = orc.rel_err(d2, ref2)
     assert e1 <= tol and e2 <= tol, (precision, e1, e2)
+
+
+@pytest.mark.parametrize("precision,tol", [("fp32", GRAD_TOL), ("bf16", BF16_TOL), ("fp16", FP16_TOL)])
+def test_grad_valu_fallback(precision, tol):
+    """The VALU gradient kernels (k_grad_q / k_grad_t, 64-bit addressing): the path dvc_corr_backward takes for
+    volumes past the matrix-core kernels' 31-bit buffer offsets (~154^3 level-0 fmaps and up, too large for a
+    test), forced here with tuning "bwd_mfma" 0 on the C = 128, L = 4, r = 4 golden vectors (grad_cfg2)."""
+    from dvccorr import _lib
+    _lib.set_tuning("bwd_mfma", 0)
+    try:
+        _check_golden("grad_cfg2", "gemm", precision, tol)
+    finally:
+        _lib.set_tuning("bwd_mfma", 1)
