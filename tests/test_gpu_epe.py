@@ -38,12 +38,14 @@ def _run(kind):
     if kind == "torch_gpu":      # the reference op sequence on the GPU: the floor of GPU arithmetic
         lookup = lambda c: torch_cpu.corr_lookup(f0, f1, c, 4, 4, False)     # noqa: E731
         tail = lambda c, dl: rl.reference_tail(c, dl, coords0, T)           # noqa: E731
-    elif kind in ("fp32", "bf16"):
+    elif kind in ("fp32", "bf16", "fp16"):
         lookup = dvccorr.CorrBlock(f0, f1, 4, 4, precision=kind)
-    elif kind in ("fused_fp32", "fused_bf16"):
+    elif kind in ("fused_fp32", "fused_bf16", "fused_fp16"):
         lookup = dvccorr.CorrBlockFused(f0, f1, 4, 4, precision=kind.split("_")[1])
-    elif kind == "bf16_convc1":
-        blk = dvccorr.CorrBlock(f0, f1, 4, 4, precision="bf16")
+    elif kind in ("bf16_convc1", "fp16_convc1", "fused_fp16_convc1"):
+        prec = "fp16" if "fp16" in kind else "bf16"
+        cls = dvccorr.CorrBlockFused if kind.startswith("fused") else dvccorr.CorrBlock
+        blk = cls(f0, f1, 4, 4, precision=prec)
         lookup = lambda c: blk.lookup_convc1(c, p["encoder.convc1.weight"], p["encoder.convc1.bias"])  # noqa
         convc1 = True
     with torch.no_grad():
@@ -52,7 +54,9 @@ def _run(kind):
     return rl.epe(flow_lo, g["flow_lo"]), flow_up
 
 
-@pytest.mark.parametrize("kind", ["torch_gpu", "fp32", "fused_fp32", "bf16", "fused_bf16", "bf16_convc1"])
+# fp16 (round 4): the reference Trainer's AMP precision on both blocks and the fused convc1 paths
+@pytest.mark.parametrize("kind", ["torch_gpu", "fp32", "fused_fp32", "bf16", "fused_bf16", "bf16_convc1", "fp16",
+                                  "fused_fp16", "fp16_convc1", "fused_fp16_convc1"])
 def test_final_flow_epe(kind):
     e, flow_up = _run(kind)
     print(f"EPE[{kind}] = {e:.3e} voxel")

@@ -1,5 +1,5 @@
 #!/bin/bash
-# The rocprofv3 --pmc recipes behind the round-3 profiles (profiles/r03/), one per name:
+# The rocprofv3 --pmc recipes behind the profiles (profiles/r03/, profiles/r04/), one per name:
 #   bash tools/pmc_recipes.sh r3e     (run on the GPU box from the repo root)
 # r3c: lookup SQ instruction / LDS counters; r3e: lookup read-request sizes (128-B lines) and L2; r3j: the small
 # launches (config #2 fp32 16^3); r3k: config #5 on-the-fly kernels (k_fused_box, convc1 path); r3m: #5 window-key
@@ -8,6 +8,9 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD
 case "${1:-}" in
+r4a)   # round 4: the headline lookup's HBM traffic (bench roofline.traffic) and its read-request sizes / LDS
+  cd $R && TAG=r4a VARIANT=2 EXTRA="--reps 2" PMC_GROUPS="FETCH_SIZE;WRITE_SIZE;TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_WRREQ_64B_sum;SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES" bash tools/pmc_groups.sh
+  ;;
 r3c)
   cd /tmp && timeout -s KILL 60 rocprofv3 -L > $R/gpurun_out/r3c_avail.txt 2>&1
   cd $R && TAG=r3c VARIANT=2 EXTRA="--reps 2" PMC_GROUPS="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_INST_LDS;SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES" bash tools/pmc_groups.sh

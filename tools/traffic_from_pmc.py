@@ -19,13 +19,11 @@ def pick(d, prefix):
 
 note = "HBM bytes per launch: 2 x FETCH_SIZE + WRITE_SIZE (KB x 1024), rocprofv3 --pmc, gfx950; source: {}"
 out = {}
-m = json.load(open(os.path.join(P, "r02_pmc_mat32_f.json")))
-m3 = json.load(open(os.path.join(P, "r03", "r03_pmc_mat32.json")))
+m4 = json.load(open(os.path.join(P, "r04", "r04_pmc_mat32.json")))
 out["materialised_bf16_32_L4_r4_n1"] = {
-    "build_hbm_bytes_per_launch": hbm(pick(m, "k_build_bf16_2b")),
-    "lookup_hbm_bytes_per_launch": hbm(pick(m3, "k_lookup_tile")),
-    "note": note.format("profiles/r03/r03_pmc_mat32.json (DVC_BRICKED level 0, round 3 lookup; build: "
-                        "profiles/r02_pmc_mat32_f.json)")}
+    "build_hbm_bytes_per_launch": hbm(pick(m4, "k_build_bf16_2b")),
+    "lookup_hbm_bytes_per_launch": hbm(pick(m4, "k_lookup_tile")),
+    "note": note.format("profiles/r04/r04_pmc_mat32.json (DVC_BRICKED level 0; tools/pmc_recipes.sh r4a)")}
 mp = json.load(open(os.path.join(P, "r02_pmc_mat32_convc1_f.json")))
 out["materialised_bf16_32_L4_r4_n1_convc1_fused"] = {
     "lookup_hbm_bytes_per_launch": hbm(pick(mp, "k_lookup_tile")),
