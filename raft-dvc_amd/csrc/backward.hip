@@ -191,25 +191,47 @@ template <int FMT> __device__ __forceinline__ unsigned gw_pair(float g) {
 // config #3.  The round-3 column-split patch (two passes over the window's column halves, half the rows in
 // registers, two waves per SIMD) was measured and dropped: 426 us (gpurun_out/r4c_bwd_*, rocprof) -- the
 // shared column loaded twice and the second pass's re-derived weights cost more than the occupancy bought.
+// Round 4, later: each window plane (NW x NW values per query, a contiguous 4 NW^2-byte piece of the query's window)
+// is staged in the wave's LDS image and leaves as 16-byte stores of consecutive pieces (a wave instruction writes
+// ~2.5 queries' planes, ~10 whole lines), instead of 8-byte stores 4 NW^3 bytes apart (64 lines per instruction:
+// 65 M partial-line writes at config #3); the next plane's output-gradient row is loaded before the flush.
+template <int R> struct WinGradCfg {
+    static constexpr int NW = 2 * R + 2;
+    static constexpr int SW = NW * NW + 4;                 // LDS image row (dwords) per query: 16-byte aligned
+    static constexpr int WAVES = R >= 6 ? 3 : 4;           // waves per workgroup (LDS: WAVES x 64 x SW x 4 bytes)
+    static constexpr int LDS = WAVES * 64 * SW * 4;
+};
 template <int R, int FMT>
-__global__ __launch_bounds__(256) void k_win_grad(BwdArgs A) {
-    constexpr int n = 2 * R + 1, NW = 2 * R + 2, NW3 = NW * NW * NW;
-    const int lane = threadIdx.x & 63;
+__global__ __launch_bounds__(64 * WinGradCfg<R>::WAVES) void k_win_grad(BwdArgs A) {
+    using G = WinGradCfg<R>;
+    constexpr int n = 2 * R + 1, NW = G::NW, NW3 = NW * NW * NW, SW = G::SW, P16 = NW * NW / 4;
+    extern __shared__ __attribute__((aligned(16))) float wg_stage[];
+    // (wave index through readfirstlane: the tile, level and descriptors below are then scalar -- per-lane
+    // descriptors would wrap every buffer access in a waterfall loop)
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const long long nqb = (A.Nq + 63) / 64;
-    const long long item = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const long long item = (long long)blockIdx.x * G::WAVES + wave;
     if (item >= (long long)A.B * A.L * nqb) return;
     const int bl = (int)(item / nqb);
     const int l = bl % A.L, b = bl / A.L;
-    const long long q = (item - (long long)bl * nqb) * 64 + lane;
-    if (q >= A.Nq || A.generic[l]) return;   // generic levels: k_win_grad_generic
+    const long long q0 = (item - (long long)bl * nqb) * 64;
+    const long long q = q0 + lane;
+    const int nvalid = (int)min(64LL, A.Nq - q0);
+    if (A.generic[l]) return;   // generic levels: k_win_grad_generic
     float *gw = A.gwin + A.goff[l] + ((long long)b * A.Nq + q) * NW3;
     if (A.zero[l]) {   // a size-1 level samples zeros (corr.py:41-44): no gradient reaches it
-        for (int i = 0; i < NW3; i += 2) *reinterpret_cast<f32x2 *>(gw + i) = f32x2{0.0f, 0.0f};
+        if (lane < nvalid)
+            for (int i = 0; i < NW3; i += 2) *reinterpret_cast<f32x2 *>(gw + i) = f32x2{0.0f, 0.0f};
         return;
     }
+    // this wave's query tile as one store descriptor (lanes past the tile's valid queries: out of range, dropped)
+    const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(
+        A.gwin + A.goff[l] + ((long long)b * A.Nq + q0) * NW3, (short)0, nvalid * NW3 * 4, 0x00020000);
+    float *img = wg_stage + wave * 64 * SW;   // [64 queries][SW], this wave's image of one window plane
+    const long long qc = q < A.Nq ? q : A.Nq - 1;   // (lanes past the end compute a copy of the last query)
     const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l];
     float cy, cx, cz;
-    load_coords(A.coords, b, A.Nq, q, cy, cx, cz);
+    load_coords(A.coords, b, A.Nq, qc, cy, cx, cz);
     WinAxes ax;
     bw_axes(A, l, cy, cx, cz, ax);
     const int ih = (int)ax.kh - R, iu = (int)ax.ku - R, iv = (int)ax.kv - R;
@@ -225,88 +247,107 @@ __global__ __launch_bounds__(256) void k_win_grad(BwdArgs A) {
     }
     const long long chu = A.legacy ? 1 : n, chv = A.legacy ? n : 1;
     const float *gbl = A.gout + (long long)bl * n * n * n * A.Nq;
-    const int q4 = (int)(q * 4), nq4 = (int)(A.Nq * 4);
+    const int q4 = (int)(qc * 4), nq4 = (int)(A.Nq * 4);
     // Window plane i collects output row a = i (corner 0) and a = i - 1 (corner 1); row i - 1 stays in registers
     // from the previous plane (ping-pong buffers)
-    auto pass = [&](auto j0c, auto j1c) {
-        constexpr int J0 = decltype(j0c)::value, J1 = decltype(j1c)::value;
-        constexpr int U0 = J0 > 0 ? J0 - 1 : 0, U1 = J1 - 1 < n - 1 ? J1 - 1 : n - 1, NU = U1 - U0 + 1;
-        float rowA[NU][n], rowB[NU][n];
+    float rowA[n][n], rowB[n][n];
+    // output row a of this lane's query; a = n (past the last row) reads zeros through an empty descriptor, so the
+    // loads are unconditional (under a branch the old register contents would stay live beside the new ones)
+    auto load_row = [&](int a, float (&dst)[n][n]) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(gbl + (long long)min(a, n - 1) * n * n * A.Nq), (short)0,
+            a < n ? (int)min((long long)n * n * nq4, 0x7fffffffLL) : 0, 0x00020000);
 #pragma unroll
-        for (int uu = 0; uu < NU; ++uu)
+        for (int uu = 0; uu < n; ++uu)
 #pragma unroll
-            for (int v = 0; v < n; ++v) rowB[uu][v] = 0.0f;
-        auto plane = [&](int i, float (&cur)[NU][n], const float (&prev)[NU][n]) {
-            float wa0 = 0.0f, wa1 = 0.0f, t0, t1;
-            if (i < n) {
-                axis_weights(ax.ph, ax.kh, i - R, ax.hs, ax.hs, t0, t1);
-                wa0 = (unsigned)(ih + i) < (unsigned)Hl ? t0 : 0.0f;
-                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(   // output row a = i
-                    (void *)(gbl + (long long)i * n * n * A.Nq), (short)0,
-                    (int)min((long long)n * n * nq4, 0x7fffffffLL), 0x00020000);
+            for (int v = 0; v < n; ++v)
+                dst[uu][v] = __builtin_bit_cast(
+                    float, __builtin_amdgcn_raw_buffer_load_b32(rs, q4, (int)((uu * chu + v * chv) * nq4), 0));
+    };
+    auto plane = [&](int i, const float (&cur)[n][n], float (&prev)[n][n]) {
+        float wa0 = 0.0f, wa1 = 0.0f, t0, t1;
+        if (i < n) {
+            axis_weights(ax.ph, ax.kh, i - R, ax.hs, ax.hs, t0, t1);
+            wa0 = (unsigned)(ih + i) < (unsigned)Hl ? t0 : 0.0f;
+        }
+        if (i >= 1) {
+            axis_weights(ax.ph, ax.kh, i - 1 - R, ax.hs, ax.hs, t0, t1);
+            wa1 = (unsigned)(ih + i) < (unsigned)Hl ? t1 : 0.0f;
+        }
+        float Pp[n];
 #pragma unroll
-                for (int uu = 0; uu < NU; ++uu)
+        for (int v = 0; v < n; ++v) Pp[v] = 0.0f;
 #pragma unroll
-                    for (int v = 0; v < n; ++v)
-                        cur[uu][v] = __builtin_bit_cast(
-                            float, __builtin_amdgcn_raw_buffer_load_b32(rs, q4, (int)(((U0 + uu) * chu + v * chv) * nq4), 0));
-            }
-            if (i >= 1) {
-                axis_weights(ax.ph, ax.kh, i - 1 - R, ax.hs, ax.hs, t0, t1);
-                wa1 = (unsigned)(ih + i) < (unsigned)Hl ? t1 : 0.0f;
-            }
-            float Pp[n];
+        for (int j = 0; j < NW; ++j) {
+            float Pc[n];
 #pragma unroll
-            for (int v = 0; v < n; ++v) Pp[v] = 0.0f;
+            for (int v = 0; v < n; ++v) Pc[v] = 0.0f;
+            if (j < n) {
+                const int uu = j < n ? j : 0;
+                if (i < n) {
 #pragma unroll
-            for (int j = U0; j < J1; ++j) {   // (j = J0 - 1 only primes Pp)
-                float Pc[n];
-#pragma unroll
-                for (int v = 0; v < n; ++v) Pc[v] = 0.0f;
-                if (j < n) {
-                    const int uu = j < n ? j - U0 : 0;
-                    if (i < n) {
-#pragma unroll
-                        for (int v = 0; v < n; ++v) Pc[v] = wa0 * cur[uu][v];
-                    }
-                    if (i >= 1) {
-#pragma unroll
-                        for (int v = 0; v < n; ++v) Pc[v] = __builtin_fmaf(wa1, prev[uu][v], Pc[v]);
-                    }
+                    for (int v = 0; v < n; ++v) Pc[v] = wa0 * cur[uu][v];
                 }
-                if (j >= J0) {
-                    const float wj0 = j < n ? wx0[j < n ? j : 0] : 0.0f;
-                    const float wj1 = j >= 1 ? wx1[j >= 1 ? j - 1 : 0] : 0.0f;
-                    float o[NW];
+                if (i >= 1) {
 #pragma unroll
-                    for (int k = 0; k < NW; ++k) o[k] = 0.0f;
-#pragma unroll
-                    for (int v = 0; v < n; ++v) {
-                        const float gz = __builtin_fmaf(wj0, Pc[v], wj1 * Pp[v]);
-                        o[v] = __builtin_fmaf(wz0[v], gz, o[v]);
-                        o[v + 1] = __builtin_fmaf(wz1[v], gz, o[v + 1]);
-                    }
-                    if constexpr (FMT != kGwF32) {
-                        u32x2 *dst = reinterpret_cast<u32x2 *>(gw + (i * NW + j) * NW);
-#pragma unroll
-                        for (int k = 0; k < NW / 2; ++k) dst[k] = u32x2{gw_pair<FMT>(o[2 * k]), gw_pair<FMT>(o[2 * k + 1])};
-                    } else {
-                        f32x2 *dst = reinterpret_cast<f32x2 *>(gw + (i * NW + j) * NW);
-#pragma unroll
-                        for (int k = 0; k < NW / 2; ++k) dst[k] = f32x2{o[2 * k], o[2 * k + 1]};
-                    }
+                    for (int v = 0; v < n; ++v) Pc[v] = __builtin_fmaf(wa1, prev[uu][v], Pc[v]);
                 }
-#pragma unroll
-                for (int v = 0; v < n; ++v) Pp[v] = Pc[v];
             }
-        };
-#pragma unroll 1
-        for (int i = 0; i < NW; i += 2) {   // NW is even
-            plane(i, rowA, rowB);
-            plane(i + 1, rowB, rowA);
+            const float wj0 = j < n ? wx0[j < n ? j : 0] : 0.0f;
+            const float wj1 = j >= 1 ? wx1[j >= 1 ? j - 1 : 0] : 0.0f;
+            float o[NW];
+#pragma unroll
+            for (int k = 0; k < NW; ++k) o[k] = 0.0f;
+#pragma unroll
+            for (int v = 0; v < n; ++v) {
+                const float gz = __builtin_fmaf(wj0, Pc[v], wj1 * Pp[v]);
+                o[v] = __builtin_fmaf(wz0[v], gz, o[v]);
+                o[v + 1] = __builtin_fmaf(wz1[v], gz, o[v + 1]);
+            }
+            u32x2 *dst = reinterpret_cast<u32x2 *>(img + lane * SW + j * NW);
+#pragma unroll
+            for (int k = 0; k < NW / 2; ++k) {
+                if constexpr (FMT != kGwF32) dst[k] = u32x2{gw_pair<FMT>(o[2 * k]), gw_pair<FMT>(o[2 * k + 1])};
+                else dst[k] = u32x2{__float_as_uint(o[2 * k]), __float_as_uint(o[2 * k + 1])};
+            }
+#pragma unroll
+            for (int v = 0; v < n; ++v) Pp[v] = Pc[v];
+        }
+        // row i - 1 is consumed: the next plane's row i + 1 goes into its registers before the flush's stores
+        // (the scheduling barrier keeps the loads below the last read of row i - 1: hoisted above the columns they
+        // would keep a third row of registers live)
+        __builtin_amdgcn_sched_barrier(0);
+        load_row(i + 1, prev);
+        // flush: piece c (16 bytes) of the tile's plane i = piece c % P16 of query c / P16 (the same wave wrote the
+        // image, so the LDS order of its own instructions covers the read-after-write)
+        // (in groups of FG pieces: the compiler would otherwise hoist every LDS read above the first store, 4 P16
+        // registers next to the two output-gradient rows)
+        constexpr int FG = 5;
+#pragma unroll
+        for (int g0 = 0; g0 < P16; g0 += FG) {
+            u32x4 v[FG];
+#pragma unroll
+            for (int u = 0; u < FG; ++u) {
+                const int c = (g0 + u) * 64 + lane;
+                const int qq = c / P16, pc = c - qq * P16;
+                if (g0 + u < P16) v[u] = *reinterpret_cast<const u32x4 *>(img + qq * SW + pc * 4);
+            }
+#pragma unroll
+            for (int u = 0; u < FG; ++u) {
+                const int c = (g0 + u) * 64 + lane;
+                const int qq = c / P16, pc = c - qq * P16;
+                if (g0 + u < P16)
+                    __builtin_amdgcn_raw_buffer_store_b128(v[u], rs_out, (qq * NW3 + i * NW * NW + pc * 4) * 4, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
         }
     };
-    pass(std::integral_constant<int, 0>{}, std::integral_constant<int, NW>{});
+    load_row(0, rowA);
+#pragma unroll 1
+    for (int i = 0; i < NW; i += 2) {   // NW is even
+        plane(i, rowA, rowB);
+        plane(i + 1, rowB, rowA);
+    }
 }
 
 // Generic (legacy W != D) levels: lane = query; the window box is zeroed, then every output's
@@ -593,7 +634,14 @@ __global__ __launch_bounds__(256) void k_tile_targets(const TT *__restrict__ Tt,
 // reads are free of bank conflicts.  Level groups (blockIdx.y) write separate partial dQ (level 0 alone, the
 // coarse levels together), summed in a fixed order by k_unpack_sum.
 constexpr int kQRows = 1024;   // batches listed at a time (a box's union at +-2 flows, r = 4: 17^2 rows x 2)
-constexpr int kQStages = 4;    // LDS stages of the batch pipeline (kQStages - 2 in flight across the barrier)
+#ifndef DVC_QSTAGES
+#define DVC_QSTAGES 4
+#endif
+constexpr int kQStages = DVC_QSTAGES;   // LDS stages of the batch pipeline (kQStages - 2 in flight across the barrier)
+// workgroups per CU the LDS allows (kQStages x 8 / 12 KB stages + the batch list, of 160 KB), the launch-bounds hint
+template <bool SPLIT> constexpr int kQOcc = (160 * 1024) / (kQStages * (SPLIT ? 12288 : 8192) + 4 * 1024 + 16) < 4
+                                                ? (160 * 1024) / (kQStages * (SPLIT ? 12288 : 8192) + 4 * 1024 + 16)
+                                                : 4;
 constexpr unsigned kOOB = 0x80000000u;   // a buffer offset past every range (reads 0)
 // diagnostics builds only (tools/build_variant.sh -DDVC_GQ_ABL=n): 1 no MFMAs, 2 no G DMAs, 4 no T DMAs
 #ifndef DVC_GQ_ABL
@@ -647,7 +695,7 @@ __device__ __forceinline__ bf16x8 dup_bf16x4(u32x2 v) {
 // after the hi ones); every batch stages both and runs the MFMAs on each, so dQ = sum (G_hi + G_lo) (T_hi + T_lo):
 // every product of the 16-bit pieces, ~2^-17 of each operand left out (the fp32 tolerance, 1e-5, holds with room).
 template <int NCT, bool F16, bool SPLIT = false>   // channel tiles of 32 (C_pad / 32, <= 4 per launch); fp16 operands
-__global__ __launch_bounds__(256, SPLIT ? 3 : 4) void k_grad_q_mfma(const bf16_t *__restrict__ Tz, float *__restrict__ dQp,
+__global__ __launch_bounds__(256, kQOcc<SPLIT>) void k_grad_q_mfma(const bf16_t *__restrict__ Tz, float *__restrict__ dQp,
                                                         long long part_stride, BwdArgs A, long long tz_lo) {
     // bytes per stage: T tile (4 KB, 16-bit) + G tile (4 KB, hi/lo pairs) [+ T lo tile (4 KB)]
     constexpr int STAGE = SPLIT ? 12288 : 8192;
@@ -1070,8 +1118,15 @@ __global__ __launch_bounds__(256) void k_qt_tiles(const TT *__restrict__ Q, cons
 // the brick (splits).
 // SPLIT (fp32 blocks): the query tiles as bf16 hi/lo (k_qt_tiles<float>, lo tiles qz_lo elements on), both staged
 // per batch and both multiplied (as k_grad_q_mfma<.., SPLIT>)
+// Round 4, later: the batches no longer wait one memory round trip each (one batch in flight per workgroup: at
+// config #3 ~260 K batches over 1024 workgroup slots, ~1.4 us apiece).  The chunks' batches are listed (kTCap at a
+// time, one entry per lane of every wave), their sorted keys resolved into an LDS table by one load per thread, and
+// the batches then stream through three register sets: batch i + 3's loads are issued while batch i is multiplied.
+// Every load is unconditional (out-of-window gradients read the zero guard before the window gradients), so
+// hipcc's counted waits name exactly the set about to be stored.
+constexpr int kTCap = 32;   // batches listed at a time
 template <int NCT, bool F16, bool SPLIT = false>   // channel tiles of 32 (C_pad / 32, <= 4 per launch); fp16 operands
-__global__ __launch_bounds__(256, 4) void k_grad_t_mfma(const bf16_t *__restrict__ Qz, long long ntq,
+__global__ __launch_bounds__(256, SPLIT ? 3 : 4) void k_grad_t_mfma(const bf16_t *__restrict__ Qz, long long ntq,
                                                         const unsigned long long *__restrict__ keys,
                                                         const int *__restrict__ starts, float *__restrict__ dT,
                                                         float *__restrict__ dTp, BwdArgs A, int b, long long qz_lo) {
@@ -1081,6 +1136,7 @@ __global__ __launch_bounds__(256, 4) void k_grad_t_mfma(const bf16_t *__restrict
     __shared__ __attribute__((aligned(16))) bf16_t Ql[2][2048];     // [buf] query tile [128 ch][16] (swizzled)
     __shared__ __attribute__((aligned(16))) bf16_t Qll[SPLIT ? 2 : 1][SPLIT ? 2048 : 8];   // [buf] its lo tile
     __shared__ __attribute__((aligned(16))) unsigned Gq[2][64][16];  // [buf][target][query] hi/lo pairs (swizzled)
+    __shared__ int tq[kTCap][16], tzr[kTCap][16];   // listed batch e, query j: query id (-1: none), origin z - oz0
     const int tid = threadIdx.x, lane = tid & 63, m = lane & 31, h = lane >> 5;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
@@ -1102,95 +1158,130 @@ __global__ __launch_bounds__(256, 4) void k_grad_t_mfma(const bf16_t *__restrict
     const int oz0 = bz * 4, oz1 = min(bz * 4 + 3, Dl - 1) + nv - 1;
     const int nox = ox1 - ox0 + 1, nrows = (oy1 - oy0 + 1) * nox;
     const unsigned *glp = reinterpret_cast<const unsigned *>(A.gwin + A.goff[l] + (long long)b * A.Nq * nw3);
+    const unsigned *gzero = reinterpret_cast<const unsigned *>(A.gwin) - 64;   // the zeroed guard
     const bf16_t *qz = Qz + (long long)(A.cbase / 128) * ntq * 2048 + 8 * tid;   // + tile * 2048: this thread's 16 B
     f32x16 acc[2];
 #pragma unroll
     for (int T = 0; T < 2; ++T)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[T][i] = 0.0f;
-    int buf = 0;
+    // listed batches, entry e in lane e of every wave: origin row, first sorted position, the chunk's [base, base + nk)
+    int e_row = 0, e_p = 0, e_base = 0, e_nk = 0;
+    int cnt = 0;
+    struct Set {
+        u32x4 q, ql, g;
+        unsigned mk;   // bit k: target z tz0 + k inside the query's window row and the level
+    };
+    auto load = [&](int i, int n, Set &S) __attribute__((always_inline)) {   // batch min(i, n - 1): every load unconditional
+        const int e = min(i, n - 1);
+        const int row = __builtin_amdgcn_readlane(e_row, e), p = __builtin_amdgcn_readlane(e_p, e);
+        __builtin_memcpy(&S.q, qz + (long long)(p >> 3) * 2048, 16);
+        if constexpr (SPLIT) __builtin_memcpy(&S.ql, qz + qz_lo + (long long)(p >> 3) * 2048, 16);
+        const int oy = oy0 + row / nox, ox = ox0 + row % nox;
+        // window position (y, x) of the staged brick row for a query of origin o' = (oy, ox, *)
+        const int py = ty - oy + nh - 1, px = tx - ox + nu - 1;
+        const bool yxok = rval && (unsigned)py < (unsigned)nh && (unsigned)px < (unsigned)nu;
+        const int qq = tq[e][sj];
+        const int pz0 = tz0 - tzr[e][sj] + nv - 1;
+        const bool ok = qq >= 0 && yxok && pz0 > -4 && pz0 < nv;
+        // (4 consecutive window z: one 16-byte load; values outside the window row are masked at the store)
+        const unsigned *src = ok ? glp + (long long)qq * nw3 + (py * nu + px) * nv + pz0 : gzero;
+        __builtin_memcpy(&S.g, src, 16);
+        unsigned mk = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) mk |= ((unsigned)(pz0 + k) < (unsigned)nv && tz0 + k < Dl) ? 1u << k : 0u;
+        S.mk = mk;
+    };
+    auto store = [&](int bb, const Set &S) __attribute__((always_inline)) {
+        *reinterpret_cast<u32x4 *>(&Ql[bb][8 * tid]) = S.q;
+        if constexpr (SPLIT) *reinterpret_cast<u32x4 *>(&Qll[bb][8 * tid]) = S.ql;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {   // target 4 sr + k, query sj: chunk (sj / 4) ^ (row >> 2 & 3)
+            const int tr = 4 * sr + k;
+            Gq[bb][tr][4 * ((sj >> 2) ^ ((tr >> 2) & 3)) + (sj & 3)] = (S.mk >> k) & 1u ? S.g[k] : 0u;
+        }
+    };
+    auto compute = [&](int bb) __attribute__((always_inline)) {
+        if (w >= NCT) return;
+        const int r = 32 * w + m, rsw = (r >> 3) & 1;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {   // queries 8 j .. 8 j + 7: K = 16 (query, hi/lo) pairs
+            const u32x2 qv = *reinterpret_cast<const u32x2 *>(
+                reinterpret_cast<const unsigned char *>(Ql[bb]) + r * 32 + 16 * (j ^ rsw) + 8 * h);
+            const bf16x8 bq = dup_bf16x4(qv);
+            bf16x8 bql = bq;
+            if constexpr (SPLIT)
+                bql = dup_bf16x4(*reinterpret_cast<const u32x2 *>(
+                    reinterpret_cast<const unsigned char *>(Qll[bb]) + r * 32 + 16 * (j ^ rsw) + 8 * h));
+#pragma unroll
+            for (int T = 0; T < 2; ++T) {
+                const int tr = 32 * T + m;
+                const bf16x8 ag = *reinterpret_cast<const bf16x8 *>(&Gq[bb][tr][4 * ((2 * j + h) ^ ((tr >> 2) & 3))]);
+                acc[T] = mma32<F16>(ag, bq, acc[T]);
+                if constexpr (SPLIT) acc[T] = mma32<F16>(ag, bql, acc[T]);
+            }
+        }
+    };
+    // the n listed batches: key table, then the three-set pipeline
+    auto process = [&](int n) __attribute__((always_inline)) {
+        __syncthreads();   // the previous list's table and tiles have been read
+        for (int e = tid >> 4; e < kTCap; e += 16) {   // (thread: entry e, query j = sj)
+            const int row = __shfl(e_row, e), p = __shfl(e_p, e), base = __shfl(e_base, e), nk = __shfl(e_nk, e);
+            const int idx = p + sj - base;
+            int qq = -1, zr = 0;
+            if (e < n && (unsigned)idx < (unsigned)nk) {
+                const unsigned long long key = keys[p + sj];
+                const long long cb = ((long long)(oy0 + row / nox) * CX + (ox0 + row % nox)) * CZ + A.coff[l];
+                qq = (int)(unsigned)(key & 0xffffffffu);
+                zr = (int)((long long)(key >> 32) - cb);   // origin z (global cells hold coff[l])
+            }
+            tq[e][sj] = qq;
+            tzr[e][sj] = zr;
+        }
+        __syncthreads();
+        Set S0, S1, S2;
+        load(0, n, S0);
+        load(1, n, S1);
+        load(2, n, S2);
+        auto step = [&](int i, Set &S) __attribute__((always_inline)) {
+            store(i & 1, S);
+            __syncthreads();   // batch i staged; every wave is done with batch i - 2 (same buffer)
+            load(i + 3, n, S);
+            if (i < n) compute(i & 1);
+        };
+        for (int i = 0; i < n; i += 3) {
+            step(i, S0);
+            step(i + 1, S1);
+            step(i + 2, S2);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the tail's clamped loads)
+    };
     // 64-query chunks of the brick's origin rows dealt round-robin to the nsplit workgroups of the brick (every
-    // wave of the workgroup walks the same chunks)
+    // wave of the workgroup walks the same chunks and lists the same batches)
     auto range = [&](int row, int &s, int &e) {
         const long long cb = ((long long)(oy0 + row / nox) * CX + (ox0 + row % nox)) * CZ;
         s = starts[cb + oz0];
         e = starts[cb + oz1 + 1];
     };
     deal_chunks(nrows, split, nsplit, lane, range, [&](int row, int s, int e, int c1) {
-        const int oy = oy0 + row / nox, ox = ox0 + row % nox;
-        const long long cbase = ((long long)oy * CX + ox) * CZ + A.coff[l];   // (keys hold global cells)
-        // window position (y, x) of the staged brick row for a query of origin o' = (oy, ox, *)
-        const int py = ty - oy + nh - 1, px = tx - ox + nu - 1;
-        const bool yxok = rval && (unsigned)py < (unsigned)nh && (unsigned)px < (unsigned)nu;
-        const int pyx = (py * nu + px) * nv;
         for (int base = s + 64 * c1; base < e; base += 64 * nsplit) {
             const int nk = min(64, e - base);
-            const unsigned long long key = lane < nk ? keys[base + lane] : 0ull;
-            const int qq_l = (int)(unsigned)(key & 0xffffffffu);
-            const int oz_l = (int)((long long)(key >> 32) - cbase);
             const int p0 = base & ~7;   // batches of 16 sorted positions from 8-aligned starts
-            u32x4 qreg, qregl, gv;
-            auto load = [&](int kb) {
-                const int p = p0 + 16 * kb;
-                __builtin_memcpy(&qreg, qz + (long long)(p >> 3) * 2048, 16);
-                if constexpr (SPLIT) __builtin_memcpy(&qregl, qz + qz_lo + (long long)(p >> 3) * 2048, 16);
-                const int idx = p + sj - base;
-                const bool in = (unsigned)idx < (unsigned)nk;
-                const int qq = __shfl(qq_l, in ? idx : 0);
-                const int pz0 = tz0 - __shfl(oz_l, in ? idx : 0) + nv - 1;
-                gv = u32x4{0u, 0u, 0u, 0u};
-                // (4 consecutive window z: one 16-byte load; values outside the window row are masked below, and
-                // the loads past either end of the gradient buffer fall in its 256-byte guards)
-                if (in && yxok && pz0 > -4 && pz0 < nv) __builtin_memcpy(&gv, glp + (long long)qq * nw3 + pyx + pz0, 16);
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (!((unsigned)(pz0 + k) < (unsigned)nv && tz0 + k < Dl)) gv[k] = 0u;
-            };
-            auto store = [&](int bb) {
-                *reinterpret_cast<u32x4 *>(&Ql[bb][8 * tid]) = qreg;
-                if constexpr (SPLIT) *reinterpret_cast<u32x4 *>(&Qll[bb][8 * tid]) = qregl;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {   // target 4 sr + k, query sj: chunk (sj / 4) ^ (row >> 2 & 3)
-                    const int tr = 4 * sr + k;
-                    Gq[bb][tr][4 * ((sj >> 2) ^ ((tr >> 2) & 3)) + (sj & 3)] = gv[k];
-                }
-            };
             const int nb = (base + nk - p0 + 15) >> 4;
-            load(0);
-            __syncthreads();   // the previous chunk's last batch has been read
-            store(buf);
-            __syncthreads();
-            for (int kb = 0; kb < nb; ++kb) {
-                const bool more = kb + 1 < nb;
-                if (more) load(kb + 1);
-                if (w < NCT) {
-                    const int r = 32 * w + m, rsw = (r >> 3) & 1;
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) {   // queries 8 j .. 8 j + 7: K = 16 (query, hi/lo) pairs
-                        const u32x2 qv = *reinterpret_cast<const u32x2 *>(
-                            reinterpret_cast<const unsigned char *>(Ql[buf]) + r * 32 + 16 * (j ^ rsw) + 8 * h);
-                        const bf16x8 bq = dup_bf16x4(qv);
-                        bf16x8 bql = bq;
-                        if constexpr (SPLIT)
-                            bql = dup_bf16x4(*reinterpret_cast<const u32x2 *>(
-                                reinterpret_cast<const unsigned char *>(Qll[buf]) + r * 32 + 16 * (j ^ rsw) + 8 * h));
-#pragma unroll
-                        for (int T = 0; T < 2; ++T) {
-                            const int tr = 32 * T + m;
-                            const bf16x8 ag = *reinterpret_cast<const bf16x8 *>(&Gq[buf][tr][4 * ((2 * j + h) ^ ((tr >> 2) & 3))]);
-                            acc[T] = mma32<F16>(ag, bq, acc[T]);
-                            if constexpr (SPLIT) acc[T] = mma32<F16>(ag, bql, acc[T]);
-                        }
-                    }
-                }
-                if (more) {
-                    store(buf ^ 1);
-                    __syncthreads();
-                    buf ^= 1;
-                }
+            if (cnt + nb > kTCap) {
+                process(cnt);
+                cnt = 0;
             }
+            if (lane >= cnt && lane < cnt + nb) {
+                e_row = row;
+                e_p = p0 + 16 * (lane - cnt);
+                e_base = base;
+                e_nk = nk;
+            }
+            cnt += nb;
         }
     });
+    if (cnt > 0) process(cnt);
     if (w >= NCT) return;
     // D layout (32x32 MFMA): acc[T][i] = D[target 32 T + 8 (i / 4) + 4 h + i % 4][channel 32 w + m]
     const float sc = A.scale;
@@ -1472,10 +1563,18 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     const long long qz_lo = (long long)P.ntq * ngroups * 2048;
     const int fmt = mfma ? (F16 ? kGwF16 : kGwBf16) : kGwF32;
     const unsigned wgrid = (unsigned)((A.B * A.L * nqb + 3) / 4);
-    switch (fmt) {
-    case kGwF16: k_win_grad<R, kGwF16><<<wgrid, 256, 0, s>>>(A); break;
-    case kGwBf16: k_win_grad<R, kGwBf16><<<wgrid, 256, 0, s>>>(A); break;
-    default: k_win_grad<R, kGwF32><<<wgrid, 256, 0, s>>>(A); break;
+    {
+        using WG = WinGradCfg<R>;
+        const unsigned wg_grid = (unsigned)((A.B * A.L * nqb + WG::WAVES - 1) / WG::WAVES);
+        auto launch_wg = [&](auto kern) {
+            (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, WG::LDS);
+            kern<<<wg_grid, 64 * WG::WAVES, WG::LDS, s>>>(A);
+        };
+        switch (fmt) {
+        case kGwF16: launch_wg(k_win_grad<R, kGwF16>); break;
+        case kGwBf16: launch_wg(k_win_grad<R, kGwBf16>); break;
+        default: launch_wg(k_win_grad<R, kGwF32>); break;
+        }
     }
     if (!launched("win_grad")) return DVC_ERR_LAUNCH;
     bool any_generic = false;

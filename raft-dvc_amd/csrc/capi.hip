@@ -579,9 +579,13 @@ int dvc_corr_build(const void *packed_q, const void *packed_t, void *corr, int B
     // column chunks per query tile: 8 (one per XCD: blocks b, b + 8, ... share an XCD and stream the same
     // eighth of the targets through its L2), doubled while the grid is short of 4 workgroups per CU (one
     // rank's slab: 32 query tiles at config #3 / 8 GPUs) and every chunk keeps >= 2 column tiles
+    // The exact-f32 kernel (k_build_f32r, two workgroups per CU) wants ONE round of workgroups: config #2 (16^3
+    // fp32, 64 query tiles) 94 -> 82 us per build with 512 instead of 1024 (gpurun_out/r4i); its target is half
+    // the 16-bit kernels'.
     const long long qtiles = ceil_div(Nq, in_dtype == DVC_F32 ? 64 : 128) * B;
+    const long long wgs = in_dtype == DVC_F32 ? std::max(1, g_build_wgs / 2) : g_build_wgs;
     long long nch = 8;
-    while (qtiles * nch < g_build_wgs && nch * 4 <= ncol_tiles && nch < 64) nch *= 2;
+    while (qtiles * nch < wgs && nch * 4 <= ncol_tiles && nch < 64) nch *= 2;
     const int nchunk = (int)std::min<long long>(nch, ncol_tiles);
     if (in_dtype == DVC_F16) {   // the AMP pyramid: fp16 operands on v_mfma_f32_32x32x16_f16, fp16 store
         if (store_dtype != DVC_F16) return fail(DVC_ERR_UNSUPPORTED, "build: float16 inputs need a float16 store");

@@ -2,7 +2,8 @@
 # One GPU-box session, steps chosen by STEPS (space list, run in order, stop at the first failure):
 #   tests   -m gpu suite (one process) + smoke
 #   bench   bench.py default line (config #3, the BASELINE metric) + the secondary lines in BENCH_SET
-#   prof    rocprofv3 --kernel-trace --stats of the default bench line
+#   prof    rocprofv3 --kernel-trace --stats of the default bench line (PROF_ARGS), then of each "name|args" entry
+#           of PROF_SET
 #   pmc     rocprofv3 --pmc passes of the default lookup (tools/pmc_groups.sh; PMC_GROUPS overrides)
 #   bwd     rocprofv3 kernel stats of the backward (tools/prof_bwd.sh), then its PMC passes (tools/pmc_bwd.sh,
 #           groups in BWD_PMC_GROUPS; skipped when empty)
@@ -57,7 +58,16 @@ for s in ${STEPS:-tests bench}; do
     ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_n1" -o run \
         -- python "$R/bench.py" --no-cpu-baseline --steps 5 --warmup 2 ${PROF_ARGS:-} > "$OUT/prof_n1.log" 2>&1 ) \
         || { echo "rocprof failed"; tail -3 "$OUT/prof_n1.log"; exit 3; }
-    echo "rocprof ok" ;;
+    echo "rocprof ok"
+    IFS=';' read -ra SET <<< "${PROF_SET:-}"   # more profiled lines: "name|bench args;..." -> prof_<name>/
+    for e in "${SET[@]}"; do
+      [ -z "$e" ] && continue
+      name=${e%%|*}; args=${e#*|}
+      ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$name" -o run \
+          -- python "$R/bench.py" --no-cpu-baseline --steps 5 --warmup 2 $args > "$OUT/prof_$name.log" 2>&1 ) \
+          || { echo "rocprof $name failed"; tail -3 "$OUT/prof_$name.log"; exit 3; }
+      echo "rocprof $name ok"
+    done ;;
   pmc)
     TAG=$T VARIANT=2 PMC_GROUPS="${PMC_GROUPS:-FETCH_SIZE;WRITE_SIZE;SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_BUSY_CYCLES;TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE GRBM_COUNT}" \
         EXTRA="${PMC_EXTRA:---reps 2}" bash tools/pmc_groups.sh || exit 3 ;;

@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD
-OUT=$R/gpurun_out/${TAG:-r01}/pmcg_v${VARIANT:-2}${TUNE:+_$TUNE}_${PREC:-bf16}_${SIZE:-32}
+OUT=$R/gpurun_out/${TAG:-r01}/pmcg_v${VARIANT:-2}${TUNE:+_$TUNE}_${PREC:-bf16}_${SIZE:-32}${SUFFIX:-}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp

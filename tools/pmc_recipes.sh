@@ -11,6 +11,13 @@ case "${1:-}" in
 r4a)   # round 4: the headline lookup's HBM traffic (bench roofline.traffic) and its read-request sizes / LDS
   cd $R && TAG=r4a VARIANT=2 EXTRA="--reps 2" PMC_GROUPS="FETCH_SIZE;WRITE_SIZE;TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_WRREQ_64B_sum;SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES" bash tools/pmc_groups.sh
   ;;
+r4i)   # round 4: instruction-cache and issue counters of the lookup at the small launches (one rank's 8-way slab of
+       # config #3, config #2 fp32) and at config #3 whole
+  ICG="SQC_ICACHE_REQ SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY"
+  cd $R && TAG=r4i VARIANT=2 SUFFIX=_s8 EXTRA="--reps 4 --shard-of 8" PMC_GROUPS="$ICG" bash tools/pmc_groups.sh || exit 1
+  cd $R && TAG=r4i VARIANT=2 SIZE=16 PREC=fp32 EXTRA="--reps 4" PMC_GROUPS="$ICG" bash tools/pmc_groups.sh || exit 1
+  cd $R && TAG=r4i VARIANT=2 EXTRA="--reps 2" PMC_GROUPS="$ICG" bash tools/pmc_groups.sh || exit 1
+  ;;
 r3c)
   cd /tmp && timeout -s KILL 60 rocprofv3 -L > $R/gpurun_out/r3c_avail.txt 2>&1
   cd $R && TAG=r3c VARIANT=2 EXTRA="--reps 2" PMC_GROUPS="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_INST_LDS;SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES" bash tools/pmc_groups.sh
@@ -40,5 +47,5 @@ r3m)
       bash tools/pmc_groups.sh || exit 1
   done
   ;;
-*) echo "usage: $0 r3c|r3e|r3j|r3k|r3m"; exit 2 ;;
+*) echo "usage: $0 r4a|r4i|r3c|r3e|r3j|r3k|r3m"; exit 2 ;;
 esac
