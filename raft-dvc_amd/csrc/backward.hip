@@ -1348,40 +1348,74 @@ struct UnpackArgs {
     long long sstride;
 };
 
+// Round 4: NS slots and NSUM partials are template parameters and every thread's 16 voxels x NS x NSUM loads are
+// issued before the first sum (unconditionally: a slot outside its level reads the voxel's own row 0 and is
+// dropped by a select), with 32-bit coordinates -- the round-3 loop (runtime slot / partial loops, 64-bit
+// divisions per voxel) waited for each load in turn: 33 us per unpack at config #3.
+template <int NS, int NSUM>
 __global__ __launch_bounds__(256) void k_unpack_sum(UnpackArgs U) {
     __shared__ float tile[64][65];
     const int b = blockIdx.z, c0 = blockIdx.y * 64;
     const long long v0 = (long long)blockIdx.x * 64;
     const float *src = U.src + (long long)b * U.src_bstride * U.Cp;
-#pragma unroll 4
+    const int c = threadIdx.x & 63, vq = threadIdx.x >> 6;   // channel c0 + c; voxels v0 + 4 k + vq
+    const bool cin = c0 + c < U.C;
+    float val[16][NS][NSUM];
+    bool ok[16][NS];
+#pragma unroll
     for (int k = 0; k < 16; ++k) {
-        const int idx = k * 256 + (int)threadIdx.x;
-        const int vl = idx >> 6, c = idx & 63;
-        const long long v = v0 + vl;
-        float s = 0.0f;
-        if (v < U.N && c0 + c < U.C) {
-            const int z = (int)(v % U.D);
-            const long long yx = v / U.D;
-            const int x = (int)(yx % U.W), y = (int)(yx / U.W);
-            for (int l = 0; l < U.ns; ++l) {
-                const int py = y >> l, px = x >> l, pz = z >> l;
-                if (py < U.Hs[l] && px < U.Ws[l] && pz < U.Ds[l]) {
-                    const float *p = src + (U.offs[l] + ((long long)py * U.Ws[l] + px) * U.Dps[l] + pz) * U.Cp + c0 + c;
-                    float v = p[0];
-                    for (int k = 1; k < U.nsum; ++k) v += p[k * U.sstride];
-                    s += U.wts[l] * v;
-                }
-            }
+        const long long v = v0 + 4 * k + vq;
+        const bool vin = v < U.N && cin;
+        const unsigned vv = vin ? (unsigned)v : 0u;   // (N < 2^31)
+        const unsigned yx = vv / (unsigned)U.D, z = vv - yx * (unsigned)U.D;
+        const unsigned y = yx / (unsigned)U.W, x = yx - y * (unsigned)U.W;
+#pragma unroll
+        for (int l = 0; l < NS; ++l) {
+            const unsigned py = y >> l, px = x >> l, pz = z >> l;
+            ok[k][l] = vin && py < (unsigned)U.Hs[l] && px < (unsigned)U.Ws[l] && pz < (unsigned)U.Ds[l];
+            const long long row = ok[k][l] ? U.offs[l] + ((long long)py * U.Ws[l] + px) * U.Dps[l] + pz : 0;
+            const float *p = src + row * U.Cp + (cin ? c0 + c : 0);
+#pragma unroll
+            for (int k2 = 0; k2 < NSUM; ++k2) val[k][l][k2] = p[k2 * U.sstride];
         }
-        tile[vl][c] = s;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        float sum = 0.0f;
+#pragma unroll
+        for (int l = 0; l < NS; ++l) {
+            float v = val[k][l][0];
+#pragma unroll
+            for (int k2 = 1; k2 < NSUM; ++k2) v += val[k][l][k2];
+            sum += ok[k][l] ? U.wts[l] * v : 0.0f;
+        }
+        tile[4 * k + vq][c] = sum;
     }
     __syncthreads();
 #pragma unroll 4
     for (int k = 0; k < 16; ++k) {
         const int idx = k * 256 + (int)threadIdx.x;
-        const int c = idx >> 6, vl = idx & 63;
+        const int cc = idx >> 6, vl = idx & 63;
         const long long v = v0 + vl;
-        if (v < U.N && c0 + c < U.C) U.dst[((long long)b * U.C + c0 + c) * U.N + v] = tile[vl][c];
+        if (v < U.N && c0 + cc < U.C) U.dst[((long long)b * U.C + c0 + cc) * U.N + v] = tile[vl][cc];
+    }
+}
+
+static void launch_unpack(const UnpackArgs &U, dim3 grid, hipStream_t s) {
+    if (U.nsum > 1) {
+        if (U.nsum == 2) k_unpack_sum<1, 2><<<grid, 256, 0, s>>>(U);
+        else k_unpack_sum<1, 3><<<grid, 256, 0, s>>>(U);
+        return;
+    }
+    switch (U.ns) {
+    case 1: k_unpack_sum<1, 1><<<grid, 256, 0, s>>>(U); break;
+    case 2: k_unpack_sum<2, 1><<<grid, 256, 0, s>>>(U); break;
+    case 3: k_unpack_sum<3, 1><<<grid, 256, 0, s>>>(U); break;
+    case 4: k_unpack_sum<4, 1><<<grid, 256, 0, s>>>(U); break;
+    case 5: k_unpack_sum<5, 1><<<grid, 256, 0, s>>>(U); break;
+    case 6: k_unpack_sum<6, 1><<<grid, 256, 0, s>>>(U); break;
+    case 7: k_unpack_sum<7, 1><<<grid, 256, 0, s>>>(U); break;
+    default: k_unpack_sum<8, 1><<<grid, 256, 0, s>>>(U); break;
     }
 }
 
@@ -1650,7 +1684,9 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
         k_bw_keys<R><<<dim3((unsigned)((A.Nq + 255) / 256), (unsigned)A.L), 256, 0, s>>>(A, b, kin);
         if (!launched("keys")) return DVC_ERR_LAUNCH;
         size_t tb = P.temp;
-        if (rocprim::radix_sort_keys(temp, tb, kin, kout, (size_t)nkeys, 0u, 32u + bits, s) != hipSuccess) {
+        // (the cell bits only: the keys enter in (level, query) order and the sort is stable, so within a cell the
+        // queries stay in ascending order -- the order of the full keys -- in 2-3 digit passes instead of 6-7)
+        if (rocprim::radix_sort_keys(temp, tb, kin, kout, (size_t)nkeys, 32u, 32u + bits, s) != hipSuccess) {
             snprintf(err, errlen, "corr_backward: radix sort failed");
             return DVC_ERR_RUNTIME;
         }
@@ -1700,7 +1736,7 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     U.ns = 1; U.Hs[0] = A.Hq; U.Ws[0] = A.Wq; U.Ds[0] = A.Dq; U.Dps[0] = A.Dq; U.offs[0] = 0; U.wts[0] = 1.0f;
     U.nsum = qparts; U.sstride = qstride;
     dim3 g1grid((unsigned)((A.Nq + 63) / 64), (unsigned)((C + 63) / 64), (unsigned)A.B);
-    k_unpack_sum<<<g1grid, 256, 0, s>>>(U);
+    launch_unpack(U, g1grid, s);
     if (!launched("unpack_q")) return DVC_ERR_LAUNCH;
     // dfmap2 (B, C, H, W, D) <- sum_l 8^-l dT_l (floor-mode avg_pool3d adjoint)
     UnpackArgs V{};
@@ -1717,7 +1753,7 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
         V.offs[l] = lay.offset[l]; V.wts[l] = wl;
     }
     dim3 g2grid((unsigned)((V.N + 63) / 64), (unsigned)((C + 63) / 64), (unsigned)A.B);
-    k_unpack_sum<<<g2grid, 256, 0, s>>>(V);
+    launch_unpack(V, g2grid, s);
     if (!launched("unpack_t")) return DVC_ERR_LAUNCH;
     return DVC_OK;
 }
