@@ -626,13 +626,17 @@ __global__ __launch_bounds__(256) void k_tile_targets(const TT *__restrict__ Tt,
 // VGPRs: one wave per SIMD, every gather's latency exposed).  Per (union row, 16-target z batch) the 256 threads
 // copy the batch straight into LDS with LDS-DMA buffer loads (no VGPR destination, 32-bit offsets): the target
 // rows Ttr[128 ch][16 z] (one 16-byte DMA per thread) and the 64 queries' window gradients G[64][16 z] as
-// bf16_hilo pairs (four 4-byte DMAs per thread; values outside a query's window are out of the buffer's range
-// and land as 0).  The pairs are the MFMA's A operand as they stand -- K runs over (z, hi/lo), and the B operand
+// bf16_hilo pairs (values outside a query's window rows are out of the buffer's range and land as 0).  The pairs are the MFMA's A operand as they stand -- K runs over (z, hi/lo), and the B operand
 // repeats each target row twice -- so no wave converts anything.  kQStages LDS stages keep kQStages - 2
 // batches in flight across the raw barrier that retires the current one (a counted vmcnt: a __syncthreads()
 // would drain every DMA in flight).  Both tiles are XOR-swizzled through the DMA source offsets so the operand
 // reads are free of bank conflicts.  Level groups (blockIdx.y) write separate partial dQ (level 0 alone, the
 // coarse levels together), summed in a fixed order by k_unpack_sum.
+// Round 4: the window gradients arrive as ONE 16-byte DMA per thread and batch (four consecutive z of one query's
+// row) instead of four 4-byte ones.  Deeper pipelines did not help (6 / 8 / 9 stages at 3 / 2 / 2 workgroups per
+// CU: 1.16-1.25 vs 1.03 ms per backward, gpurun_out/r4k, r4n): the per-lane gathers' instruction count through the
+// texture addresser was the bound.  A chunk straddling the query's window row carries values of the neighbouring
+// rows; the A-operand read zeroes every z outside [iv, iv + nv) (four selects per operand).
 constexpr int kQRows = 1024;   // batches listed at a time (a box's union at +-2 flows, r = 4: 17^2 rows x 2)
 #ifndef DVC_QSTAGES
 #define DVC_QSTAGES 4
@@ -729,8 +733,6 @@ __global__ __launch_bounds__(256, kQOcc<SPLIT>) void k_grad_q_mfma(const bf16_t 
     const u32x4 rs_tl = sgpr_rsrc(Tz + tz_lo + (((long long)b * ((A.Cp + 127) / 128) + A.cbase / 128) * ntz) * 2048,
                                   (unsigned)min(ntz * 4096, 0x7fffffffLL));
     const unsigned tvo = 16u * (unsigned)tid;
-    // G DMA role, instruction k: query gq = 16 w + 4 k + lane / 16, physical dword lane & 15 of its 64-byte row =
-    // logical z 4 ((lane >> 2 & 3) ^ (gq >> 2 & 3)) + (lane & 3)
     f32x16 acc[2];
 #pragma unroll
     for (int T = 0; T < 2; ++T)
@@ -755,23 +757,31 @@ __global__ __launch_bounds__(256, kQOcc<SPLIT>) void k_grad_q_mfma(const bf16_t 
         const int zlo = max(bw_wave_min(live ? iv : BIG), 0) & ~7;
         const int zhi = min(bw_wave_max(live ? iv : -BIG) + nv - 1, Dl - 1);
         const int nzb = zhi >= zlo ? (zhi - zlo + 16) >> 4 : 0;
-        // the box's window gradients of this level as one buffer (the box spans < 4 (W, D) planes of queries)
+        // the box's window gradients of this level as one buffer (the box spans < 4 (W, D) planes of queries), its
+        // base 16 bytes early: a 16-byte chunk may start up to 3 values before a window row (those values, like the
+        // ones past its end, belong to other rows and are masked when the operand is read)
         const int nw3 = (int)bw_nw3(A, l);
-        const u32x4 rs_g = sgpr_rsrc(A.gwin + A.goff[l] + ((long long)b * A.Nq + qb0) * nw3,
-                                     (unsigned)min((long long)(3 * A.Wq * A.Dq + 3 * A.Dq + 4) * nw3 * 4, 0x7fffffffLL));
-        // this thread's four G queries: window origin and first gradient (bytes)
-        int goh[4], gou[4], gov[4], gqo[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int gq = 16 * w + 4 * k + (lane >> 4);
+        const u32x4 rs_g = sgpr_rsrc(A.gwin + A.goff[l] + ((long long)b * A.Nq + qb0) * nw3 - 4,
+                                     (unsigned)min((long long)(3 * A.Wq * A.Dq + 3 * A.Dq + 4) * nw3 * 4 + 32,
+                                                   0x7fffffffLL));
+        // this thread's G chunk (round 4: one 16-byte DMA per thread and batch, was four 4-byte ones -- the texture
+        // addresser's instruction count bound the kernel): query gq = 16 w + lane / 4, physical chunk lane & 3 of its
+        // 64-byte row = logical z chunk (lane & 3) ^ (gq >> 2 & 3)
+        int goh, gou, gov, gqo;
+        {
+            const int gq = 16 * w + (lane >> 2);
             // (every shuffle runs on all lanes: under a branch, ds_bpermute reads 0 from switched-off lanes)
             const bool lv = __shfl((int)live, gq) != 0;
             const int sh = __shfl(ih, gq);
-            goh[k] = lv ? sh : -BIG;   // (dead / inactive queries take no values)
-            gou[k] = __shfl(iu, gq);
-            gov[k] = __shfl(iv, gq) - 4 * (((lane >> 2) & 3) ^ ((gq >> 2) & 3)) - (lane & 3);
-            gqo[k] = __shfl(qrel, gq) * nw3;
+            goh = lv ? sh : -BIG;   // (dead / inactive queries take no values)
+            gou = __shfl(iu, gq);
+            gov = __shfl(iv, gq) - 4 * ((lane & 3) ^ ((gq >> 2) & 3));
+            gqo = __shfl(qrel, gq) * nw3;
         }
+        // operand masks: the A rows this lane reads are queries 32 T + m; their window z origin
+        int ivq[2];
+#pragma unroll
+        for (int T = 0; T < 2; ++T) ivq[T] = __shfl(iv, 32 * T + m);
         const long long tzl = A.tz0[l];
         const int kbl = Dpl >> 3;
         // one batch's DMAs into stage st: 1 T + 4 G per thread
@@ -784,12 +794,11 @@ __global__ __launch_bounds__(256, kQOcc<SPLIT>) void k_grad_q_mfma(const bf16_t 
                 blds(rs_t, tvo, toff, sb + 1024 * w, W16{});
                 if constexpr (SPLIT) blds(rs_tl, tvo, toff, sb + 8192 + 1024 * w, W16{});
             }
-#pragma unroll
-            for (int k = 0; k < 4 && !(DVC_GQ_ABL & 2); ++k) {
-                const int wy = y - goh[k], wx = x - gou[k], wz = z0 - gov[k];
-                const bool ok = (unsigned)wy < (unsigned)nh && (unsigned)wx < (unsigned)nu && (unsigned)wz < (unsigned)nv;
-                blds(rs_g, ok ? (unsigned)((gqo[k] + (wy * nu + wx) * nv + wz) * 4) : kOOB, 0u,
-                     sb + 4096 + 256 * (4 * w + k), W4{});
+            if (!(DVC_GQ_ABL & 2)) {
+                const int wy = y - goh, wx = x - gou, wz = z0 - gov;
+                const bool ok = (unsigned)wy < (unsigned)nh && (unsigned)wx < (unsigned)nu && wz > -4 && wz < nv;
+                blds(rs_g, ok ? (unsigned)((gqo + (wy * nu + wx) * nv + wz) * 4 + 16) : kOOB, 0u, sb + 4096 + 1024 * w,
+                     W16{});
             }
         };
         // the batches: every z batch of each union row some window of the box contains, listed by wave 0 (lane =
@@ -824,7 +833,7 @@ __global__ __launch_bounds__(256, kQOcc<SPLIT>) void k_grad_q_mfma(const bf16_t 
             for (int it = 0; it < nit; ++it) {
                 // batch it has landed (this thread's DMAs; kQStages - 2 newer batches may fly), then every thread's
                 // has, and every wave is done with batch it - 1, whose stage the next DMA refills
-                constexpr int kDma = ((DVC_GQ_ABL & 4) ? 0 : (SPLIT ? 2 : 1)) + ((DVC_GQ_ABL & 2) ? 0 : 4);   // DMAs per batch
+                constexpr int kDma = ((DVC_GQ_ABL & 4) ? 0 : (SPLIT ? 2 : 1)) + ((DVC_GQ_ABL & 2) ? 0 : 1);   // DMAs per batch
                 asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kDma * (kQStages - 2)) : "memory");
                 __builtin_amdgcn_s_barrier();
                 asm volatile("" ::: "memory");
@@ -832,6 +841,7 @@ __global__ __launch_bounds__(256, kQOcc<SPLIT>) void k_grad_q_mfma(const bf16_t 
                 if (w < NCT && !(DVC_GQ_ABL & 1)) {
                     const unsigned char *sb = stg + (it % kQStages) * STAGE;
                     const int r = 32 * w + m, rsw = (r >> 3) & 1;
+                    const int bz0 = (int)(__builtin_amdgcn_readfirstlane(qrows[it]) >> 22);   // the batch's z0
 #pragma unroll
                     for (int j = 0; j < 2; ++j) {   // z 8 j .. 8 j + 7: K = 16 (z, hi/lo) pairs
                         // B: this lane's 4 targets z = 8 j + 4 h .. + 3 of channel r, each twice
@@ -843,8 +853,12 @@ __global__ __launch_bounds__(256, kQOcc<SPLIT>) void k_grad_q_mfma(const bf16_t 
 #pragma unroll
                         for (int T = 0; T < 2; ++T) {
                             const int gq = 32 * T + m, sw = (gq >> 2) & 3;
-                            const bf16x8 ag =
-                                *reinterpret_cast<const bf16x8 *>(sb + 4096 + gq * 64 + 16 * ((2 * j + h) ^ sw));
+                            u32x4 av = *reinterpret_cast<const u32x4 *>(sb + 4096 + gq * 64 + 16 * ((2 * j + h) ^ sw));
+                            // (target z = bz0 + 4 (2 j + h) + i: its window z of query gq must lie in [0, nv))
+                            const int wz0 = bz0 + 4 * (2 * j + h) - ivq[T];
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) av[i] = (unsigned)(wz0 + i) < (unsigned)nv ? av[i] : 0u;
+                            const bf16x8 ag = __builtin_bit_cast(bf16x8, av);
                             acc[T] = mma32<F16>(ag, bt, acc[T]);
                             if constexpr (SPLIT) acc[T] = mma32<F16>(ag, btl, acc[T]);
                         }
