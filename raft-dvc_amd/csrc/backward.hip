@@ -87,12 +87,37 @@ struct BwdArgs {
     long long tz0[DVC_MAX_LEVELS + 1];
 };
 
+// XCD-contiguous block order: the dispatcher deals workgroups round-robin over the 8 XCDs (workgroup i on XCD i % 8),
+// so logical block b = XCD x's share [x q + min(x, r), ...) of n = 8 q + r makes each XCD's L2 serve a contiguous
+// run of logical blocks (neighbouring bricks / boxes, whose queries' windows overlap) instead of every eighth one
+__device__ __forceinline__ int xcd_block(int i, int n) {
+    const int q = n >> 3, r = n & 7, x = i & 7;
+    return x * q + min(x, r) + (i >> 3);
+}
+// the same in groups of 8 C logical blocks (each XCD a run of C of every group; the tail past the last whole group
+// keeps the round-robin order): a launch whose block costs vary by range (k_grad_t: level 0's bricks, then the
+// coarse levels' splits) stays balanced over the XCDs
+#ifndef DVC_GT_XCD
+#define DVC_GT_XCD 64   // k_grad_t_mfma: logical blocks per XCD run
+#endif
+#ifndef DVC_GQ_XCD
+#define DVC_GQ_XCD 0    // k_grad_q_mfma: boxes per XCD run (0: one contiguous run per XCD)
+#endif
+template <int C> __device__ __forceinline__ int xcd_block_grouped(int i, int n) {
+    if (i >= n / (8 * C) * (8 * C)) return i;
+    const int x = i & 7, slot = i >> 3;
+    return (slot / C) * (8 * C) + x * C + slot % C;
+}
+
 // (level, brick, split) of this k_grad_t workgroup (wave-uniform: from blockIdx and the level table)
 struct GtBlock {
     int l, brick, split, nsplit;
 };
 __device__ __forceinline__ GtBlock gt_block(const BwdArgs &A) {
-    const int bx = (int)blockIdx.x;
+    // (round 4: runs of 64 blocks per XCD -- the window gradients of a brick's queries are re-read by its
+    // neighbours: L2 hit rate 0.21 and 1.7 GB of HBM reads per launch at config #3 with consecutive bricks on
+    // different XCDs; one contiguous run per XCD instead put level 0's heavy bricks on three XCDs: 286 -> 450 us)
+    const int bx = xcd_block_grouped<DVC_GT_XCD>((int)blockIdx.x, (int)gridDim.x);
     int l = 0;
     while (l + 1 < A.L && bx >= A.gt_blk0[l + 1]) ++l;
     GtBlock g;
@@ -708,7 +733,10 @@ __global__ __launch_bounds__(256, kQOcc<SPLIT>) void k_grad_q_mfma(const bf16_t 
     const int tid = threadIdx.x, lane = tid & 63, m = lane & 31, h = lane >> 5;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nbz = (A.Dq + 3) >> 2, nbx = (A.Wq + 3) >> 2, nby = (A.Hq + 3) >> 2;
-    int t = blockIdx.x;
+    // (XCD runs of boxes: neighbours share target tiles)
+    int t;
+    if constexpr (DVC_GQ_XCD > 0) t = xcd_block_grouped<DVC_GQ_XCD>((int)blockIdx.x, (int)gridDim.x);
+    else t = xcd_block((int)blockIdx.x, (int)gridDim.x);
     const int bz = t % nbz; t /= nbz;
     const int bx = t % nbx; t /= nbx;
     const int by = t % nby;

@@ -18,6 +18,9 @@ r4i)   # round 4: instruction-cache and issue counters of the lookup at the smal
   cd $R && TAG=r4i VARIANT=2 SIZE=16 PREC=fp32 EXTRA="--reps 4" PMC_GROUPS="$ICG" bash tools/pmc_groups.sh || exit 1
   cd $R && TAG=r4i VARIANT=2 EXTRA="--reps 2" PMC_GROUPS="$ICG" bash tools/pmc_groups.sh || exit 1
   ;;
+r4p)   # round 4: the backward's gradient kernels at config #3 (tools/bwd_only.py): HBM / L2, issue, LDS, addresser
+  cd $R && TAG=r4p PMC_GROUPS="FETCH_SIZE;WRITE_SIZE TCC_HIT_sum TCC_MISS_sum;TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum;SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES;SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_VMEM_RD TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum" bash tools/pmc_bwd.sh
+  ;;
 r3c)
   cd /tmp && timeout -s KILL 60 rocprofv3 -L > $R/gpurun_out/r3c_avail.txt 2>&1
   cd $R && TAG=r3c VARIANT=2 EXTRA="--reps 2" PMC_GROUPS="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_INST_LDS;SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES" bash tools/pmc_groups.sh
@@ -47,5 +50,5 @@ r3m)
       bash tools/pmc_groups.sh || exit 1
   done
   ;;
-*) echo "usage: $0 r4a|r4i|r3c|r3e|r3j|r3k|r3m"; exit 2 ;;
+*) echo "usage: $0 r4a|r4i|r4p|r3c|r3e|r3j|r3k|r3m"; exit 2 ;;
 esac
