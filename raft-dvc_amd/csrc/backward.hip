@@ -1579,7 +1579,7 @@ static bool mfma_offsets_fit(const BwdArgs &A, const BwdPlan &P) {
     if (P.tz0[A.L] * 4096 > lim) return false;
     const long long span = 3LL * A.Wq * A.Dq + 3LL * A.Dq + 4;
     for (int l = 0; l < A.L; ++l)
-        if (span * ((long long)A.nwh[l] * A.nwu[l] * A.nwv[l]) * 4 > lim) return false;
+        if (span * ((long long)A.nwh[l] * A.nwu[l] * A.nwv[l]) * 4 + 32 > lim) return false;   // (+32: rs_g's slack)
     return true;
 }
 
