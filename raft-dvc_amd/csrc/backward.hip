@@ -7,7 +7,7 @@
 // per-channel atomics; here nothing is atomic and no dense d(corr) is formed --
 // memory is O(C * voxels + Nq * (2r+2)^3):
 //
-//   k_win_grad    dwin[b][l][q][i][j][k]: the transpose of the lookup's separable
+//   k_win_grad_pairs  dwin[b][l][q][i][j][k]: the transpose of the lookup's separable
 //                 interpolation, i.e. each query's gradient on the (2r+2)^3 integer
 //                 window of every level (lane = query);
 //   k_grad_q      dQ[q] = s * sum_l sum_{p in win_l(q)} dwin[q][p - o_q] * T_l[p]:
@@ -220,52 +220,66 @@ template <int FMT> __device__ __forceinline__ unsigned gw_pair(float g) {
 // is staged in the wave's LDS image and leaves as 16-byte stores of consecutive pieces (a wave instruction writes
 // ~2.5 queries' planes, ~10 whole lines), instead of 8-byte stores 4 NW^3 bytes apart (64 lines per instruction:
 // 65 M partial-line writes at config #3); the next plane's output-gradient row is loaded before the flush.
-template <int R> struct WinGradCfg {
-    static constexpr int NW = 2 * R + 2;
+// Round 4, last: TWO lanes per query (lanes 0-31 and 32-63 take the window's column halves j < R + 1 and j >= R + 1 of
+// the same 32 queries), so a lane holds R + 2 output-gradient columns of each of the two rows instead of 2 R + 1:
+// 108 instead of 162 row registers at r = 4, 226 VGPRs and two waves per SIMD instead of one at 328 (the output
+// gradient column u = R is read by both halves: +11 % of the output-gradient reads).  Same arithmetic, same order,
+// bitwise-equal results (tools/ab_bwd.py --compare); 222 -> 214 us at config #3: the kernel moves its ~950 MB at
+// ~4.4 TB/s, the mixed read/write rate, so the occupancy bought little.
+template <int R> struct WinGradPCfg {
+    static constexpr int NW = 2 * R + 2, HC = R + 1;        // window columns per half
     static constexpr int SW = NW * NW + 4;                 // LDS image row (dwords) per query: 16-byte aligned
-    static constexpr int WAVES = R >= 6 ? 3 : 4;           // waves per workgroup (LDS: WAVES x 64 x SW x 4 bytes)
-    static constexpr int LDS = WAVES * 64 * SW * 4;
+    static constexpr int WAVES = 4;
+    static constexpr int LDS = WAVES * 32 * SW * 4;
 };
 template <int R, int FMT>
-__global__ __launch_bounds__(64 * WinGradCfg<R>::WAVES) void k_win_grad(BwdArgs A) {
-    using G = WinGradCfg<R>;
-    constexpr int n = 2 * R + 1, NW = G::NW, NW3 = NW * NW * NW, SW = G::SW, P16 = NW * NW / 4;
+__global__ __launch_bounds__(256) void k_win_grad_pairs(BwdArgs A) {
+    using G = WinGradPCfg<R>;
+    constexpr int n = 2 * R + 1, NW = G::NW, NW3 = NW * NW * NW, SW = G::SW, P16 = NW * NW / 4, HC = G::HC;
+    constexpr int NCOL = R + 2;   // output-gradient columns u = U0 .. U0 + R + 1 of this lane's half
+    constexpr unsigned kOff = 0x80000000u;   // a buffer offset past every range (reads 0, stores dropped)
     extern __shared__ __attribute__((aligned(16))) float wg_stage[];
-    // (wave index through readfirstlane: the tile, level and descriptors below are then scalar -- per-lane
-    // descriptors would wrap every buffer access in a waterfall loop)
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const long long nqb = (A.Nq + 63) / 64;
+    const int ql = lane & 31, half = lane >> 5;
+    const long long nqb = (A.Nq + 31) / 32;
     const long long item = (long long)blockIdx.x * G::WAVES + wave;
     if (item >= (long long)A.B * A.L * nqb) return;
     const int bl = (int)(item / nqb);
     const int l = bl % A.L, b = bl / A.L;
-    const long long q0 = (item - (long long)bl * nqb) * 64;
-    const long long q = q0 + lane;
-    const int nvalid = (int)min(64LL, A.Nq - q0);
+    const long long q0 = (item - (long long)bl * nqb) * 32;
+    const long long q = q0 + ql;
+    const int nvalid = (int)min(32LL, A.Nq - q0);
     if (A.generic[l]) return;   // generic levels: k_win_grad_generic
-    float *gw = A.gwin + A.goff[l] + ((long long)b * A.Nq + q) * NW3;
     if (A.zero[l]) {   // a size-1 level samples zeros (corr.py:41-44): no gradient reaches it
-        if (lane < nvalid)
-            for (int i = 0; i < NW3; i += 2) *reinterpret_cast<f32x2 *>(gw + i) = f32x2{0.0f, 0.0f};
+        float *gw = A.gwin + A.goff[l] + ((long long)b * A.Nq + q) * NW3;
+        if (ql < nvalid)
+            for (int i = half * 2; i < NW3; i += 4) *reinterpret_cast<f32x2 *>(gw + i) = f32x2{0.0f, 0.0f};
         return;
     }
-    // this wave's query tile as one store descriptor (lanes past the tile's valid queries: out of range, dropped)
     const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(
         A.gwin + A.goff[l] + ((long long)b * A.Nq + q0) * NW3, (short)0, nvalid * NW3 * 4, 0x00020000);
-    float *img = wg_stage + wave * 64 * SW;   // [64 queries][SW], this wave's image of one window plane
-    const long long qc = q < A.Nq ? q : A.Nq - 1;   // (lanes past the end compute a copy of the last query)
+    float *img = wg_stage + wave * 32 * SW;   // [32 queries][SW], this wave's image of one window plane
+    const long long qc = q < A.Nq ? q : A.Nq - 1;
     const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l];
     float cy, cx, cz;
     load_coords(A.coords, b, A.Nq, qc, cy, cx, cz);
     WinAxes ax;
     bw_axes(A, l, cy, cx, cz, ax);
     const int ih = (int)ax.kh - R, iu = (int)ax.ku - R, iv = (int)ax.kv - R;
-    float wx0[n], wx1[n], wz0[n], wz1[n];
+    const int J0 = half * HC, U0 = J0 - 1;
+    // this lane's column weights: window column j = J0 + jj takes wx0[j] (j < n) and wx1[j - 1] (j >= 1)
+    float wj0[HC], wj1[HC], wz0[n], wz1[n];
+#pragma unroll
+    for (int jj = 0; jj < HC; ++jj) {
+        const int j = J0 + jj;
+        float a0, a1, b0, b1;
+        axis_weights(ax.pu, ax.ku, j - R, ax.un, ax.uu, a0, a1);
+        axis_weights(ax.pu, ax.ku, j - 1 - R, ax.un, ax.uu, b0, b1);
+        wj0[jj] = j < n && (unsigned)(iu + j) < (unsigned)Wl ? a0 : 0.0f;
+        wj1[jj] = j >= 1 && (unsigned)(iu + j) < (unsigned)Wl ? b1 : 0.0f;
+    }
 #pragma unroll
     for (int t = 0; t < n; ++t) {
-        axis_weights(ax.pu, ax.ku, t - R, ax.un, ax.uu, wx0[t], wx1[t]);
-        wx0[t] = (unsigned)(iu + t) < (unsigned)Wl ? wx0[t] : 0.0f;
-        wx1[t] = (unsigned)(iu + t + 1) < (unsigned)Wl ? wx1[t] : 0.0f;
         axis_weights(ax.pv, ax.kv, t - R, ax.vn, ax.vu, wz0[t], wz1[t]);
         wz0[t] = (unsigned)(iv + t) < (unsigned)Dl ? wz0[t] : 0.0f;
         wz1[t] = (unsigned)(iv + t + 1) < (unsigned)Dl ? wz1[t] : 0.0f;
@@ -273,23 +287,25 @@ __global__ __launch_bounds__(64 * WinGradCfg<R>::WAVES) void k_win_grad(BwdArgs 
     const long long chu = A.legacy ? 1 : n, chv = A.legacy ? n : 1;
     const float *gbl = A.gout + (long long)bl * n * n * n * A.Nq;
     const int q4 = (int)(qc * 4), nq4 = (int)(A.Nq * 4);
-    // Window plane i collects output row a = i (corner 0) and a = i - 1 (corner 1); row i - 1 stays in registers
-    // from the previous plane (ping-pong buffers)
-    float rowA[n][n], rowB[n][n];
-    // output row a of this lane's query; a = n (past the last row) reads zeros through an empty descriptor, so the
-    // loads are unconditional (under a branch the old register contents would stay live beside the new ones)
-    auto load_row = [&](int a, float (&dst)[n][n]) {
+    unsigned voff[NCOL];   // column u = U0 + c of this lane's query (u outside [0, n): reads 0)
+#pragma unroll
+    for (int c = 0; c < NCOL; ++c) {
+        const int u = U0 + c;
+        voff[c] = (unsigned)u < (unsigned)n ? (unsigned)(q4 + (int)(u * chu) * nq4) : kOff;
+    }
+    float rowA[NCOL][n], rowB[NCOL][n];
+    auto load_row = [&](int a, float (&dst)[NCOL][n]) {   // a = n: an empty descriptor (zeros, unconditional loads)
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             (void *)(gbl + (long long)min(a, n - 1) * n * n * A.Nq), (short)0,
             a < n ? (int)min((long long)n * n * nq4, 0x7fffffffLL) : 0, 0x00020000);
 #pragma unroll
-        for (int uu = 0; uu < n; ++uu)
+        for (int c = 0; c < NCOL; ++c)
 #pragma unroll
             for (int v = 0; v < n; ++v)
-                dst[uu][v] = __builtin_bit_cast(
-                    float, __builtin_amdgcn_raw_buffer_load_b32(rs, q4, (int)((uu * chu + v * chv) * nq4), 0));
+                dst[c][v] = __builtin_bit_cast(
+                    float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)voff[c], (int)(v * chv * nq4), 0));
     };
-    auto plane = [&](int i, const float (&cur)[n][n], float (&prev)[n][n]) {
+    auto plane = [&](int i, const float (&cur)[NCOL][n], float (&prev)[NCOL][n]) {
         float wa0 = 0.0f, wa1 = 0.0f, t0, t1;
         if (i < n) {
             axis_weights(ax.ph, ax.kh, i - R, ax.hs, ax.hs, t0, t1);
@@ -299,37 +315,34 @@ __global__ __launch_bounds__(64 * WinGradCfg<R>::WAVES) void k_win_grad(BwdArgs 
             axis_weights(ax.ph, ax.kh, i - 1 - R, ax.hs, ax.hs, t0, t1);
             wa1 = (unsigned)(ih + i) < (unsigned)Hl ? t1 : 0.0f;
         }
-        float Pp[n];
+        auto pcol = [&](int c, float (&P)[n]) {   // the plane's row combination of column U0 + c
 #pragma unroll
-        for (int v = 0; v < n; ++v) Pp[v] = 0.0f;
+            for (int v = 0; v < n; ++v) P[v] = 0.0f;
+            if (i < n) {
 #pragma unroll
-        for (int j = 0; j < NW; ++j) {
-            float Pc[n];
-#pragma unroll
-            for (int v = 0; v < n; ++v) Pc[v] = 0.0f;
-            if (j < n) {
-                const int uu = j < n ? j : 0;
-                if (i < n) {
-#pragma unroll
-                    for (int v = 0; v < n; ++v) Pc[v] = wa0 * cur[uu][v];
-                }
-                if (i >= 1) {
-#pragma unroll
-                    for (int v = 0; v < n; ++v) Pc[v] = __builtin_fmaf(wa1, prev[uu][v], Pc[v]);
-                }
+                for (int v = 0; v < n; ++v) P[v] = wa0 * cur[c][v];
             }
-            const float wj0 = j < n ? wx0[j < n ? j : 0] : 0.0f;
-            const float wj1 = j >= 1 ? wx1[j >= 1 ? j - 1 : 0] : 0.0f;
+            if (i >= 1) {
+#pragma unroll
+                for (int v = 0; v < n; ++v) P[v] = __builtin_fmaf(wa1, prev[c][v], P[v]);
+            }
+        };
+        float Pp[n];
+        pcol(0, Pp);
+#pragma unroll
+        for (int jj = 0; jj < HC; ++jj) {
+            float Pc[n];
+            pcol(jj + 1, Pc);
             float o[NW];
 #pragma unroll
             for (int k = 0; k < NW; ++k) o[k] = 0.0f;
 #pragma unroll
             for (int v = 0; v < n; ++v) {
-                const float gz = __builtin_fmaf(wj0, Pc[v], wj1 * Pp[v]);
+                const float gz = __builtin_fmaf(wj0[jj], Pc[v], wj1[jj] * Pp[v]);
                 o[v] = __builtin_fmaf(wz0[v], gz, o[v]);
                 o[v + 1] = __builtin_fmaf(wz1[v], gz, o[v + 1]);
             }
-            u32x2 *dst = reinterpret_cast<u32x2 *>(img + lane * SW + j * NW);
+            u32x2 *dst = reinterpret_cast<u32x2 *>(img + ql * SW + (J0 + jj) * NW);
 #pragma unroll
             for (int k = 0; k < NW / 2; ++k) {
                 if constexpr (FMT != kGwF32) dst[k] = u32x2{gw_pair<FMT>(o[2 * k]), gw_pair<FMT>(o[2 * k + 1])};
@@ -338,32 +351,26 @@ __global__ __launch_bounds__(64 * WinGradCfg<R>::WAVES) void k_win_grad(BwdArgs 
 #pragma unroll
             for (int v = 0; v < n; ++v) Pp[v] = Pc[v];
         }
-        // row i - 1 is consumed: the next plane's row i + 1 goes into its registers before the flush's stores
-        // (the scheduling barrier keeps the loads below the last read of row i - 1: hoisted above the columns they
-        // would keep a third row of registers live)
         __builtin_amdgcn_sched_barrier(0);
         load_row(i + 1, prev);
-        // flush: piece c (16 bytes) of the tile's plane i = piece c % P16 of query c / P16 (the same wave wrote the
-        // image, so the LDS order of its own instructions covers the read-after-write)
-        // (in groups of FG pieces: the compiler would otherwise hoist every LDS read above the first store, 4 P16
-        // registers next to the two output-gradient rows)
-        constexpr int FG = 5;
+        // flush the 32 queries' plane i: piece c = piece c % P16 of query c / P16 (out-of-range pieces: dropped)
+        constexpr int NIT = (32 * P16 + 63) / 64, FG = 4;
 #pragma unroll
-        for (int g0 = 0; g0 < P16; g0 += FG) {
+        for (int g0 = 0; g0 < NIT; g0 += FG) {
             u32x4 v[FG];
+            int off[FG];
 #pragma unroll
             for (int u = 0; u < FG; ++u) {
                 const int c = (g0 + u) * 64 + lane;
-                const int qq = c / P16, pc = c - qq * P16;
-                if (g0 + u < P16) v[u] = *reinterpret_cast<const u32x4 *>(img + qq * SW + pc * 4);
+                const bool ok = g0 + u < NIT && c < 32 * P16;
+                const int cc = ok ? c : 0;
+                const int qq = cc / P16, pc = cc - qq * P16;
+                v[u] = *reinterpret_cast<const u32x4 *>(img + qq * SW + pc * 4);
+                off[u] = ok ? (qq * NW3 + i * NW * NW + pc * 4) * 4 : (int)kOff;
             }
 #pragma unroll
-            for (int u = 0; u < FG; ++u) {
-                const int c = (g0 + u) * 64 + lane;
-                const int qq = c / P16, pc = c - qq * P16;
-                if (g0 + u < P16)
-                    __builtin_amdgcn_raw_buffer_store_b128(v[u], rs_out, (qq * NW3 + i * NW * NW + pc * 4) * 4, 0, 0);
-            }
+            for (int u = 0; u < FG; ++u)
+                if (g0 + u < NIT) __builtin_amdgcn_raw_buffer_store_b128(v[u], rs_out, off[u], 0, 0);
             __builtin_amdgcn_sched_barrier(0);
         }
     };
@@ -583,7 +590,7 @@ __global__ __launch_bounds__(256) void k_grad_q(const TT *__restrict__ Tt, float
 // 2b. bf16 path of step 2 on the matrix cores.  Per 4x4x4 query box, union row (y, x) and
 // 16-target z batch: dQ[64 queries][Cp] += G[64 queries][16 targets] x T[16 targets][Cp] on
 // v_mfma_f32_32x32x16_bf16 (queries = M, channels = N, targets = K); G = the queries' window
-// gradients as bf16 hi + lo pairs (k_win_grad<R, true>).  The B operand needs consecutive targets
+// gradients as bf16 hi + lo pairs (k_win_grad_pairs).  The B operand needs consecutive targets
 // per lane: k_tile_targets first writes the packed targets as channel-major 16-z tiles.
 // ---------------------------------------------------------------------------------
 // Target tiles of the dQ kernel: per level row (y, x) and 8-aligned z start 8 k, the packed targets of z = 8 k ..
@@ -1639,17 +1646,18 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     const long long qz_lo = (long long)P.ntq * ngroups * 2048;
     const int fmt = mfma ? (F16 ? kGwF16 : kGwBf16) : kGwF32;
     const unsigned wgrid = (unsigned)((A.B * A.L * nqb + 3) / 4);
-    {
-        using WG = WinGradCfg<R>;
-        const unsigned wg_grid = (unsigned)((A.B * A.L * nqb + WG::WAVES - 1) / WG::WAVES);
+    {   // two lanes per query (k_win_grad_pairs)
+        using WG = WinGradPCfg<R>;
+        const long long nqb2 = (A.Nq + 31) / 32;
+        const unsigned wg_grid = (unsigned)((A.B * A.L * nqb2 + WG::WAVES - 1) / WG::WAVES);
         auto launch_wg = [&](auto kern) {
             (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, WG::LDS);
             kern<<<wg_grid, 64 * WG::WAVES, WG::LDS, s>>>(A);
         };
         switch (fmt) {
-        case kGwF16: launch_wg(k_win_grad<R, kGwF16>); break;
-        case kGwBf16: launch_wg(k_win_grad<R, kGwBf16>); break;
-        default: launch_wg(k_win_grad<R, kGwF32>); break;
+        case kGwF16: launch_wg(k_win_grad_pairs<R, kGwF16>); break;
+        case kGwBf16: launch_wg(k_win_grad_pairs<R, kGwBf16>); break;
+        default: launch_wg(k_win_grad_pairs<R, kGwF32>); break;
         }
     }
     if (!launched("win_grad")) return DVC_ERR_LAUNCH;
