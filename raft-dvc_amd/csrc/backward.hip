@@ -353,7 +353,10 @@ __global__ __launch_bounds__(256) void k_win_grad_pairs(BwdArgs A) {
         }
         __builtin_amdgcn_sched_barrier(0);
         load_row(i + 1, prev);
-        // flush the 32 queries' plane i: piece c = piece c % P16 of query c / P16 (out-of-range pieces: dropped)
+        // flush the 32 queries' plane i: piece c = piece c % P16 of query c / P16 (out-of-range pieces: dropped).
+        // A plane outside the level (ih + i not in [0, H_l)) is never read -- every consumer clips its union rows
+        // and target bricks to the level, and values a 16-byte read straddles into are dropped by a select -- so
+        // it is not written: ~150 MB less per backward at config #3, mostly levels 2-3, whose windows overhang.
         constexpr int NIT = (32 * P16 + 63) / 64, FG = 4;
 #pragma unroll
         for (int g0 = 0; g0 < NIT; g0 += FG) {
@@ -362,9 +365,10 @@ __global__ __launch_bounds__(256) void k_win_grad_pairs(BwdArgs A) {
 #pragma unroll
             for (int u = 0; u < FG; ++u) {
                 const int c = (g0 + u) * 64 + lane;
-                const bool ok = g0 + u < NIT && c < 32 * P16;
-                const int cc = ok ? c : 0;
+                const int cc = g0 + u < NIT && c < 32 * P16 ? c : 0;
                 const int qq = cc / P16, pc = cc - qq * P16;
+                const int ihq = __shfl(ih, qq);   // (lane qq holds query qq: ql = lane & 31)
+                const bool ok = g0 + u < NIT && c < 32 * P16 && (unsigned)(ihq + i) < (unsigned)Hl;
                 v[u] = *reinterpret_cast<const u32x4 *>(img + qq * SW + pc * 4);
                 off[u] = ok ? (qq * NW3 + i * NW * NW + pc * 4) * 4 : (int)kOff;
             }
