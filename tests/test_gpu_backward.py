@@ -254,3 +254,33 @@ def test_grad_valu_fallback(precision, tol):
         _check_golden("grad_cfg2", "gemm", precision, tol)
     finally:
         _lib.set_tuning("bwd_mfma", 1)
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_grad_stale_workspace(precision):
+    """The window-gradient planes outside a level are never written (k_win_grad_pairs) and the 16-byte gradient
+    reads of k_grad_q_mfma / k_grad_t_mfma straddle into neighbouring rows: no consumer may use such values.  The
+    caching allocator is filled with NaN / -7 / 3e4 before each call, so the workspace holds stale values; the
+    gradients (16^3, C = 128, L = 4, r = 4 with flows off the volume: coarse windows overhang their level) must be
+    finite and bitwise equal across the three poisons."""
+    from dvccorr import ops
+    S, C, L, r = 16, 128, 4, 4
+    seed = 4242
+    f1 = torch.from_numpy(prng.normal(seed, (1, C, S, S, S))).to(DEV)
+    f2 = torch.from_numpy(prng.normal(seed + 1, (1, C, S, S, S))).to(DEV)
+    coords = torch.from_numpy(prng.flow_coords(seed + 2, 1, S, S, S, r + 3.0)).to(DEV).reshape(1, 3, -1)
+    G = torch.from_numpy(prng.normal(seed + 3, (1, L * (2 * r + 1) ** 3, S ** 3))).to(DEV)
+    dt = ops.dtype_code(precision)
+    q = ops.pack_queries(f1.reshape(1, C, -1), dt)
+    t = ops.pack_targets(f2, L, dt)
+    nws = ops.lib().dvc_corr_backward_workspace_bytes(1, S ** 3, C, S, S, S, L, r)
+    outs = []
+    for val in (float("nan"), -7.0, 3.0e4):
+        poison = torch.full((2 * nws // 4 + (1 << 20),), val, device=DEV)
+        del poison
+        d1, d2 = ops.corr_backward(q, t, coords, G, C, S, S, S, L, r, False, dt)
+        torch.cuda.synchronize()
+        assert bool(torch.isfinite(d1).all()) and bool(torch.isfinite(d2).all()), (precision, val)
+        outs.append((d1.clone(), d2.clone()))
+    for d1, d2 in outs[1:]:
+        assert torch.equal(d1, outs[0][0]) and torch.equal(d2, outs[0][1]), precision
