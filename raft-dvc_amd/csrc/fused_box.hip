@@ -201,25 +201,22 @@ __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__re
 
         // ---------------- phase 1: window dots on MFMA ----------------
         if (ny > 0 && nx > 0 && nz > 0 && !(ABL & 2)) {
-            // this wave's iterations it = wave + NWAVES k over (row, z block), row-major,
-            // z block fastest; (by, bx, zb) advance without divisions
-            const int total = ny * nx * nzb;
-            const int nit = total > wave ? (total - wave + NWAVES - 1) / NWAVES : 0;
-            const int dzb = NWAVES % nzb, dblk = NWAVES / nzb;
+            // this wave's rows r = wave + NWAVES k of the union (row-major), each with all its z blocks in turn, so the
+            // epilogue's window-row test of a row serves every z block of it (round 4: it was dealt per (row, z
+            // block), the test redone for every block); (by, bx, zb) advance without divisions
+            const int nrows = ny * nx;
+            const int nit = nrows > wave ? (nrows - wave + NWAVES - 1) / NWAVES * nzb : 0;
             struct Pos { int by, bx, zb; };
             auto advance = [&](Pos &p) {
-                p.zb += dzb;
-                p.bx += dblk;
-                if (p.zb >= nzb) { p.zb -= nzb; p.bx += 1; }
+                if (++p.zb < nzb) return;
+                p.zb = 0;
+                p.bx += NWAVES;
                 while (p.bx >= nx) { p.bx -= nx; p.by += 1; }
             };
             Pos pl;   // position of the next load
-            {
-                const int blk = wave / nzb;
-                pl.zb = wave - blk * nzb;
-                pl.by = blk / nx;
-                pl.bx = blk - pl.by * nx;
-            }
+            pl.zb = 0;
+            pl.by = wave / nx;
+            pl.bx = wave - pl.by * nx;
             Pos pe = pl;   // position of the next epilogue
             // Every iteration issues its loads, past the wave's last block with an out-of-range offset (zeros, no
             // memory traffic): loads under a branch leave hipcc's waitcnt pass unsure how many younger loads
@@ -252,9 +249,15 @@ __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__re
                     for (int j = 0; j < 4; ++j)
                         acc[j] = E16<E>::mma(a[ks], bq[j][ks], acc[j]);
             };
+            bool rowok[4] = {false, false, false, false};   // this lane's queries' windows contain the current row
             auto epilogue = [&](const f32x4 (&acc)[4]) {
                 const int z0 = zs + 16 * pe.zb;
                 const int y = ys + pe.by, x = xs + pe.bx;
+                if (pe.zb == 0) {   // (uniform) a new row
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        rowok[j] = (unsigned)(y - oh[j]) < (unsigned)NW && (unsigned)(x - ou[j]) < (unsigned)NW;
+                }
                 advance(pe);
                 const int rowu = (y * NW + x) * C::WROW + z0 * 2;
 #pragma unroll
@@ -267,7 +270,7 @@ __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__re
                         sink ^= p01 ^ p23;
                         continue;
                     }
-                    const bool rok = (unsigned)(y - oh[j]) < (unsigned)NW && (unsigned)(x - ou[j]) < (unsigned)NW;
+                    const bool rok = rowok[j];
                     const int t0 = z0 - ov[j];                   // stored-row offset of this lane's first pair
                     const int base = wb[j] + rowu;
                     const int a0 = rok && (unsigned)t0 <= (unsigned)NW ? base : trash;
