@@ -54,9 +54,28 @@ def test_grad_golden(case, kind):
 # r = 4 (the shapes k_grad_q_mfma / k_grad_t_mfma are benchmarked at, with more than one split per level).
 @pytest.mark.parametrize("kind", ["gemm", "fused"])
 @pytest.mark.parametrize("precision,tol", [("bf16", BF16_TOL), ("fp16", FP16_TOL)])
-@pytest.mark.parametrize("case", ["grad_cfg2", "grad_edge_888_L4_r4", "grad_legacy_cube_L3_r2"])
+@pytest.mark.parametrize("case", ["grad_cfg2", "grad_edge_888_L4_r4", "grad_legacy_cube_L3_r2", "grad_equiv_L2_r4_rand"])
 def test_grad_golden_low_precision(case, kind, precision, tol):
     _check_golden(case, kind, precision, tol)
+
+
+@pytest.mark.parametrize("legacy", [False, True])
+def test_grad_batch2_matrix_cores(legacy):
+    """Batch 2 through the bf16 / fp16 MFMA gradient kernels (every (batch, level) pair is its own GEMM / window
+    set): ragged 12 x 10 x 16 volumes, C = 128, L = 3, r = 4, flows that leave the volume, a different G per item."""
+    B, (H, W, D), C, L, r = 2, (12, 10, 16), 128, 3, 4
+    seed = 9100 + int(legacy)
+    f1 = prng.normal(seed, (B, C, H, W, D))
+    f2 = prng.normal(seed + 1, (B, C, H, W, D))
+    coords = prng.flow_coords(seed + 2, B, H, W, D, r + 3.0)
+    G = prng.normal(seed + 3, (B, L * (2 * r + 1) ** 3, H, W, D))
+    ref1, ref2 = oracle_grads(f1, f2, coords, G, L, r, legacy)
+    for precision, tol in (("bf16", BF16_TOL), ("fp16", FP16_TOL)):
+        for kind in ("gemm", "fused"):
+            d1, d2 = _gpu_grads(kind, f1, f2, coords, G, L, r, legacy, precision=precision)
+            for b in range(B):   # per item, so a batch-offset bug cannot hide behind the other item's scale
+                e1, e2 = orc.rel_err(d1[b], ref1[b]), orc.rel_err(d2[b], ref2[b])
+                assert e1 <= tol and e2 <= tol, (kind, precision, legacy, b, e1, e2)
 
 
 def _check_golden(case, kind, precision, tol):
