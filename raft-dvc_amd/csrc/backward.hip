@@ -103,6 +103,9 @@ __device__ __forceinline__ int xcd_block(int i, int n) {
 #ifndef DVC_GQ_XCD
 #define DVC_GQ_XCD 0    // k_grad_q_mfma: boxes per XCD run (0: one contiguous run per XCD)
 #endif
+#ifndef DVC_GQ_SORT
+#define DVC_GQ_SORT 2   // k_grad_q_mfma: levels 0 .. DVC_GQ_SORT - 1 over origin-sorted query groups (0: 4^3 boxes)
+#endif
 template <int C> __device__ __forceinline__ int xcd_block_grouped(int i, int n) {
     if (i >= n / (8 * C) * (8 * C)) return i;
     const int x = i & 7, slot = i >> 3;
@@ -734,9 +737,22 @@ __device__ __forceinline__ bf16x8 dup_bf16x4(u32x2 v) {
 // SPLIT (fp32 blocks, round 4): the targets as bf16 hi/lo tiles (k_tile_targets<float>, the lo tiles tz_lo elements
 // after the hi ones); every batch stages both and runs the MFMAs on each, so dQ = sum (G_hi + G_lo) (T_hi + T_lo):
 // every product of the 16-bit pieces, ~2^-17 of each operand left out (the fp32 tolerance, 1e-5, holds with room).
+//
+// Origin-sorted groups (round 4): levels 0 .. nsl - 1 of batch element bsort, grid row blockIdx.y = the level: block t
+// of the row takes the 64 queries at sorted positions [64 t, 64 t + 64) of that level's window-origin order (skeys:
+// k_bw_keys + the radix sort; level l's Nq keys are the l-th Nq sorted ones, the queries whose windows miss the level
+// last), so the union of a group's windows is that of ~2 origin columns instead of a 4^3 box spread by the flows:
+// -28 % (level 0) and -29 % (level 1) batches at config #3 (+-2 voxel random flows).  The window gradients are
+// addressed from the level's first query (the host takes this path only where that range fits the descriptor:
+// gq_sorted_fits) and dQ is scattered per query.  The other blocks are boxes: row nsl = levels [lfirst, L) of batch
+// element bsort (lfirst = nsl > 0, launched after the sort beside the sorted groups so that one launch fills the
+// chip), or every batch element's boxes over the gridDim.y level groups (lfirst = 0, nsl = 0).  Partial sums: sorted
+// level l slot l, boxes with lfirst > 0 slot lfirst, else slot blockIdx.y.
 template <int NCT, bool F16, bool SPLIT = false>   // channel tiles of 32 (C_pad / 32, <= 4 per launch); fp16 operands
 __global__ __launch_bounds__(256, kQOcc<SPLIT>) void k_grad_q_mfma(const bf16_t *__restrict__ Tz, float *__restrict__ dQp,
-                                                        long long part_stride, BwdArgs A, long long tz_lo) {
+                                                        long long part_stride, BwdArgs A, long long tz_lo,
+                                                        const unsigned long long *__restrict__ skeys, int bsort,
+                                                        int ns, int nsl, int lfirst) {
     // bytes per stage: T tile (4 KB, 16-bit) + G tile (4 KB, hi/lo pairs) [+ T lo tile (4 KB)]
     constexpr int STAGE = SPLIT ? 12288 : 8192;
     __shared__ __attribute__((aligned(16))) unsigned char stg[kQStages * STAGE];
@@ -744,25 +760,43 @@ __global__ __launch_bounds__(256, kQOcc<SPLIT>) void k_grad_q_mfma(const bf16_t 
     const int tid = threadIdx.x, lane = tid & 63, m = lane & 31, h = lane >> 5;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nbz = (A.Dq + 3) >> 2, nbx = (A.Wq + 3) >> 2, nby = (A.Hq + 3) >> 2;
-    // (XCD runs of boxes: neighbours share target tiles)
+    // (XCD runs of blocks: neighbours share target tiles)
     int t;
     if constexpr (DVC_GQ_XCD > 0) t = xcd_block_grouped<DVC_GQ_XCD>((int)blockIdx.x, (int)gridDim.x);
     else t = xcd_block((int)blockIdx.x, (int)gridDim.x);
-    const int bz = t % nbz; t /= nbz;
-    const int bx = t % nbx; t /= nbx;
-    const int by = t % nby;
-    const int b = t / nby;
-    // level groups (gridDim.y = grad_q_parts(L)): 1 -- every level; 2 -- level 0, then levels 1 .. L-1; 3 -- the
-    // first and second half of level 0's union rows, then levels 1 .. L-1
+    // a sorted launch (nsl > 0): row blockIdx.y < nsl = the sorted groups of level blockIdx.y, row nsl = the boxes of
+    // levels [nsl, L); each row's blocks are dealt over the XCDs on their own, so every XCD gets a share of each
     const int np = gridDim.y, py = blockIdx.y;
-    const int lg0 = np == 1 || py < np - 1 ? 0 : 1;
-    const int lg1 = np == 1 ? A.L : (py < np - 1 ? 1 : A.L);
-    const int rhalf = np == 3 && py < 2 ? py + 1 : 0;   // 1 / 2: first / second half of level 0's rows
-    // lane-as-query view (union bounds, row list): query i = lane of the box
-    const int qy = by * 4 + (lane >> 4), qx = bx * 4 + ((lane >> 2) & 3), qz = bz * 4 + (lane & 3);
-    const bool active = qy < A.Hq && qx < A.Wq && qz < A.Dq;
-    const long long qb0 = ((long long)by * 4 * A.Wq + bx * 4) * A.Dq + bz * 4;   // the box's first query
-    const int qrel = active ? (int)(((long long)qy * A.Wq + qx) * A.Dq + qz - qb0) : 0;
+    const bool srt = nsl > 0 && py < nsl;
+    if (nsl > 0 && t >= (srt ? ns : nbz * nbx * nby)) return;   // (the rows are as long as the longest)
+    const int ls = srt ? py : 0;   // a sorted group's level
+    int by = 0, bx = 0, bz = 0, b = bsort;
+    if (!srt) {
+        bz = t % nbz; t /= nbz;
+        bx = t % nbx; t /= nbx;
+        by = t % nby;
+        if (bsort < 0) b = t / nby;
+    }
+    // box launches: level groups (gridDim.y = grad_q_parts(L)): 1 -- every level; 2 -- level 0, then levels 1 .. L-1;
+    // 3 -- the first and second half of level 0's union rows, then levels 1 .. L-1
+    const int lg0 = srt ? ls : lfirst > 0 ? lfirst : (np == 1 || py < np - 1 ? 0 : 1);
+    const int lg1 = srt ? ls + 1 : lfirst > 0 ? A.L : (np == 1 ? A.L : (py < np - 1 ? 1 : A.L));
+    const int rhalf = !srt && lfirst == 0 && np == 3 && py < 2 ? py + 1 : 0;   // 1 / 2: level 0's row halves
+    // lane-as-query view (union bounds, row list): query i = lane of the box / sorted group, qrel its offset from
+    // qb0 (the box's first query; sorted groups: query 0)
+    int qrel;
+    bool active;
+    long long qb0 = 0;
+    if (srt) {
+        const long long si = (long long)t * 64 + lane;
+        active = si < A.Nq;
+        qrel = active ? (int)(unsigned)skeys[(long long)ls * A.Nq + si] : 0;
+    } else {
+        const int qy = by * 4 + (lane >> 4), qx = bx * 4 + ((lane >> 2) & 3), qz = bz * 4 + (lane & 3);
+        active = qy < A.Hq && qx < A.Wq && qz < A.Dq;
+        qb0 = ((long long)by * 4 * A.Wq + bx * 4) * A.Dq + bz * 4;
+        qrel = active ? (int)(((long long)qy * A.Wq + qx) * A.Dq + qz - qb0) : 0;
+    }
     float cy = 0.0f, cx = 0.0f, cz = 0.0f;
     if (active) load_coords(A.coords, b, A.Nq, qb0 + qrel, cy, cx, cz);
     // T DMA: the batch's 4 KB target tile (k_tile_targets) as it stands, 16 bytes per thread
@@ -800,9 +834,9 @@ __global__ __launch_bounds__(256, kQOcc<SPLIT>) void k_grad_q_mfma(const bf16_t 
         // base 16 bytes early: a 16-byte chunk may start up to 3 values before a window row (those values, like the
         // ones past its end, belong to other rows and are masked when the operand is read)
         const int nw3 = (int)bw_nw3(A, l);
+        const long long gspan = srt ? A.Nq : 3LL * A.Wq * A.Dq + 3 * A.Dq + 4;   // queries the buffer covers
         const u32x4 rs_g = sgpr_rsrc(A.gwin + A.goff[l] + ((long long)b * A.Nq + qb0) * nw3 - 4,
-                                     (unsigned)min((long long)(3 * A.Wq * A.Dq + 3 * A.Dq + 4) * nw3 * 4 + 32,
-                                                   0x7fffffffLL));
+                                     (unsigned)min(gspan * nw3 * 4 + 32, 0x7fffffffLL));
         // this thread's G chunk (round 4: one 16-byte DMA per thread and batch, was four 4-byte ones -- the texture
         // addresser's instruction count bound the kernel): query gq = 16 w + lane / 4, physical chunk lane & 3 of its
         // 64-byte row = logical z chunk (lane & 3) ^ (gq >> 2 & 3)
@@ -836,7 +870,7 @@ __global__ __launch_bounds__(256, kQOcc<SPLIT>) void k_grad_q_mfma(const bf16_t 
             if (!(DVC_GQ_ABL & 2)) {
                 const int wy = y - goh, wx = x - gou, wz = z0 - gov;
                 const bool ok = (unsigned)wy < (unsigned)nh && (unsigned)wx < (unsigned)nu && wz > -4 && wz < nv;
-                blds(rs_g, ok ? (unsigned)((gqo + (wy * nu + wx) * nv + wz) * 4 + 16) : kOOB, 0u, sb + 4096 + 1024 * w,
+                blds(rs_g, ok ? (unsigned)(gqo + (wy * nu + wx) * nv + wz) * 4u + 16u : kOOB, 0u, sb + 4096 + 1024 * w,
                      W16{});
             }
         };
@@ -909,7 +943,20 @@ __global__ __launch_bounds__(256, kQOcc<SPLIT>) void k_grad_q_mfma(const bf16_t 
     }
     if (w >= NCT) return;
     // acc[T][i] = D[query 32 T + 8 (i / 4) + 4 h + i % 4][channel 32 w + m]
-    float *dq = dQp + (long long)blockIdx.y * part_stride;
+    float *dq = dQp + (long long)(srt ? ls : lfirst > 0 ? lfirst : (int)blockIdx.y) * part_stride;
+    if (srt) {
+        const long long s0 = (long long)t * 64;
+#pragma unroll
+        for (int T = 0; T < 2; ++T)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int qi = 32 * T + 8 * (i >> 2) + 4 * h + (i & 3);
+                const int q = __shfl(qrel, qi);   // (every lane: a shuffle under a branch reads 0 from idle lanes)
+                if (s0 + qi < A.Nq)
+                    dq[((long long)b * A.Nq + q) * A.Cp + A.cbase + 32 * w + m] = acc[T][i] * A.scale;
+            }
+        return;
+    }
 #pragma unroll
     for (int T = 0; T < 2; ++T)
 #pragma unroll
@@ -1520,6 +1567,10 @@ static int grad_t_splits(const dvc_layout &lay, int l, long long Nq) {
 #define DVC_GQ_PARTS 2
 #endif
 static int grad_q_parts(int L) { return L > 1 ? DVC_GQ_PARTS : 1; }
+// origin-sorted levels of k_grad_q_mfma and its partial-sum slots then (one per sorted level + one for the boxes)
+static_assert(DVC_GQ_SORT >= 0 && DVC_GQ_SORT <= 2, "k_unpack_sum adds at most 3 partial sums");
+static int gq_sort_levels(int L) { return std::min(L, DVC_GQ_SORT); }
+static int gq_sorted_slots(int L) { return gq_sort_levels(L) + (L > gq_sort_levels(L) ? 1 : 0); }
 
 static long long level_cells(const dvc_layout &lay, int l, const int nw[3]) {
     return (long long)(lay.H[l] + nw[0] - 1) * (lay.W[l] + nw[1] - 1) * (lay.D[l] + nw[2] - 1);
@@ -1549,7 +1600,7 @@ static void bwd_plan(int B, long long Nq, const dvc_layout &lay, int radius, boo
     P.gwin = al256(gw) + 512;   // + 256-byte guards before and after (k_grad_q_mfma's 8-float loads)
     // partial dQ per k_grad_q_mfma level group; the workspace query has no dtype, so this covers the MFMA path
     // (the VALU kernels of fp32 blocks use the first part only)
-    P.dq = al256((size_t)grad_q_parts(L) * B * Nq * lay.c_pad * sizeof(float));
+    P.dq = al256((size_t)std::max(grad_q_parts(L), gq_sorted_slots(L)) * B * Nq * lay.c_pad * sizeof(float));
     P.dt = al256((size_t)B * lay.row_stride * lay.c_pad * sizeof(float));
     P.keys = al256((size_t)nkeys * sizeof(unsigned long long));
     P.starts = al256((size_t)(cells + 1) * sizeof(int));
@@ -1591,6 +1642,14 @@ static bool mfma_offsets_fit(const BwdArgs &A, const BwdPlan &P) {
     const long long span = 3LL * A.Wq * A.Dq + 3LL * A.Dq + 4;
     for (int l = 0; l < A.L; ++l)
         if (span * ((long long)A.nwh[l] * A.nwu[l] * A.nwv[l]) * 4 + 32 > lim) return false;   // (+32: rs_g's slack)
+    return true;
+}
+
+// k_grad_q_mfma's origin-sorted groups: levels 0 .. nsl - 1, each level's window gradients of one batch element as
+// one descriptor
+static bool gq_sorted_fits(const BwdArgs &A, int nsl) {
+    for (int l = 0; l < nsl; ++l)
+        if (A.Nq * ((long long)A.nwh[l] * A.nwu[l] * A.nwv[l]) * 4 + 32 > 0x7fffffffLL) return false;
     return true;
 }
 
@@ -1677,8 +1736,27 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     }
     const long long boxes = (long long)A.B * ((A.Hq + 3) / 4) * ((A.Wq + 3) / 4) * ((A.Dq + 3) / 4);
     // partial dQ per level group of the MFMA path (qparts of them, qstride floats apart)
-    const int qparts = mfma ? grad_q_parts(A.L) : 1;
+    // levels 0 .. nsl - 1's dQ from origin-sorted query groups (k_grad_q_mfma, nsl > 0) where their window gradients
+    // fit one descriptor each
+    const int nsl = gq_sort_levels(A.L);
+    const bool qsorted = mfma && nsl > 0 && gq_sorted_fits(A, nsl);
+    const int qparts = mfma ? (qsorted ? gq_sorted_slots(A.L) : grad_q_parts(A.L)) : 1;
     const long long qstride = (long long)A.B * A.Nq * A.Cp;
+    // one k_grad_q_mfma launch per 128-channel group: grid, sorted keys and batch element (or -1: every batch
+    // element's boxes), sorted groups per level and sorted levels at the start of the grid, first level of the
+    // boxes (0: the level groups)
+    auto launch_q = [&](dim3 grid, const unsigned long long *sk, int bs, int ns, int nsl_, int lfirst) {
+        for (int g = 0; g < ngroups; ++g) {
+            BwdArgs Ag = A;
+            Ag.cbase = 128 * g;
+            switch (std::min(128, A.Cp - Ag.cbase) / 32) {
+            case 1: k_grad_q_mfma<1, F16, SPLIT><<<grid, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo, sk, bs, ns, nsl_, lfirst); break;
+            case 2: k_grad_q_mfma<2, F16, SPLIT><<<grid, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo, sk, bs, ns, nsl_, lfirst); break;
+            case 3: k_grad_q_mfma<3, F16, SPLIT><<<grid, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo, sk, bs, ns, nsl_, lfirst); break;
+            default: k_grad_q_mfma<4, F16, SPLIT><<<grid, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo, sk, bs, ns, nsl_, lfirst); break;
+            }
+        }
+    };
     bool done_q = false;
     if constexpr (k16) {
         if (mfma) {
@@ -1690,17 +1768,8 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
                 k_tile_targets<bf16_t><<<dim3((unsigned)P.tz0[A.L], (unsigned)ngroups, (unsigned)A.B), 256, 0, s>>>(
                     reinterpret_cast<const bf16_t *>(Tt), ttr, A, 0);
             if (!launched("tile_targets")) return DVC_ERR_LAUNCH;
-            const dim3 qg((unsigned)boxes, (unsigned)qparts);   // level groups: {0}, {1 .. L-1}
-            for (int g = 0; g < ngroups; ++g) {
-                BwdArgs Ag = A;
-                Ag.cbase = 128 * g;
-                switch (std::min(128, A.Cp - Ag.cbase) / 32) {
-                case 1: k_grad_q_mfma<1, F16, SPLIT><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo); break;
-                case 2: k_grad_q_mfma<2, F16, SPLIT><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo); break;
-                case 3: k_grad_q_mfma<3, F16, SPLIT><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo); break;
-                default: k_grad_q_mfma<4, F16, SPLIT><<<qg, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo); break;
-                }
-            }
+            // (qsorted: after each batch element's sort, below)
+            if (!qsorted) launch_q(dim3((unsigned)boxes, (unsigned)qparts), nullptr, -1, 0, 0, 0);
             done_q = true;
         }
     }
@@ -1746,6 +1815,13 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
         }
         k_cell_starts<<<(unsigned)((ncell + 1 + 255) / 256), 256, 0, s>>>(kout, nkeys, ncell, starts);
         if (!launched("cell_starts")) return DVC_ERR_LAUNCH;
+        if (qsorted) {   // level l's keys are the l-th Nq sorted ones (its cells come after level l - 1's); the
+                         // coarser levels' boxes of this batch element in the same launch
+            const int ns = (int)((A.Nq + 63) / 64);
+            launch_q(dim3((unsigned)std::max<long long>(ns, A.L > nsl ? boxes / A.B : 0),
+                          (unsigned)(nsl + (A.L > nsl ? 1 : 0))), kout, b, ns, nsl, nsl);
+            if (!launched("grad_q_sorted")) return DVC_ERR_LAUNCH;
+        }
         if (nblk == 0) continue;
         bool done_t = false;
         if constexpr (k16) {
