@@ -1452,19 +1452,22 @@ struct UnpackArgs {
 // issued before the first sum (unconditionally: a slot outside its level reads the voxel's own row 0 and is
 // dropped by a select), with 32-bit coordinates -- the round-3 loop (runtime slot / partial loops, 64-bit
 // divisions per voxel) waited for each load in turn: 33 us per unpack at config #3.
+// Round 4, last: a thread loads 4 channels (16 bytes) of 4 voxels instead of 1 channel of 16, a quarter of the load
+// instructions -- the unpack issued one dword load per (voxel, channel, slot, partial) and was bound by their issue:
+// 25 us (4 slots) / 15.5 us (3 partials) at config #3.
 template <int NS, int NSUM>
 __global__ __launch_bounds__(256) void k_unpack_sum(UnpackArgs U) {
     __shared__ float tile[64][65];
     const int b = blockIdx.z, c0 = blockIdx.y * 64;
     const long long v0 = (long long)blockIdx.x * 64;
     const float *src = U.src + (long long)b * U.src_bstride * U.Cp;
-    const int c = threadIdx.x & 63, vq = threadIdx.x >> 6;   // channel c0 + c; voxels v0 + 4 k + vq
-    const bool cin = c0 + c < U.C;
-    float val[16][NS][NSUM];
-    bool ok[16][NS];
+    const int cq = threadIdx.x & 15, vs = threadIdx.x >> 4;   // channels c0 + 4 cq .. + 3; voxels v0 + 16 k + vs
+    const bool cin = c0 + 4 * cq < U.Cp;                     // (Cp is a multiple of 4: the quad is in the row)
+    f32x4 val[4][NS][NSUM];
+    bool ok[4][NS];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const long long v = v0 + 4 * k + vq;
+    for (int k = 0; k < 4; ++k) {
+        const long long v = v0 + 16 * k + vs;
         const bool vin = v < U.N && cin;
         const unsigned vv = vin ? (unsigned)v : 0u;   // (N < 2^31)
         const unsigned yx = vv / (unsigned)U.D, z = vv - yx * (unsigned)U.D;
@@ -1474,23 +1477,25 @@ __global__ __launch_bounds__(256) void k_unpack_sum(UnpackArgs U) {
             const unsigned py = y >> l, px = x >> l, pz = z >> l;
             ok[k][l] = vin && py < (unsigned)U.Hs[l] && px < (unsigned)U.Ws[l] && pz < (unsigned)U.Ds[l];
             const long long row = ok[k][l] ? U.offs[l] + ((long long)py * U.Ws[l] + px) * U.Dps[l] + pz : 0;
-            const float *p = src + row * U.Cp + (cin ? c0 + c : 0);
+            const float *p = src + row * U.Cp + (cin ? c0 + 4 * cq : 0);
 #pragma unroll
-            for (int k2 = 0; k2 < NSUM; ++k2) val[k][l][k2] = p[k2 * U.sstride];
+            for (int k2 = 0; k2 < NSUM; ++k2) val[k][l][k2] = *reinterpret_cast<const f32x4 *>(p + k2 * U.sstride);
         }
     }
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        float sum = 0.0f;
+    for (int k = 0; k < 4; ++k)
 #pragma unroll
-        for (int l = 0; l < NS; ++l) {
-            float v = val[k][l][0];
+        for (int j = 0; j < 4; ++j) {
+            float sum = 0.0f;
 #pragma unroll
-            for (int k2 = 1; k2 < NSUM; ++k2) v += val[k][l][k2];
-            sum += ok[k][l] ? U.wts[l] * v : 0.0f;
+            for (int l = 0; l < NS; ++l) {
+                float v = val[k][l][0][j];
+#pragma unroll
+                for (int k2 = 1; k2 < NSUM; ++k2) v += val[k][l][k2][j];
+                sum += ok[k][l] ? U.wts[l] * v : 0.0f;
+            }
+            tile[16 * k + vs][4 * cq + j] = sum;
         }
-        tile[4 * k + vq][c] = sum;
-    }
     __syncthreads();
 #pragma unroll 4
     for (int k = 0; k < 16; ++k) {
