@@ -1164,47 +1164,69 @@ __global__ __launch_bounds__(256) void k_grad_t(const TT *__restrict__ Qp, const
 // positions from every 8-aligned start, [128 ch][16] bf16 = 4 KB (the halves of channel c swapped when
 // (c >> 3) & 1), so a batch's B operand is one contiguous tile.
 // ---------------------------------------------------------------------------------
-// fp32 queries (TT = float): hi tiles into Qz, lo tiles into Qz + lo (elements), as k_tile_targets<float>
+// fp32 queries (TT = float): hi tiles into Qz, lo tiles into Qz + lo (elements), as k_tile_targets<float>.
+// Round 4: kQtPer tiles per workgroup, every key and row load issued before the first is used -- one tile per
+// workgroup paid two dependent round trips (key, then row) for 4 KB (22.8 us at config #3).
+constexpr int kQtPer = 4;
 template <typename TT>
 __global__ __launch_bounds__(256) void k_qt_tiles(const TT *__restrict__ Q, const unsigned long long *__restrict__ keys,
                                                   bf16_t *__restrict__ Qz, long long Nq, long long nkeys, int Cp, int b,
-                                                  long long lo) {
+                                                  long long lo, long long ntq) {
     constexpr bool SPLIT = std::is_same<TT, float>::value;
-    __shared__ __attribute__((aligned(16))) bf16_t tile[SPLIT ? 2 : 1][16][128 + 8];
-    const long long t = blockIdx.x, ntq = gridDim.x;
+    constexpr int NS = SPLIT ? 2 : 1;
+    __shared__ __attribute__((aligned(16))) bf16_t tile[kQtPer][NS][16][128 + 8];
+    const long long t0 = (long long)blockIdx.x * kQtPer;
     const int g = blockIdx.y, cb = 128 * g, cg = min(128, Cp - cb);
     {
         const int r = threadIdx.x >> 4, ch = threadIdx.x & 15;   // 16 sorted positions x 16 chunks of 8 channels
-        const long long i = 8 * t + r;
-        const bool in = i < nkeys && 8 * ch < cg;
-        const TT *row = Q + ((long long)b * Nq + (in ? (long long)(keys[i] & 0xffffffffull) : 0)) * Cp + cb + 8 * ch;
+        long long qi[kQtPer];
+        bool in[kQtPer];
+#pragma unroll
+        for (int k = 0; k < kQtPer; ++k) {
+            const long long i = 8 * (t0 + k) + r;
+            in[k] = t0 + k < ntq && i < nkeys && 8 * ch < cg;
+            qi[k] = in[k] ? (long long)(keys[i] & 0xffffffffull) : 0;
+        }
         if constexpr (SPLIT) {
-            f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = v0;
-            if (in) {
-                v0 = *reinterpret_cast<const f32x4 *>(row);
-                v1 = *reinterpret_cast<const f32x4 *>(row + 4);
+            f32x4 v0[kQtPer], v1[kQtPer];
+#pragma unroll
+            for (int k = 0; k < kQtPer; ++k) {
+                const TT *row = Q + ((long long)b * Nq + qi[k]) * Cp + cb + 8 * ch;
+                v0[k] = in[k] ? *reinterpret_cast<const f32x4 *>(row) : f32x4{0.f, 0.f, 0.f, 0.f};
+                v1[k] = in[k] ? *reinterpret_cast<const f32x4 *>(row + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
             }
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                split_bf16(v0[k], tile[0][r][8 * ch + k], tile[1][r][8 * ch + k]);
-                split_bf16(v1[k], tile[0][r][8 * ch + 4 + k], tile[1][r][8 * ch + 4 + k]);
-            }
+            for (int k = 0; k < kQtPer; ++k)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    split_bf16(v0[k][e], tile[k][0][r][8 * ch + e], tile[k][1][r][8 * ch + e]);
+                    split_bf16(v1[k][e], tile[k][0][r][8 * ch + 4 + e], tile[k][1][r][8 * ch + 4 + e]);
+                }
         } else {
-            u32x4 v = {0u, 0u, 0u, 0u};
-            if (in) v = *reinterpret_cast<const u32x4 *>(row);
-            *reinterpret_cast<u32x4 *>(&tile[0][r][8 * ch]) = v;
+            u32x4 v[kQtPer];
+#pragma unroll
+            for (int k = 0; k < kQtPer; ++k) {
+                const TT *row = Q + ((long long)b * Nq + qi[k]) * Cp + cb + 8 * ch;
+                v[k] = in[k] ? *reinterpret_cast<const u32x4 *>(row) : u32x4{0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (int k = 0; k < kQtPer; ++k) *reinterpret_cast<u32x4 *>(&tile[k][0][r][8 * ch]) = v[k];
         }
     }
     __syncthreads();
     const int c = threadIdx.x >> 1, hh = threadIdx.x & 1;
-    bf16_t *dst = Qz + ((long long)g * ntq + t) * 2048 + c * 16 + 8 * (hh ^ ((c >> 3) & 1));
 #pragma unroll
-    for (int s = 0; s < (SPLIT ? 2 : 1); ++s) {
-        unsigned w[4];
+    for (int k = 0; k < kQtPer; ++k) {
+        if (t0 + k >= ntq) break;
+        bf16_t *dst = Qz + ((long long)g * ntq + t0 + k) * 2048 + c * 16 + 8 * (hh ^ ((c >> 3) & 1));
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            w[i] = (unsigned)tile[s][8 * hh + 2 * i][c] | ((unsigned)tile[s][8 * hh + 2 * i + 1][c] << 16);
-        *reinterpret_cast<u32x4 *>(dst + s * lo) = u32x4{w[0], w[1], w[2], w[3]};
+        for (int s = 0; s < NS; ++s) {
+            unsigned w[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                w[i] = (unsigned)tile[k][s][8 * hh + 2 * i][c] | ((unsigned)tile[k][s][8 * hh + 2 * i + 1][c] << 16);
+            *reinterpret_cast<u32x4 *>(dst + s * lo) = u32x4{w[0], w[1], w[2], w[3]};
+        }
     }
 }
 
@@ -1833,11 +1855,11 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
             if (mfma) {
                 // matrix-core path: sorted + transposed query rows, then 16-query MFMA batches
                 if constexpr (SPLIT)
-                    k_qt_tiles<float><<<dim3((unsigned)P.ntq, (unsigned)ngroups), 256, 0, s>>>(
-                        Q, kout, qt, A.Nq, nkeys, A.Cp, b, qz_lo);
+                    k_qt_tiles<float><<<dim3((unsigned)((P.ntq + kQtPer - 1) / kQtPer), (unsigned)ngroups), 256, 0, s>>>(
+                        Q, kout, qt, A.Nq, nkeys, A.Cp, b, qz_lo, P.ntq);
                 else
-                    k_qt_tiles<bf16_t><<<dim3((unsigned)P.ntq, (unsigned)ngroups), 256, 0, s>>>(
-                        reinterpret_cast<const bf16_t *>(Q), kout, qt, A.Nq, nkeys, A.Cp, b, 0);
+                    k_qt_tiles<bf16_t><<<dim3((unsigned)((P.ntq + kQtPer - 1) / kQtPer), (unsigned)ngroups), 256, 0, s>>>(
+                        reinterpret_cast<const bf16_t *>(Q), kout, qt, A.Nq, nkeys, A.Cp, b, 0, P.ntq);
                 if (!launched("qt_tiles")) return DVC_ERR_LAUNCH;
                 for (int cg = 0; cg < ngroups; ++cg) {
                     BwdArgs Ag = A;
