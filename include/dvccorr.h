@@ -178,12 +178,18 @@ int dvc_corr_backward(const void *packed_q, const void *packed_t, const float *c
                       float *grad_fmap1, float *grad_fmap2, void *workspace, int B, int64_t Nq, int C, int H, int W,
                       int D, int num_levels, int radius, int convention, int dtype, void *stream);
 /* Pure host function: 1 when dvc_corr_backward runs this shape's gradient sums on the matrix cores
- * (bf16 operands on v_mfma_f32_32x32x16_bf16, fp16 on _f16, the window gradients entering as hi/lo
- * pairs), 0 when it takes the VALU kernels (fp32 operands, or a volume whose MFMA-kernel buffer
- * offsets would exceed 31 bits: level-0 fmaps of about 154^3 and up).  Same results either way within
- * the dtype's tolerance. */
+ * (bf16 operands on v_mfma_f32_32x32x16_bf16, fp16 on _f16, fp32 operands split into bf16 hi/lo
+ * tiles and multiplied twice, ~2^-16 relative per operand; the window gradients entering as hi/lo
+ * pairs), 0 when it takes the VALU kernels (a volume whose MFMA-kernel buffer offsets would exceed
+ * 31 bits: level-0 fmaps of about 154^3 and up).  The answer also follows the CALLING THREAD's
+ * dvc_set_tuning("bwd_mfma", v) knob (0: VALU kernels for every dtype).  Same results either way
+ * within the dtype's tolerance. */
 int dvc_corr_backward_mfma(int B, int64_t Nq, int C, int H, int W, int D, int num_levels, int radius, int convention,
                            int dtype);
+/* Pure host function: 1 when the window-gradient pass of dvc_corr_backward reads grad_out through
+ * 64-bit addresses because one output row of (2r+1)^2 channels spans more than 2^31 - 1 bytes
+ * ((2r+1)^2 * 4 * Nq; Nq > ~6.6 M at r = 4), 0 when it uses 32-bit buffer offsets.  Same values. */
+int dvc_corr_backward_gout64(int64_t Nq, int radius);
 
 /* Lookup with the motion encoder's convc1 (1x1x1 Conv3d L*(2r+1)^3 -> 96, + ReLU,
  * update.py:222, 246) fused into its epilogue: the L*(2r+1)^3-channel lookup output

@@ -235,7 +235,10 @@ template <int R> struct WinGradPCfg {
     static constexpr int WAVES = 4;
     static constexpr int LDS = WAVES * 32 * SW * 4;
 };
-template <int R, int FMT>
+// G64: the output-gradient row a spans n^2 Nq floats; where n^2 * 4 Nq passes 2^31 - 1 (Nq > ~6.6 M at
+// r = 4) the buffer offsets of the row descriptor would wrap, so those volumes read the row through 64-bit addresses
+// (same values, same arithmetic; win_grad_needs_g64 on the host picks it).
+template <int R, int FMT, bool G64 = false>
 __global__ __launch_bounds__(256) void k_win_grad_pairs(BwdArgs A) {
     using G = WinGradPCfg<R>;
     constexpr int n = 2 * R + 1, NW = G::NW, NW3 = NW * NW * NW, SW = G::SW, P16 = NW * NW / 4, HC = G::HC;
@@ -298,6 +301,21 @@ __global__ __launch_bounds__(256) void k_win_grad_pairs(BwdArgs A) {
     }
     float rowA[NCOL][n], rowB[NCOL][n];
     auto load_row = [&](int a, float (&dst)[NCOL][n]) {   // a = n: an empty descriptor (zeros, unconditional loads)
+        if constexpr (G64) {
+            const float *ga = gbl + (long long)min(a, n - 1) * n * n * A.Nq + qc;
+#pragma unroll
+            for (int c = 0; c < NCOL; ++c) {
+                const int u = U0 + c;
+                const bool ok = a < n && (unsigned)u < (unsigned)n;
+                const long long cu = (long long)(ok ? u : 0) * chu;
+#pragma unroll
+                for (int v = 0; v < n; ++v) {
+                    const float x = ga[(cu + v * chv) * A.Nq];
+                    dst[c][v] = ok ? x : 0.0f;
+                }
+            }
+            return;
+        }
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             (void *)(gbl + (long long)min(a, n - 1) * n * n * A.Nq), (short)0,
             a < n ? (int)min((long long)n * n * nq4, 0x7fffffffLL) : 0, 0x00020000);
@@ -1674,6 +1692,12 @@ static bool mfma_offsets_fit(const BwdArgs &A, const BwdPlan &P) {
 
 // k_grad_q_mfma's origin-sorted groups: levels 0 .. nsl - 1, each level's window gradients of one batch element as
 // one descriptor
+// k_win_grad_pairs' output-gradient row descriptor: n^2 channels of Nq floats addressed with 32-bit offsets
+bool win_grad_needs_g64(long long Nq, int radius) {
+    const long long n = 2LL * radius + 1;
+    return n * n * 4 * Nq + 256 > 0x7fffffffLL;
+}
+
 static bool gq_sorted_fits(const BwdArgs &A, int nsl) {
     for (int l = 0; l < nsl; ++l)
         if (A.Nq * ((long long)A.nwh[l] * A.nwu[l] * A.nwv[l]) * 4 + 32 > 0x7fffffffLL) return false;
@@ -1685,6 +1709,10 @@ static bool gq_sorted_fits(const BwdArgs &A, int nsl) {
 // "bwd_mfma", thread-local like every dvc_set_tuning knob)
 static thread_local int g_bwd_mfma = 1;
 void set_backward_mfma(int v) { g_bwd_mfma = v; }
+// 1: k_win_grad_pairs' 64-bit-addressed instance at every size (tests; the product picks it only past the 31-bit
+// row range, win_grad_needs_g64)
+static thread_local int g_bwd_g64 = 0;
+void set_backward_g64(int v) { g_bwd_g64 = v; }
 
 // dtype codes of the packed operands whose gradient sums run on the matrix cores (the rest: VALU)
 int backward_uses_mfma(int B, long long Nq, const dvc_layout &lay, int radius, int convention, int dtype) {
@@ -1744,10 +1772,11 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
             (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, WG::LDS);
             kern<<<wg_grid, 64 * WG::WAVES, WG::LDS, s>>>(A);
         };
+        const bool g64 = g_bwd_g64 || win_grad_needs_g64(A.Nq, R);
         switch (fmt) {
-        case kGwF16: launch_wg(k_win_grad_pairs<R, kGwF16>); break;
-        case kGwBf16: launch_wg(k_win_grad_pairs<R, kGwBf16>); break;
-        default: launch_wg(k_win_grad_pairs<R, kGwF32>); break;
+        case kGwF16: g64 ? launch_wg(k_win_grad_pairs<R, kGwF16, true>) : launch_wg(k_win_grad_pairs<R, kGwF16>); break;
+        case kGwBf16: g64 ? launch_wg(k_win_grad_pairs<R, kGwBf16, true>) : launch_wg(k_win_grad_pairs<R, kGwBf16>); break;
+        default: g64 ? launch_wg(k_win_grad_pairs<R, kGwF32, true>) : launch_wg(k_win_grad_pairs<R, kGwF32>); break;
         }
     }
     if (!launched("win_grad")) return DVC_ERR_LAUNCH;

@@ -62,6 +62,8 @@ int corr_backward(const void *packed_q, const void *packed_t, const float *coord
 size_t backward_workspace_bytes(int B, long long Nq, const dvc_layout &lay, int radius);
 int backward_uses_mfma(int B, long long Nq, const dvc_layout &lay, int radius, int convention, int dtype);
 void set_backward_mfma(int v);
+bool win_grad_needs_g64(long long Nq, int radius);
+void set_backward_g64(int v);
 __global__ void k_coords_grid(float *, long long, int, int, int);
 template <bool DELTA, bool SUBGRID, int VEC, bool STAGED>
 __global__ void k_upflow(const float *, const float *, float *, float *, long long, int, int, int, int, int, int, int,
@@ -357,6 +359,11 @@ int dvc_set_tuning(const char *key, int value) {
     if (!strcmp(key, "bwd_mfma")) {   // 1 = gradient sums on the matrix cores (default), 0 = the VALU kernels
         if (value < 0 || value > 1) return fail(DVC_ERR_INVALID, "set_tuning: bwd_mfma %d", value);
         set_backward_mfma(value);
+        return DVC_OK;
+    }
+    if (!strcmp(key, "bwd_gout64")) {   // 1 = the window-gradient pass's 64-bit-addressed instance at every size
+        if (value < 0 || value > 1) return fail(DVC_ERR_INVALID, "set_tuning: bwd_gout64 %d", value);
+        set_backward_g64(value);
         return DVC_OK;
     }
     if (!strcmp(key, "build_wgs")) {
@@ -877,6 +884,11 @@ int dvc_corr_backward_mfma(int B, int64_t Nq, int C, int H, int W, int D, int nu
     if (dvc_layout_init(H, W, D, num_levels, C, &lay)) return 0;
     if (B < 1 || Nq < 1 || radius < 1 || radius > 6) return 0;
     return backward_uses_mfma(B, Nq, lay, radius, convention, dtype);
+}
+
+int dvc_corr_backward_gout64(int64_t Nq, int radius) {
+    if (Nq < 1 || radius < 1 || radius > 6) return 0;
+    return win_grad_needs_g64(Nq, radius) ? 1 : 0;
 }
 
 int dvc_sample3d(const float *vol, const float *pts, float *out, int B, int C, int Hv, int Wv, int Dv, int64_t Nq,

@@ -27,7 +27,7 @@ EXPORTED = (
     "dvc_sample3d", "dvc_set_tuning", "dvc_last_error", "dvc_version", "dvc_abi_version",
     "dvc_corr_backward_workspace_bytes", "dvc_corr_backward", "dvc_proj_packed_bytes", "dvc_proj_pack",
     "dvc_corr_lookup_proj", "dvc_lookup_fused_proj_workspace_bytes", "dvc_corr_lookup_fused_proj",
-    "dvc_coords_grid", "dvc_upflow", "dvc_flow_step", "dvc_bricked_levels", "dvc_corr_backward_mfma",
+    "dvc_coords_grid", "dvc_upflow", "dvc_flow_step", "dvc_bricked_levels", "dvc_corr_backward_mfma", "dvc_corr_backward_gout64",
 )
 PROJ_COUT = 96          # DVC_PROJ_COUT (convc1 output channels, update.py:222)
 PROJ_MAX_RADIUS = 4     # DVC_PROJ_MAX_RADIUS
@@ -86,6 +86,7 @@ def lib() -> ctypes.CDLL:
         "dvc_corr_backward": (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i64, i32, i32, i32, i32, i32, i32, i32, i32,
                                     vp]),
         "dvc_corr_backward_mfma": (i32, [i32, i64, i32, i32, i32, i32, i32, i32, i32, i32]),
+        "dvc_corr_backward_gout64": (i32, [i64, i32]),
         "dvc_proj_packed_bytes": (sz, [i32, i32]),
         "dvc_proj_pack": (i32, [vp, vp, i32, i32, i32, i32, vp]),
         "dvc_corr_lookup_proj": (i32, [vp, vp, vp, vp, vp, i32, i64, i32, i32, i32, i32, i32, i32, i32, vp]),

@@ -163,6 +163,22 @@ def test_backward_path_selection_without_gpu():
     assert L.dvc_corr_backward_mfma(1, 32768, 128, 32, 32, 32, 4, 9, 0, _lib.DVC_BF16) == 0   # radius outside 1..6
 
 
+def test_backward_gout64_bound_without_gpu():
+    """k_win_grad_pairs addresses one output-gradient row ((2r+1)^2 channels of Nq floats) through a buffer
+    descriptor with 32-bit offsets; rows past 2^31 - 1 bytes (Nq > ~6.6 M at r = 4, ~3.2 M at r = 6) switch to the
+    64-bit-addressed instance instead of reading zeros past the range."""
+    from dvccorr import _lib
+    L = _lib.lib()
+    for r in range(1, 7):
+        n2 = (2 * r + 1) ** 2
+        edge = (0x7FFFFFFF - 256) // (4 * n2)          # the largest Nq whose row still fits
+        assert L.dvc_corr_backward_gout64(edge, r) == 0
+        assert L.dvc_corr_backward_gout64(edge + 1, r) == 1
+    assert L.dvc_corr_backward_gout64(32768, 4) == 0            # config #3
+    assert L.dvc_corr_backward_gout64(188 ** 3, 4) == 1         # a 188^3 fmap at r = 4
+    assert L.dvc_corr_backward_gout64(150 ** 3, 6) == 1         # 3.4 M queries at r = 6
+
+
 def test_coords_grid_matches_reference_fixture():
     import numpy as np
     import prng

@@ -275,6 +275,33 @@ def test_grad_valu_fallback(precision, tol):
         _lib.set_tuning("bwd_mfma", 1)
 
 
+@pytest.mark.parametrize("precision", ["bf16", "fp16", "fp32"])
+def test_grad_gout64_instance(precision):
+    """k_win_grad_pairs' 64-bit-addressed instance (the one volumes with more than 2^31 - 1 bytes per
+    output-gradient row take, Nq > ~6.6 M at r = 4, too large for a test) forced with tuning "bwd_gout64" 1: the
+    same gradients as the 32-bit-offset instance, bit for bit, and the golden vectors still pass."""
+    from dvccorr import _lib, ops
+    S, C, L, r = 12, 64, 3, 4
+    seed = 515
+    f1 = torch.from_numpy(prng.normal(seed, (1, C, S, S, S))).to(DEV)
+    f2 = torch.from_numpy(prng.normal(seed + 1, (1, C, S, S, S))).to(DEV)
+    coords = torch.from_numpy(prng.flow_coords(seed + 2, 1, S, S, S, 3.0)).to(DEV).reshape(1, 3, -1)
+    G = torch.from_numpy(prng.normal(seed + 3, (1, L * (2 * r + 1) ** 3, S ** 3))).to(DEV)
+    dt = ops.dtype_code(precision)
+    q = ops.pack_queries(f1.reshape(1, C, -1), dt)
+    t = ops.pack_targets(f2, L, dt)
+    base = ops.corr_backward(q, t, coords, G, C, S, S, S, L, r, False, dt)
+    _lib.set_tuning("bwd_gout64", 1)
+    try:
+        wide = ops.corr_backward(q, t, coords, G, C, S, S, S, L, r, False, dt)
+        torch.cuda.synchronize()
+        _check_golden("grad_cfg2", "gemm", precision, {"fp32": GRAD_TOL, "bf16": BF16_TOL, "fp16": FP16_TOL}[precision])
+    finally:
+        _lib.set_tuning("bwd_gout64", 0)
+    for a, b in zip(base, wide):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("precision", ["bf16", "fp32"])
 def test_grad_stale_workspace(precision):
     """The window-gradient planes outside a level are never written (k_win_grad_pairs) and the 16-byte gradient

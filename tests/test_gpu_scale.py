@@ -81,22 +81,30 @@ def test_cfg4_rank_slab(rank):
     assert orc.rel_err(_rows(part, local), ref) <= BF16_TOL
 
 
-def test_cfg5_fused_rows():
+FP16_TOL = 5e-3     # the reference's AMP tolerance (test_corr_equivalence.py:156-186)
+
+
+@pytest.mark.parametrize("precision,tol", [("bf16", BF16_TOL), ("fp16", FP16_TOL)])
+def test_cfg5_fused_rows(precision, tol):
     """Config #5: 128^3 x 128 fmaps, L=2, r=4, on-the-fly block (the 9.9 TB volume is never built):
-    sampled query rows against the f64 oracle at the bf16 tolerance."""
+    256 sampled query rows (plus corners, edges and one chunk's lanes 48-63) against the f64 oracle at the
+    operand dtype's tolerance -- bf16 (the bench's dtype) and fp16 (the Trainer's AMP operands)."""
     import dvccorr
     S, C, L, r = 128, 128, 2, 4
     f1, f2, c = _inputs(505, C, S)
     with torch.no_grad():
-        blk = dvccorr.CorrBlockFused(f1, f2, L, r, precision="bf16")
+        blk = dvccorr.CorrBlockFused(f1, f2, L, r, precision=precision)
         out = blk(c).reshape(1, L * (2 * r + 1) ** 3, -1)
         torch.cuda.synchronize()
     assert torch.isfinite(out).all()
     N = S ** 3
-    rows = np.sort(np.random.default_rng(505).choice(N, 24, replace=False))
-    rows = np.concatenate([rows, [0, N - 1, S * S * 64 + S * 3 + 127]]).astype(np.int64)
+    rows = np.sort(np.random.default_rng(505).choice(N, 256, replace=False))
+    rows = np.unique(np.concatenate([rows, [0, N - 1, S - 1, S * S - 1, S * S * 64 + S * 3 + 127,
+                                            4096 + 48, 4096 + 63]])).astype(np.int64)
     ref = _oracle_rows(f1, f2, c, L, r, rows)
-    assert orc.rel_err(_rows(out, rows), ref) <= BF16_TOL
+    assert orc.rel_err(_rows(out, rows), ref) <= tol
+    if precision != "bf16":
+        return
     # the same kernels, a slab of queries (the sharded #5 layout) is the slab of the whole result
     from dvccorr.sharded import HipRows
     with torch.no_grad():
