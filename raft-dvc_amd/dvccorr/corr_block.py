@@ -119,15 +119,29 @@ class _Block:
             raise ValueError(f"coords must be (B, 3, H, W, D) = {(B, 3, H, W, D)}; got {tuple(coords.shape)}")
 
     def _convc1_fusable(self, weight: torch.Tensor, bias: torch.Tensor, w: torch.Tensor) -> bool:
-        """The fused convc1 kernels cover a bf16 / fp16 block without gradients, radius 1..4, 96 output channels
-        and no legacy level with W != D; fp32 blocks keep the reference's fp32 convc1 (update.py:246), since the
-        kernels' fp16 MFMA operands would cost ~1e-3 relative error."""
+        """The fused convc1 kernels cover a bf16 / fp16 block, radius 1..4, 96 output channels and no legacy level
+        with W != D; fp32 blocks keep the reference's fp32 convc1 (update.py:246), since the kernels' fp16 MFMA
+        operands would cost ~1e-3 relative error.  With gradients (the Trainer's path, trainer.py:249-257) the
+        fused kernel runs as dvccorr::lookup_convc1_ad (_convc1_grad)."""
         return (self.precision in ("bf16", "fp16")
-                and not (torch.is_grad_enabled() and (weight.requires_grad or bias.requires_grad or
-                                                      self._grad_fmaps is not None))
                 and 1 <= self.radius <= ops._lib.PROJ_MAX_RADIUS and w.shape[0] == ops._lib.PROJ_COUT
                 and not (self.legacy_wd_swap and any(lw != ld and min(lh, lw, ld) > 1
                                                      for lh, lw, ld in self._lay.levels())))
+
+    def _convc1_grad(self, weight: torch.Tensor, bias: torch.Tensor) -> bool:
+        return torch.is_grad_enabled() and (weight.requires_grad or bias.requires_grad or
+                                            self._grad_fmaps is not None)
+
+    def _convc1_ad(self, coords: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, packed: torch.Tensor,
+                   corr: Optional[torch.Tensor]) -> torch.Tensor:
+        """relu(convc1(lookup)) through dvccorr::lookup_convc1_ad: the fused kernel forward, gradients for the
+        fmaps (when the block's fmaps require grad), convc1.weight and convc1.bias."""
+        B, C, H, W, D = self.shape
+        f1, f2 = self._grad_fmaps if self._grad_fmaps is not None else (coords.new_empty(0), coords.new_empty(0))
+        out = library.lookup_convc1_ad(f1, f2, weight, bias, corr, self._q, self._t, coords.reshape(B, 3, H * W * D),
+                                       packed, C, H, W, D, self.num_levels, self.radius, self.legacy_wd_swap,
+                                       self._dt, getattr(self, "_ldt", self._dt))
+        return out.view(B, -1, H, W, D)
 
     def _convc1_composition(self, coords: torch.Tensor, w: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
         out = self(coords)
@@ -247,16 +261,19 @@ class CorrBlock(_Block):
 
         The motion encoder's first layer (update.py:219-222, 246: Conv3d(L*(2r+1)^3, 96, 1) + ReLU)
         runs on fp16 MFMA (fp32 accumulation; the reference's AMP convc1 is fp16 too) inside the
-        lookup kernel of a bf16 block, so the L*(2r+1)^3-channel tensor never reaches HBM
-        (dvc_corr_lookup_proj; tolerance 1e-2 max-normalised).  An fp32 block (tolerance 1e-5),
-        gradients, or radii/conventions the fused kernel does not cover take the composition
-        F.relu(F.conv3d(self(coords), weight, bias)) on the GPU."""
+        lookup kernel of a bf16 / fp16 block, so the L*(2r+1)^3-channel tensor never reaches HBM
+        (dvc_corr_lookup_proj; tolerance 1e-2 max-normalised).  Under autograd (fmaps, weight or bias
+        requiring grad) it runs as dvccorr::lookup_convc1_ad, whose backward recomputes the lookup.  An
+        fp32 block (tolerance 1e-5), or radii/conventions the fused kernel does not cover take the
+        composition F.relu(F.conv3d(self(coords), weight, bias)) on the GPU."""
         self._check_coords(coords)
         B, _, H, W, D = self.shape
         w = weight.reshape(weight.shape[0], -1)
         if not self._convc1_fusable(weight, bias, w):
             return self._convc1_composition(coords, w, bias)
         packed = ops.proj_pack_cached(weight, self.num_levels, self.radius, self.legacy_wd_swap)
+        if self._convc1_grad(weight, bias):
+            return self._convc1_ad(coords, weight, bias, packed, self._corr)
         out = ops.lookup_proj(self._corr, coords.reshape(B, 3, H * W * D), packed, bias, H, W, D,
                               self.num_levels, self.radius, self.legacy_wd_swap, self._ldt)
         return out.view(B, -1, H, W, D)
@@ -303,6 +320,8 @@ class CorrBlockFused(_Block):
         if not (self._convc1_fusable(weight, bias, w) and self._lay.c_pad in (32, 64, 128)):
             return self._convc1_composition(coords, w, bias)
         packed = ops.proj_pack_cached(weight, self.num_levels, self.radius, self.legacy_wd_swap)
+        if self._convc1_grad(weight, bias):
+            return self._convc1_ad(coords, weight, bias, packed, None)
         out = library.lookup_fused_proj(self._q, self._t, coords.reshape(B, 3, H * W * D), packed, bias, C, H, W,
                                         D, self.num_levels, self.radius, self.legacy_wd_swap, self._dt)
         return out.view(B, -1, H, W, D)
