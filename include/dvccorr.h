@@ -197,16 +197,23 @@ int dvc_corr_backward_gout64(int64_t Nq, int radius);
  *   dvc_proj_pack: convc1.weight viewed (96, L*(2r+1)^3) float32 -> packed fp16
  *     weights (dvc_proj_packed_bytes) in the kernel's MFMA operand order for one
  *     (num_levels, radius, convention); pack once per weight update.
+ *   dvc_proj_pack_exact: the same weights as bf16 hi + lo blocks (2 x dvc_proj_packed_bytes:
+ *     hi = bf16(w), then lo = bf16(w - hi)) for DVC_F32 pyramids.
  *   dvc_corr_lookup_proj: out (B, 96, Nq) float32 = relu(W . lookup(coords) + bias),
- *     bias (96) float32.  The lookup values and the weights enter fp16 MFMA with
- *     float32 accumulation (tolerance 1e-2 max-normalised against the float32
- *     reference).  Supported: radius 1..4, tile-kernel row widths, and for the legacy
- *     convention W == D at every non-zero level (DVC_ERR_UNSUPPORTED otherwise). */
+ *     bias (96) float32.  bf16 / f16 pyramids (dvc_proj_pack weights): the lookup values and
+ *     the weights enter fp16 MFMA with float32 accumulation (tolerance 1e-2 max-normalised
+ *     against the float32 reference).  DVC_F32 pyramids (dvc_proj_pack_exact weights, round 5):
+ *     both operands split into bf16 hi + lo, three MFMAs per step (x_hi w_hi + x_lo w_hi +
+ *     x_hi w_lo, float32 accumulation): the fp32 tolerance 1e-5 (the reference's fp32
+ *     evaluation, evaluate_phase1.py:115-131).  Supported: radius 1..4, tile-kernel row widths,
+ *     and for the legacy convention W == D at every non-zero level (DVC_ERR_UNSUPPORTED otherwise). */
 #define DVC_PROJ_COUT 96
 #define DVC_PROJ_MAX_RADIUS 4
 size_t dvc_proj_packed_bytes(int num_levels, int radius);
 int dvc_proj_pack(const float *weight, void *packed, int cout, int num_levels, int radius, int convention,
                   void *stream);
+int dvc_proj_pack_exact(const float *weight, void *packed, int cout, int num_levels, int radius, int convention,
+                        void *stream);
 int dvc_corr_lookup_proj(const void *corr, const float *coords, const void *packed_w, const float *bias, float *out,
                          int B, int64_t Nq, int H, int W, int D, int num_levels, int radius, int convention,
                          int store_dtype, void *stream);

@@ -42,9 +42,9 @@ template <typename T>
 __global__ void k_corr_pool(T *, long long, long long, long long, int, int, long long, int, int, int, int);
 template <typename T, int R, bool WINBUF, bool ALIGNED> __global__ void k_lookup_win(LookupArgs);
 template <typename T> __global__ void k_lookup_generic(LookupArgs);
-template <typename T, int R, bool NT, int ABL, bool PROJ, int ACH, int NWV = 0, int SPOL = -1>
+template <typename T, int R, bool NT, int ABL, int PROJ, int ACH, int NWV = 0, int SPOL = -1>
 __global__ void k_lookup_tile(LookupArgs);
-__global__ void k_proj_pack(const float *, bf16_t *, int, int, int, long long);
+__global__ void k_proj_pack(const float *, bf16_t *, int, int, int, long long, int);
 __global__ void k_sample3d(const float *, const float *, float *, int, int, int, int, int, long long, int);
 int fused_lookup(const void *packed_q, const void *packed_t, const float *coords, float *out, void *workspace, int B,
                  long long Nq, int C, const dvc_layout &lay, int radius, int convention, int dtype, int variant,
@@ -784,8 +784,25 @@ int dvc_proj_pack(const float *weight, void *packed, int cout, int num_levels, i
         return fail(DVC_ERR_INVALID, "proj_pack: bad convention %d", convention);
     const long long total = (long long)(dvc_proj_packed_bytes(num_levels, radius) / sizeof(bf16_t));
     k_proj_pack<<<(unsigned)ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(
-        weight, (bf16_t *)packed, num_levels, radius, convention == DVC_LEGACY, total);
+        weight, (bf16_t *)packed, num_levels, radius, convention == DVC_LEGACY, total, 0);
     return check_launch("proj_pack");
+}
+
+int dvc_proj_pack_exact(const float *weight, void *packed, int cout, int num_levels, int radius, int convention,
+                        void *stream) {
+    if (!weight || !packed) return fail(DVC_ERR_INVALID, "proj_pack_exact: null pointer");
+    if (cout != DVC_PROJ_COUT)
+        return fail(DVC_ERR_UNSUPPORTED, "proj_pack_exact: %d output channels (convc1 has %d)", cout, DVC_PROJ_COUT);
+    if (num_levels < 1 || num_levels > DVC_MAX_LEVELS)
+        return fail(DVC_ERR_INVALID, "proj_pack_exact: num_levels=%d outside [1, %d]", num_levels, DVC_MAX_LEVELS);
+    if (radius < 1 || radius > DVC_PROJ_MAX_RADIUS)
+        return fail(DVC_ERR_UNSUPPORTED, "proj_pack_exact: radius %d outside [1, %d]", radius, DVC_PROJ_MAX_RADIUS);
+    if (convention != DVC_FIXED && convention != DVC_LEGACY)
+        return fail(DVC_ERR_INVALID, "proj_pack_exact: bad convention %d", convention);
+    const long long total = (long long)(dvc_proj_packed_bytes(num_levels, radius) / sizeof(bf16_t));
+    k_proj_pack<<<(unsigned)ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(
+        weight, (bf16_t *)packed, num_levels, radius, convention == DVC_LEGACY, total, 1);
+    return check_launch("proj_pack_exact");
 }
 
 int dvc_corr_lookup_proj(const void *corr, const float *coords, const void *packed_w, const float *bias, float *out,
@@ -819,16 +836,16 @@ int dvc_corr_lookup_proj(const void *corr, const float *coords, const void *pack
     const unsigned blocks = (unsigned)(B * A.nqb);
     const unsigned threads = 64u * (unsigned)((2 * radius + 3) / 3 + 1);
     hipStream_t s = (hipStream_t)stream;
-#define DVC_PROJ_LAUNCH(T)                                                                   \
+#define DVC_PROJ_LAUNCH(T, P)                                                                \
     switch (radius) {                                                                        \
-    case 1: k_lookup_tile<T, 1, true, 0, true, 0><<<blocks, threads, 0, s>>>(A); break;        \
-    case 2: k_lookup_tile<T, 2, true, 0, true, 0><<<blocks, threads, 0, s>>>(A); break;        \
-    case 3: k_lookup_tile<T, 3, true, 0, true, 0><<<blocks, threads, 0, s>>>(A); break;        \
-    default: k_lookup_tile<T, 4, true, 0, true, 0><<<blocks, threads, 0, s>>>(A); break;       \
+    case 1: k_lookup_tile<T, 1, true, 0, P, 0><<<blocks, threads, 0, s>>>(A); break;           \
+    case 2: k_lookup_tile<T, 2, true, 0, P, 0><<<blocks, threads, 0, s>>>(A); break;           \
+    case 3: k_lookup_tile<T, 3, true, 0, P, 0><<<blocks, threads, 0, s>>>(A); break;           \
+    default: k_lookup_tile<T, 4, true, 0, P, 0><<<blocks, threads, 0, s>>>(A); break;          \
     }
-    if (store_dtype == DVC_BF16) { DVC_PROJ_LAUNCH(bf16_t) }
-    else if (store_dtype == DVC_F16) { DVC_PROJ_LAUNCH(f16_t) }
-    else { DVC_PROJ_LAUNCH(float) }
+    if (store_dtype == DVC_BF16) { DVC_PROJ_LAUNCH(bf16_t, 1) }
+    else if (store_dtype == DVC_F16) { DVC_PROJ_LAUNCH(f16_t, 1) }
+    else { DVC_PROJ_LAUNCH(float, 2) }   // fp32 pyramid: the exact split consumer (dvc_proj_pack_exact weights)
 #undef DVC_PROJ_LAUNCH
     return check_launch("corr_lookup_proj");
 }

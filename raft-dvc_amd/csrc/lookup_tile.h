@@ -177,6 +177,12 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 struct ProjCfg {
     static constexpr int COUT = 96, OT = COUT / 16, KW = 32;
 };
+// PROJ == 2 (round 5, fp32 blocks: the reference's fp32 evaluation path, evaluate_phase1.py:115-131): the same
+// consumer with every operand split into bf16 hi + lo (x = xh + xl + O(2^-16 x), w likewise) and three MFMAs per step,
+// xh wh + xl wh + xh wl: each product keeps ~2^-16 relative, well inside the fp32 tolerance 1e-5 on sums of
+// L (2r+1)^3 terms, with fp32's exponent range (fp16 pairs would overflow above 65504).  The producers write X as a hi
+// tile and a lo tile; the weights come hi block then lo block (dvc_proj_pack_exact).  fp32 plane strips (62.5 KB) +
+// two X tiles (26.6 KB) leave one workgroup per CU, so these instances are built for one wave per SIMD (512 VGPRs).
 
 // ABL (diagnostics only, never the product path): 1 = skip output stores, 2 = skip loads, 4 = the same
 // output bytes as 16-byte stores (a column's 9 values leave as 2 x dwordx4 + 1 dword per lane, at
@@ -185,8 +191,9 @@ struct ProjCfg {
 // (ACH + 1 window planes), for launches whose (tile, level) pairs alone cannot fill the chip.
 // SPOL >= 0 (diagnostics, tuning "lookup_stpol"): the output stores' cache-policy bits instead of NT's
 // (16 = sc1: the line is not kept in the XCD's L2, which the plane loads then have to themselves).
-template <typename T, int R, bool NT, int ABL, bool PROJ, int ACH, int NWV = 0, int SPOL = -1>
-__global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)), 2) void k_lookup_tile(LookupArgs A) {
+template <typename T, int R, bool NT, int ABL, int PROJ, int ACH, int NWV = 0, int SPOL = -1>
+__global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)), PROJ == 2 ? 1 : 2) void k_lookup_tile(
+    LookupArgs A) {
     using C = TileCfg<T, R, NWV>;
     static_assert(!PROJ || NWV == 0, "the convc1 weight packing assumes the 3-column waves");
     constexpr bool BAL = NWV > 0;
@@ -198,7 +205,8 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
     static_assert(!PROJ || C::COLS * n <= ProjCfg::KW, "PROJ: one wave's row values must fit a 32-k slice");
     __shared__ __attribute__((aligned(16))) unsigned char smem[C::LDS];
     __shared__ int tab[5][64];   // per query of the tile: ih, cs, za, iv, iu (element units)
-    __shared__ __attribute__((aligned(16))) unsigned char xs[PROJ ? 64 * XROW : 16];
+    __shared__ __attribute__((aligned(16))) unsigned char xs[PROJ ? PROJ * 64 * XROW : 16];   // X (PROJ 2: hi, lo)
+    static_assert(PROJ != 2 || std::is_same<T, float>::value, "the split convc1 is the fp32 pyramid's");
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -222,6 +230,8 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
 #pragma unroll
                 for (int j = 0; j < 4; ++j) acc[ot][j] = f32x4{0.f, 0.f, 0.f, 0.f};
             const f16x8 *wp = reinterpret_cast<const f16x8 *>(A.proj_w) + lane;
+            // PROJ 2: the lo weights, one packed block after the hi ones
+            const long long wlo = PROJ == 2 ? (long long)A.Ltot * n * NWP * OT * 64 : 0;
             for (int li = 0; li < A.nl; ++li) {
                 const int l = A.l0 + (rev ? A.nl - 1 - li : li);
                 if (A.zero[l] || A.generic[l]) continue;   // (the producers skip the same levels)
@@ -232,13 +242,43 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
                 for (int a = 0; a < n; ++a) {
                     // this row's weight block, [wave slice ks][16-channel tile ot][lane] x 8 fp16
                     const f16x8 *wr = wp + (long long)(l * n + a) * NWP * OT * 64;
-                    f16x8 wa[NWP][OT];
+                    f16x8 wa[NWP][OT], wal[PROJ == 2 ? NWP : 1][OT];
 #pragma unroll
                     for (int ks = 0; ks < NWP; ++ks)
 #pragma unroll
                         for (int ot = 0; ot < OT; ++ot) wa[ks][ot] = wr[(ks * OT + ot) * 64];
+                    if constexpr (PROJ == 2) {
+#pragma unroll
+                        for (int ks = 0; ks < NWP; ++ks)
+#pragma unroll
+                            for (int ot = 0; ot < OT; ++ot) wal[ks][ot] = wr[wlo + (ks * OT + ot) * 64];
+                    }
                     __syncthreads();   // the producers may overwrite X: row a-1 has been read
                     __syncthreads();   // row a complete in X
+                    if constexpr (PROJ == 2) {
+#pragma unroll
+                        for (int ks = 0; ks < NWP; ++ks) {
+                            bf16x8 xh[4], xl[4];
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) {
+                                const int xo = (16 * j + m16) * XROW + ks * 64 + h4 * 16;
+                                xh[j] = *reinterpret_cast<const bf16x8 *>(xs + xo);
+                                xl[j] = *reinterpret_cast<const bf16x8 *>(xs + 64 * XROW + xo);
+                            }
+#pragma unroll
+                            for (int ot = 0; ot < OT; ++ot) {
+                                const bf16x8 whi = __builtin_bit_cast(bf16x8, wa[ks][ot]);
+                                const bf16x8 wlw = __builtin_bit_cast(bf16x8, wal[ks][ot]);
+#pragma unroll
+                                for (int j = 0; j < 4; ++j) {
+                                    acc[ot][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi, xh[j], acc[ot][j], 0, 0, 0);
+                                    acc[ot][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi, xl[j], acc[ot][j], 0, 0, 0);
+                                    acc[ot][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlw, xh[j], acc[ot][j], 0, 0, 0);
+                                }
+                            }
+                        }
+                        continue;
+                    }
 #pragma unroll
                     for (int ks = 0; ks < NWP; ++ks) {
                         f16x8 xb[4];
@@ -522,7 +562,8 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
             // column by column: once window column k of plane a+1 is lerped, output
             // column k-1 is complete and plane a's column k-1 retires
             ZRun<n> zprev;
-            unsigned xr[NU * NP];   // PROJ: this row's value pairs as f16x2
+            unsigned xr[NU * NP];   // PROJ: this row's value pairs as f16x2 (PROJ 2: bf16x2 hi)
+            unsigned xrl[PROJ == 2 ? NU * NP : 1];   // PROJ 2: bf16x2 lo
             float xt[NU];           // PROJ: tails (v = n - 1)
 #pragma unroll
             for (int k = 0; k <= NU; ++k) {
@@ -543,7 +584,12 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
                         acc = __builtin_elementwise_fma(P10, zp[uu + 1].p[i], acc);
                         acc = __builtin_elementwise_fma(P01, zprev.p[i], acc);
                         acc = __builtin_elementwise_fma(P11, zcur.p[i], acc);
-                        if constexpr (PROJ) {
+                        if constexpr (PROJ == 2) {
+                            const bf16x2 hv = __builtin_convertvector(acc, bf16x2);
+                            xr[uu * NP + i] = __builtin_bit_cast(unsigned, hv);
+                            xrl[uu * NP + i] = __builtin_bit_cast(
+                                unsigned, __builtin_convertvector(acc - __builtin_convertvector(hv, f32x2), bf16x2));
+                        } else if constexpr (PROJ) {
                             xr[uu * NP + i] = __builtin_bit_cast(unsigned, __builtin_convertvector(acc, f16x2));
                         } else if constexpr ((ABL & 4) != 0) {
                             wide[2 * i] = acc[0];
@@ -579,19 +625,36 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
             if constexpr (PROJ) {
                 // this wave's 32-k slice of the row: pairs, then the tails, then zeros
                 constexpr int T0 = NU * NP;
-                unsigned xw[ProjCfg::KW / 2];
+                unsigned xw[ProjCfg::KW / 2], xwl[PROJ == 2 ? ProjCfg::KW / 2 : 1];
 #pragma unroll
                 for (int d = 0; d < ProjCfg::KW / 2; ++d) xw[d] = d < T0 ? xr[d < T0 ? d : 0] : 0u;
+                if constexpr (PROJ == 2) {
+#pragma unroll
+                    for (int d = 0; d < ProjCfg::KW / 2; ++d) xwl[d] = d < T0 ? xrl[d < T0 ? d : 0] : 0u;
+                }
 #pragma unroll
                 for (int p = 0; 2 * p < NU; ++p) {
                     const f32x2 t2 = {xt[2 * p], 2 * p + 1 < NU ? xt[2 * p + 1 < NU ? 2 * p + 1 : 0] : 0.0f};
-                    xw[T0 + p] = __builtin_bit_cast(unsigned, __builtin_convertvector(t2, f16x2));
+                    if constexpr (PROJ == 2) {
+                        const bf16x2 hv = __builtin_convertvector(t2, bf16x2);
+                        xw[T0 + p] = __builtin_bit_cast(unsigned, hv);
+                        xwl[T0 + p] = __builtin_bit_cast(
+                            unsigned, __builtin_convertvector(t2 - __builtin_convertvector(hv, f32x2), bf16x2));
+                    } else {
+                        xw[T0 + p] = __builtin_bit_cast(unsigned, __builtin_convertvector(t2, f16x2));
+                    }
                 }
                 __syncthreads();   // the consumer has read the previous row of X
                 u32x4 *dst = reinterpret_cast<u32x4 *>(xs + lane * XROW + wave * (ProjCfg::KW * 2));
 #pragma unroll
                 for (int j = 0; j < ProjCfg::KW / 8; ++j)
                     dst[j] = u32x4{xw[4 * j], xw[4 * j + 1], xw[4 * j + 2], xw[4 * j + 3]};
+                if constexpr (PROJ == 2) {
+                    u32x4 *dl = reinterpret_cast<u32x4 *>(xs + 64 * XROW + lane * XROW + wave * (ProjCfg::KW * 2));
+#pragma unroll
+                    for (int j = 0; j < ProjCfg::KW / 8; ++j)
+                        dl[j] = u32x4{xwl[4 * j], xwl[4 * j + 1], xwl[4 * j + 2], xwl[4 * j + 3]};
+                }
             }
             if (ia + 2 < NPL) {   // plane a+2 into the slot of plane a (read in row a-1)
                 write_plane(ia & 1, a + 2, st[(ia + 2) % PD]);

@@ -4,8 +4,10 @@ namespace dvc {
 
 // convc1-fused instances of k_lookup_tile (lookup_tile.h; radii whose (2r+1) x 3 row values fit one
 // 32-k slice) and their weight packing
-#define DVC_TILE_PROJ(T, R) template __global__ void k_lookup_tile<T, R, true, 0, true, 0>(LookupArgs);
-DVC_TILE_PROJ(float, 1) DVC_TILE_PROJ(float, 2) DVC_TILE_PROJ(float, 3) DVC_TILE_PROJ(float, 4)
+#define DVC_TILE_PROJ(T, R) template __global__ void k_lookup_tile<T, R, true, 0, 1, 0>(LookupArgs);
+// fp32 pyramids: the exact split consumer (PROJ 2, bf16 hi/lo operands, lookup_tile.h)
+#define DVC_TILE_PROJX(R) template __global__ void k_lookup_tile<float, R, true, 0, 2, 0>(LookupArgs);
+DVC_TILE_PROJX(1) DVC_TILE_PROJX(2) DVC_TILE_PROJX(3) DVC_TILE_PROJX(4)
 DVC_TILE_PROJ(bf16_t, 1) DVC_TILE_PROJ(bf16_t, 2) DVC_TILE_PROJ(bf16_t, 3) DVC_TILE_PROJ(bf16_t, 4)
 DVC_TILE_PROJ(f16_t, 1) DVC_TILE_PROJ(f16_t, 2) DVC_TILE_PROJ(f16_t, 3) DVC_TILE_PROJ(f16_t, 4)
 
@@ -15,8 +17,9 @@ DVC_TILE_PROJ(f16_t, 1) DVC_TILE_PROJ(f16_t, 2) DVC_TILE_PROJ(f16_t, 3) DVC_TILE
 // channel o = 16 ot + m16 at the slice positions k = 8 h4 .. 8 h4 + 7 (k order above);
 // positions past the wave's values are 0.  Reference channel of (l, a, u, v):
 // l (2r+1)^3 + a (2r+1)^2 + u chstep_u + v chstep_v (corr.py:188-208).
+// split = 1 (dvc_proj_pack_exact, fp32 blocks): bf16 hi = bf16(w) at [idx], bf16 lo = bf16(w - hi) at [total + idx]
 __global__ void k_proj_pack(const float *__restrict__ w, bf16_t *__restrict__ out, int L, int r, int legacy,
-                            long long total) {
+                            long long total, int split) {
     const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= total) return;
     const int n = 2 * r + 1, NP = n / 2, COLS = 3, NWV = (n + COLS - 1) / COLS, OT = ProjCfg::OT;
@@ -43,6 +46,12 @@ __global__ void k_proj_pack(const float *__restrict__ w, bf16_t *__restrict__ ou
         const int u = w8 * COLS + uu;
         const long long ch = (long long)l * n * n * n + (long long)a * n * n + (legacy ? u + v * n : u * n + v);
         val = w[(long long)o * L * n * n * n + ch];
+    }
+    if (split) {
+        const __bf16 hi = (__bf16)val;
+        out[idx] = __builtin_bit_cast(bf16_t, hi);
+        out[total + idx] = __builtin_bit_cast(bf16_t, (__bf16)(val - (float)hi));
+        return;
     }
     out[idx] = __builtin_bit_cast(bf16_t, (_Float16)val);   // fp16 bits
 }

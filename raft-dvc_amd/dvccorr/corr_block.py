@@ -119,11 +119,12 @@ class _Block:
             raise ValueError(f"coords must be (B, 3, H, W, D) = {(B, 3, H, W, D)}; got {tuple(coords.shape)}")
 
     def _convc1_fusable(self, weight: torch.Tensor, bias: torch.Tensor, w: torch.Tensor) -> bool:
-        """The fused convc1 kernels cover a bf16 / fp16 block, radius 1..4, 96 output channels and no legacy level
-        with W != D; fp32 blocks keep the reference's fp32 convc1 (update.py:246), since the kernels' fp16 MFMA
-        operands would cost ~1e-3 relative error.  With gradients (the Trainer's path, trainer.py:249-257) the
-        fused kernel runs as dvccorr::lookup_convc1_ad (_convc1_grad)."""
-        return (self.precision in ("bf16", "fp16")
+        """The fused convc1 kernels cover radius 1..4, 96 output channels and no legacy level with W != D: a bf16 /
+        fp16 block with fp16 MFMA operands, and (round 5, materialised blocks only) an fp32 block through the exact
+        split consumer (bf16 hi/lo operands, fp32 tolerance; the reference's fp32 evaluation path,
+        evaluate_phase1.py:115-131).  The on-the-fly fp32 block keeps the composition.  With gradients (the
+        Trainer's path, trainer.py:249-257) the fused kernel runs as dvccorr::lookup_convc1_ad (_convc1_grad)."""
+        return ((self.precision in ("bf16", "fp16") or (self.precision == "fp32" and isinstance(self, CorrBlock)))
                 and 1 <= self.radius <= ops._lib.PROJ_MAX_RADIUS and w.shape[0] == ops._lib.PROJ_COUT
                 and not (self.legacy_wd_swap and any(lw != ld and min(lh, lw, ld) > 1
                                                      for lh, lw, ld in self._lay.levels())))
@@ -262,16 +263,18 @@ class CorrBlock(_Block):
         The motion encoder's first layer (update.py:219-222, 246: Conv3d(L*(2r+1)^3, 96, 1) + ReLU)
         runs on fp16 MFMA (fp32 accumulation; the reference's AMP convc1 is fp16 too) inside the
         lookup kernel of a bf16 / fp16 block, so the L*(2r+1)^3-channel tensor never reaches HBM
-        (dvc_corr_lookup_proj; tolerance 1e-2 max-normalised).  Under autograd (fmaps, weight or bias
-        requiring grad) it runs as dvccorr::lookup_convc1_ad, whose backward recomputes the lookup.  An
-        fp32 block (tolerance 1e-5), or radii/conventions the fused kernel does not cover take the
-        composition F.relu(F.conv3d(self(coords), weight, bias)) on the GPU."""
+        (dvc_corr_lookup_proj; tolerance 1e-2 max-normalised); an fp32 block splits both operands into
+        bf16 hi + lo (three MFMAs per step, tolerance 1e-5).  Under autograd (fmaps, weight or bias
+        requiring grad) it runs as dvccorr::lookup_convc1_ad, whose backward recomputes the lookup.
+        Radii / conventions the fused kernel does not cover take the composition
+        F.relu(F.conv3d(self(coords), weight, bias)) on the GPU."""
         self._check_coords(coords)
         B, _, H, W, D = self.shape
         w = weight.reshape(weight.shape[0], -1)
         if not self._convc1_fusable(weight, bias, w):
             return self._convc1_composition(coords, w, bias)
-        packed = ops.proj_pack_cached(weight, self.num_levels, self.radius, self.legacy_wd_swap)
+        packed = ops.proj_pack_cached(weight, self.num_levels, self.radius, self.legacy_wd_swap,
+                                      exact=self.precision == "fp32")
         if self._convc1_grad(weight, bias):
             return self._convc1_ad(coords, weight, bias, packed, self._corr)
         out = ops.lookup_proj(self._corr, coords.reshape(B, 3, H * W * D), packed, bias, H, W, D,

@@ -155,8 +155,9 @@ def lookup(corr: torch.Tensor, coords: torch.Tensor, H: int, W: int, D: int, num
     return out
 
 
-def proj_pack(weight: torch.Tensor, num_levels: int, radius: int, legacy: bool) -> torch.Tensor:
-    """convc1.weight (96, L*(2r+1)^3[, 1, 1, 1]) -> the fused kernel's packed fp16 operand (dvc_proj_pack)."""
+def proj_pack(weight: torch.Tensor, num_levels: int, radius: int, legacy: bool, exact: bool = False) -> torch.Tensor:
+    """convc1.weight (96, L*(2r+1)^3[, 1, 1, 1]) -> the fused kernel's packed fp16 operand (dvc_proj_pack), or for
+    fp32 pyramids (exact=True) its bf16 hi + lo blocks (dvc_proj_pack_exact, twice the bytes)."""
     _need_cuda(weight)
     w = _f32c(weight.detach().reshape(weight.shape[0], -1))
     nbytes = lib().dvc_proj_packed_bytes(num_levels, radius)
@@ -165,27 +166,29 @@ def proj_pack(weight: torch.Tensor, num_levels: int, radius: int, legacy: bool) 
     if w.shape[1] != num_levels * (2 * radius + 1) ** 3:
         raise ValueError(f"convc1 weight has {w.shape[1]} input channels; the lookup has "
                          f"{num_levels * (2 * radius + 1) ** 3}")
-    out = torch.empty((nbytes // 2,), dtype=torch.float16, device=w.device)
-    check(lib().dvc_proj_pack(_ptr(w), _ptr(out), w.shape[0], num_levels, radius,
-                              DVC_LEGACY if legacy else DVC_FIXED, _stream(w)), "proj_pack")
+    out = torch.empty(((2 if exact else 1) * nbytes // 2,), dtype=torch.float16, device=w.device)
+    fn = lib().dvc_proj_pack_exact if exact else lib().dvc_proj_pack
+    check(fn(_ptr(w), _ptr(out), w.shape[0], num_levels, radius, DVC_LEGACY if legacy else DVC_FIXED, _stream(w)),
+          "proj_pack")
     return out
 
 
 _PACK_CACHE: dict = {}
 
 
-def proj_pack_cached(weight: torch.Tensor, num_levels: int, radius: int, legacy: bool) -> torch.Tensor:
+def proj_pack_cached(weight: torch.Tensor, num_levels: int, radius: int, legacy: bool,
+                     exact: bool = False) -> torch.Tensor:
     """proj_pack, re-packed only when the weight changes: the packing is once per optimiser step, not once
     per lookup.  Entries belong to the weight tensor OBJECT (a weak reference, checked on every hit, and a
     finalizer that drops the entry), plus its in-place version counter and shape, so a new weight that
     lands on a freed weight's address never reuses the old packing."""
     import weakref
-    key = (id(weight), num_levels, radius, bool(legacy))
+    key = (id(weight), num_levels, radius, bool(legacy), bool(exact))
     hit = _PACK_CACHE.get(key)
     state = (weight._version, tuple(weight.shape), weight.device, weight.data_ptr())
     if hit is not None and hit[0]() is weight and hit[1] == state:
         return hit[2]
-    packed = proj_pack(weight, num_levels, radius, legacy)
+    packed = proj_pack(weight, num_levels, radius, legacy, exact)
     if hit is None or hit[0]() is not weight:
         weakref.finalize(weight, _PACK_CACHE.pop, key, None)
     _PACK_CACHE[key] = (weakref.ref(weight), state, packed)

@@ -4,7 +4,8 @@ Reference: CorrBlock.__call__ (src/core/corr.py:169-208) followed by MotionEncod
 F.relu(self.convc1(corr)) (src/core/update.py:219-222, 246).  On a bf16 block the fused kernel
 feeds the lookup values and the weights to fp16 MFMA with fp32 accumulation (as the reference's
 AMP convc1 runs in fp16), so the tolerance is the bf16 one of SURVEY.md 8(c): max|out - ref| /
-max|ref| <= 1e-2; an fp32 block keeps fp32 arithmetic and the fp32 tolerance 1e-5.  Against
+max|ref| <= 1e-2; an fp32 block (round 5) runs the exact split consumer -- lookup values and weights as bf16
+hi + lo, three MFMAs per step -- at the fp32 tolerance 1e-5.  Against
   * the reference's own outputs (tests/golden/proj_*.npz, gen_proj_golden.py),
   * the CPU oracle (f64 lookup + motion_convc1) on ragged / non-cubic / zero-level cases,
   * the unfused GPU composition relu(conv3d(lookup)) at the bench size (32^3, C=128, L=4, r=4).
@@ -140,3 +141,29 @@ def test_unsupported_radius_falls_back_and_direct_call_raises():
         ops.proj_pack(tw, 1, 5, False)
     with pytest.raises(ValueError):
         ops.proj_pack(tw[:, :100], 1, 4, False)
+
+
+def test_fp32_block_fused_exact_at_bench_size():
+    """fp32 pyramid (the reference's fp32 evaluation, evaluate_phase1.py:115-131) at the bench shape: the fused
+    exact consumer (dvc_proj_pack_exact + dvc_corr_lookup_proj, never the composition) against relu(conv3d(lookup))
+    on the same pyramid at 1e-5, and bitwise repeatable."""
+    import dvccorr
+    S, C, L, r = 32, 128, 4, 4
+    g = torch.Generator(device="cpu").manual_seed(79)
+    f1 = torch.randn(1, C, S, S, S, generator=g).to(DEV)
+    f2 = torch.randn(1, C, S, S, S, generator=g).to(DEV)
+    base = dvccorr.coords_grid_3d(1, S, S, S, DEV)
+    coords = base + (torch.rand(1, 3, S, S, S, generator=g) * 4 - 2).to(DEV)
+    w, b = (torch.from_numpy(a).to(DEV) for a in _conv_inputs(80, L, r))
+    blk = dvccorr.CorrBlock(f1, f2, L, r, precision="fp32")
+    ref = torch.relu(torch.nn.functional.conv3d(blk(coords), w.view(96, -1, 1, 1, 1), b))
+
+    def _no_composition(*a, **k):
+        raise AssertionError("fp32 lookup_convc1 took the composition")
+    blk._convc1_composition = _no_composition
+    out = blk.lookup_convc1(coords, w, b)
+    out2 = blk.lookup_convc1(coords, w, b)
+    torch.cuda.synchronize()
+    err = float((out - ref).abs().max() / ref.abs().max())
+    assert err < FP32_TOL, err
+    assert torch.equal(out, out2)
