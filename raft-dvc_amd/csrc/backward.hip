@@ -208,11 +208,22 @@ __device__ __forceinline__ unsigned f16_hilo(float g) {
 }
 
 // Window-gradient formats: fp32 (the VALU gradient kernels), or hi/lo pairs that ARE the MFMA kernels' A operand
-enum GwinFmt { kGwF32 = 0, kGwBf16 = 1, kGwF16 = 2 };
+// (fp32 blocks: kGwBf16 pairs with the split operands), or (round 5, kGwS16B / kGwS16H: bf16 / fp16 blocks) ONE
+// 16-bit value per window cell -- bf16 for bf16 blocks; fp16 for the AMP blocks, the rounding the reference's own AMP
+// backward applies to d(corr) (trainer.py:249-257) -- in rows of RZ = (nv + 2) & ~1 values: window row (i, j) of a
+// query holds target z = (iv & ~1) + e at element e (iv = the window's first z), zeros outside [iv, iv + nv), so
+// every row starts at an even target z and the consumers' 8-aligned z batches read it 4-byte aligned.  Per query
+// nh * nu * RZ / 2 dwords (a level's region is sized for the fp32 format: the rows are packed within it).
+enum GwinFmt { kGwF32 = 0, kGwBf16 = 1, kGwF16 = 2, kGwS16B = 3, kGwS16H = 4 };
 template <int FMT> __device__ __forceinline__ unsigned gw_pair(float g) {
     if constexpr (FMT == kGwF16) return f16_hilo(g);
     else return bf16_hilo(g);
 }
+template <int FMT> __device__ __forceinline__ unsigned gw_s16(float g) {   // one 16-bit value in the low half
+    if constexpr (FMT == kGwS16H) return (unsigned)__builtin_bit_cast(unsigned short, (_Float16)g);
+    else return (unsigned)__builtin_bit_cast(unsigned short, (__bf16)g);
+}
+__host__ __device__ constexpr int gw_rz(int nv) { return (nv + 2) & ~1; }   // S16 row length (values)
 
 // Round 4: the output gradients arrive through buffer loads (the (b, l) block's plane as a descriptor, the lane's
 // query as the vector offset, the channel as a scalar one) instead of per-lane 64-bit addresses: 330 -> 292 us at
@@ -229,9 +240,11 @@ template <int FMT> __device__ __forceinline__ unsigned gw_pair(float g) {
 // gradient column u = R is read by both halves: +11 % of the output-gradient reads).  Same arithmetic, same order,
 // bitwise-equal results (tools/ab_bwd.py --compare); 222 -> 214 us at config #3: the kernel moves its ~950 MB at
 // ~4.4 TB/s, the mixed read/write rate, so the occupancy bought little.
-template <int R> struct WinGradPCfg {
+template <int R, bool S16 = false> struct WinGradPCfg {
     static constexpr int NW = 2 * R + 2, HC = R + 1;        // window columns per half
-    static constexpr int SW = NW * NW + 4;                 // LDS image row (dwords) per query: 16-byte aligned
+    static constexpr int RZ2 = gw_rz(NW) / 2;               // S16: dwords per window row
+    // LDS image row (dwords) per query: 16-byte aligned (+4: bank spread)
+    static constexpr int SW = S16 ? ((NW * RZ2 + 3) & ~3) + 4 : NW * NW + 4;
     static constexpr int WAVES = 4;
     static constexpr int LDS = WAVES * 32 * SW * 4;
 };
@@ -240,8 +253,12 @@ template <int R> struct WinGradPCfg {
 // (same values, same arithmetic; win_grad_needs_g64 on the host picks it).
 template <int R, int FMT, bool G64 = false>
 __global__ __launch_bounds__(256) void k_win_grad_pairs(BwdArgs A) {
-    using G = WinGradPCfg<R>;
-    constexpr int n = 2 * R + 1, NW = G::NW, NW3 = NW * NW * NW, SW = G::SW, P16 = NW * NW / 4, HC = G::HC;
+    constexpr bool S16 = FMT == kGwS16B || FMT == kGwS16H;
+    using G = WinGradPCfg<R, S16>;
+    constexpr int n = 2 * R + 1, NW = G::NW, SW = G::SW, HC = G::HC, RZ2 = G::RZ2;
+    // dwords per query (S16: NW x NW rows of RZ2 dwords) and 16-byte pieces per window plane
+    constexpr int NW3 = S16 ? NW * NW * RZ2 : NW * NW * NW, PLD = S16 ? NW * RZ2 : NW * NW, P16 = PLD / 4;
+    static_assert(PLD % 4 == 0, "a window plane must be whole 16-byte pieces");
     constexpr int NCOL = R + 2;   // output-gradient columns u = U0 .. U0 + R + 1 of this lane's half
     constexpr unsigned kOff = 0x80000000u;   // a buffer offset past every range (reads 0, stores dropped)
     extern __shared__ __attribute__((aligned(16))) float wg_stage[];
@@ -272,6 +289,7 @@ __global__ __launch_bounds__(256) void k_win_grad_pairs(BwdArgs A) {
     WinAxes ax;
     bw_axes(A, l, cy, cx, cz, ax);
     const int ih = (int)ax.kh - R, iu = (int)ax.ku - R, iv = (int)ax.kv - R;
+    const bool odd_iv = (iv & 1) != 0;   // S16: the window's first z is odd -> its rows start one value in
     const int J0 = half * HC, U0 = J0 - 1;
     // this lane's column weights: window column j = J0 + jj takes wx0[j] (j < n) and wx1[j - 1] (j >= 1)
     float wj0[HC], wj1[HC], wz0[n], wz1[n];
@@ -363,11 +381,30 @@ __global__ __launch_bounds__(256) void k_win_grad_pairs(BwdArgs A) {
                 o[v] = __builtin_fmaf(wz0[v], gz, o[v]);
                 o[v + 1] = __builtin_fmaf(wz1[v], gz, o[v + 1]);
             }
-            u32x2 *dst = reinterpret_cast<u32x2 *>(img + ql * SW + (J0 + jj) * NW);
+            if constexpr (S16) {
+                // row (i, J0 + jj): element e = k + (iv & 1) holds window z k, zeros around it
+                unsigned *dr = reinterpret_cast<unsigned *>(img + ql * SW + (J0 + jj) * RZ2);
+                unsigned hv[NW + 2];
+                hv[0] = 0u;
 #pragma unroll
-            for (int k = 0; k < NW / 2; ++k) {
-                if constexpr (FMT != kGwF32) dst[k] = u32x2{gw_pair<FMT>(o[2 * k]), gw_pair<FMT>(o[2 * k + 1])};
-                else dst[k] = u32x2{__float_as_uint(o[2 * k]), __float_as_uint(o[2 * k + 1])};
+                for (int k = 0; k < NW; ++k) hv[k + 1] = gw_s16<FMT>(o[k]);
+                hv[NW + 1] = 0u;
+#pragma unroll
+                for (int d = 0; d < RZ2; ++d) {
+                    // elements (2d, 2d + 1): even iv (hv[2d + 1], hv[2d + 2]), odd iv (hv[2d], hv[2d + 1])
+                    constexpr int LAST = NW + 1;
+                    const unsigned hi_even = 2 * d + 2 <= LAST ? hv[2 * d + 2 <= LAST ? 2 * d + 2 : 0] : 0u;
+                    const unsigned e0 = odd_iv ? hv[2 * d] : hv[2 * d + 1];
+                    const unsigned e1 = odd_iv ? hv[2 * d + 1] : hi_even;
+                    dr[d] = e0 | (e1 << 16);
+                }
+            } else {
+                u32x2 *dst = reinterpret_cast<u32x2 *>(img + ql * SW + (J0 + jj) * NW);
+#pragma unroll
+                for (int k = 0; k < NW / 2; ++k) {
+                    if constexpr (FMT != kGwF32) dst[k] = u32x2{gw_pair<FMT>(o[2 * k]), gw_pair<FMT>(o[2 * k + 1])};
+                    else dst[k] = u32x2{__float_as_uint(o[2 * k]), __float_as_uint(o[2 * k + 1])};
+                }
             }
 #pragma unroll
             for (int v = 0; v < n; ++v) Pp[v] = Pc[v];
@@ -391,7 +428,7 @@ __global__ __launch_bounds__(256) void k_win_grad_pairs(BwdArgs A) {
                 const int ihq = __shfl(ih, qq);   // (lane qq holds query qq: ql = lane & 31)
                 const bool ok = g0 + u < NIT && c < 32 * P16 && (unsigned)(ihq + i) < (unsigned)Hl;
                 v[u] = *reinterpret_cast<const u32x4 *>(img + qq * SW + pc * 4);
-                off[u] = ok ? (qq * NW3 + i * NW * NW + pc * 4) * 4 : (int)kOff;
+                off[u] = ok ? (qq * NW3 + i * PLD + pc * 4) * 4 : (int)kOff;
             }
 #pragma unroll
             for (int u = 0; u < FG; ++u)
@@ -766,7 +803,11 @@ __device__ __forceinline__ bf16x8 dup_bf16x4(u32x2 v) {
 // element bsort (lfirst = nsl > 0, launched after the sort beside the sorted groups so that one launch fills the
 // chip), or every batch element's boxes over the gridDim.y level groups (lfirst = 0, nsl = 0).  Partial sums: sorted
 // level l slot l, boxes with lfirst > 0 slot lfirst, else slot blockIdx.y.
-template <int NCT, bool F16, bool SPLIT = false>   // channel tiles of 32 (C_pad / 32, <= 4 per launch); fp16 operands
+// G16 (round 5, bf16 / fp16 blocks): the window gradients as single 16-bit values (kGwS16B / kGwS16H rows): the G tile
+// of a batch is [64 queries][16 z] 16-bit (2 KB, two 16-byte DMAs per query by waves 0-1; waves 2-3 issue an empty DMA
+// into a spare region so that every wave counts the same DMAs), K = the batch's 16 z in ONE MFMA per query block
+// (the pair format needs two), and the B operand is the target tile's 8 z as they stand.
+template <int NCT, bool F16, bool SPLIT = false, bool G16 = false>   // channel tiles of 32 (C_pad / 32, <= 4 per launch)
 __global__ __launch_bounds__(256, kQOcc<SPLIT>) void k_grad_q_mfma(const bf16_t *__restrict__ Tz, float *__restrict__ dQp,
                                                         long long part_stride, BwdArgs A, long long tz_lo,
                                                         const unsigned long long *__restrict__ skeys, int bsort,
@@ -851,7 +892,8 @@ __global__ __launch_bounds__(256, kQOcc<SPLIT>) void k_grad_q_mfma(const bf16_t 
         // the box's window gradients of this level as one buffer (the box spans < 4 (W, D) planes of queries), its
         // base 16 bytes early: a 16-byte chunk may start up to 3 values before a window row (those values, like the
         // ones past its end, belong to other rows and are masked when the operand is read)
-        const int nw3 = (int)bw_nw3(A, l);
+        const int rz = gw_rz(nv);                                          // G16: values per window row
+        const int nw3 = G16 ? nh * nu * (rz >> 1) : (int)bw_nw3(A, l);   // dwords per query
         const long long gspan = srt ? A.Nq : 3LL * A.Wq * A.Dq + 3 * A.Dq + 4;   // queries the buffer covers
         const u32x4 rs_g = sgpr_rsrc(A.gwin + A.goff[l] + ((long long)b * A.Nq + qb0) * nw3 - 4,
                                      (unsigned)min(gspan * nw3 * 4 + 32, 0x7fffffffLL));
@@ -859,7 +901,17 @@ __global__ __launch_bounds__(256, kQOcc<SPLIT>) void k_grad_q_mfma(const bf16_t 
         // addresser's instruction count bound the kernel): query gq = 16 w + lane / 4, physical chunk lane & 3 of its
         // 64-byte row = logical z chunk (lane & 3) ^ (gq >> 2 & 3)
         int goh, gou, gov, gqo;
-        {
+        if constexpr (G16) {
+            // waves 0-1: query gq = 32 w + lane / 2, physical 16-byte chunk lane & 1 of its 32-byte row = logical z chunk
+            // (lane & 1) ^ (gq >> 3 & 1); gov = the element of target z 0 minus 8 x that chunk
+            const int gq = 32 * (w & 1) + (lane >> 1);
+            const bool lv = __shfl((int)live, gq) != 0;
+            const int sh = __shfl(ih, gq);
+            goh = lv && w < 2 ? sh : -BIG;   // (waves 2-3: the spare DMA, every offset out of range)
+            gou = __shfl(iu, gq);
+            gov = (__shfl(iv, gq) & ~1) - 8 * ((lane & 1) ^ ((gq >> 3) & 1));
+            gqo = __shfl(qrel, gq) * nw3;
+        } else {
             const int gq = 16 * w + (lane >> 2);
             // (every shuffle runs on all lanes: under a branch, ds_bpermute reads 0 from switched-off lanes)
             const bool lv = __shfl((int)live, gq) != 0;
@@ -887,9 +939,15 @@ __global__ __launch_bounds__(256, kQOcc<SPLIT>) void k_grad_q_mfma(const bf16_t 
             }
             if (!(DVC_GQ_ABL & 2)) {
                 const int wy = y - goh, wx = x - gou, wz = z0 - gov;
-                const bool ok = (unsigned)wy < (unsigned)nh && (unsigned)wx < (unsigned)nu && wz > -4 && wz < nv;
-                blds(rs_g, ok ? (unsigned)(gqo + (wy * nu + wx) * nv + wz) * 4u + 16u : kOOB, 0u, sb + 4096 + 1024 * w,
-                     W16{});
+                if constexpr (G16) {   // wz = the chunk's first element in the row (even)
+                    const bool ok = (unsigned)wy < (unsigned)nh && (unsigned)wx < (unsigned)nu && wz > -8 && wz < rz;
+                    blds(rs_g, ok ? (unsigned)(2 * gqo + (wy * nu + wx) * rz + wz) * 2u + 16u : kOOB, 0u,
+                         sb + 4096 + 1024 * w, W16{});
+                } else {
+                    const bool ok = (unsigned)wy < (unsigned)nh && (unsigned)wx < (unsigned)nu && wz > -4 && wz < nv;
+                    blds(rs_g, ok ? (unsigned)(gqo + (wy * nu + wx) * nv + wz) * 4u + 16u : kOOB, 0u,
+                         sb + 4096 + 1024 * w, W16{});
+                }
             }
         };
         // the batches: every z batch of each union row some window of the box contains, listed by wave 0 (lane =
@@ -929,7 +987,28 @@ __global__ __launch_bounds__(256, kQOcc<SPLIT>) void k_grad_q_mfma(const bf16_t 
                 __builtin_amdgcn_s_barrier();
                 asm volatile("" ::: "memory");
                 issue(min(it + kQStages - 1, nit - 1), (it + kQStages - 1) % kQStages);
-                if (w < NCT && !(DVC_GQ_ABL & 1)) {
+                if (G16 && w < NCT && !(DVC_GQ_ABL & 1)) {
+                    const unsigned char *sb = stg + (it % kQStages) * STAGE;
+                    const int r = 32 * w + m, rsw = (r >> 3) & 1;
+                    const int bz0 = (int)(__builtin_amdgcn_readfirstlane(qrows[it]) >> 22);   // the batch's z0
+                    // B: this lane's 8 targets z = 8 h .. 8 h + 7 of channel r
+                    const bf16x8 bt = *reinterpret_cast<const bf16x8 *>(sb + r * 32 + 16 * (h ^ rsw));
+#pragma unroll
+                    for (int T = 0; T < 2; ++T) {
+                        const int gq = 32 * T + m;
+                        u32x4 av = *reinterpret_cast<const u32x4 *>(sb + 4096 + gq * 32 + 16 * (h ^ ((gq >> 3) & 1)));
+                        // targets z = bz0 + 8 h + i: their window z of query gq must lie in [0, nv) (the 16 values
+                        // of a batch straddle the 12-value rows: the neighbouring rows' values are dropped)
+                        const int wz0 = bz0 + 8 * h - ivq[T];
+#pragma unroll
+                        for (int d = 0; d < 4; ++d) {
+                            const unsigned mlo = (unsigned)(wz0 + 2 * d) < (unsigned)nv ? 0x0000ffffu : 0u;
+                            const unsigned mhi = (unsigned)(wz0 + 2 * d + 1) < (unsigned)nv ? 0xffff0000u : 0u;
+                            av[d] &= mlo | mhi;
+                        }
+                        acc[T] = mma32<F16>(__builtin_bit_cast(bf16x8, av), bt, acc[T]);
+                    }
+                } else if (w < NCT && !(DVC_GQ_ABL & 1)) {
                     const unsigned char *sb = stg + (it % kQStages) * STAGE;
                     const int r = 32 * w + m, rsw = (r >> 3) & 1;
                     const int bz0 = (int)(__builtin_amdgcn_readfirstlane(qrows[it]) >> 22);   // the batch's z0
@@ -1265,7 +1344,11 @@ __global__ __launch_bounds__(256) void k_qt_tiles(const TT *__restrict__ Q, cons
 // Every load is unconditional (out-of-window gradients read the zero guard before the window gradients), so
 // hipcc's counted waits name exactly the set about to be stored.
 constexpr int kTCap = 32;   // batches listed at a time
-template <int NCT, bool F16, bool SPLIT = false>   // channel tiles of 32 (C_pad / 32, <= 4 per launch); fp16 operands
+// G16 (round 5, bf16 / fp16 blocks): the window gradients as single 16-bit values (kGwS16B / kGwS16H rows): a thread
+// loads its 4 targets' values as 8 bytes (the row element of target z is z - (origin & ~1): even for the brick's
+// 4-aligned z), the staged G tile is [64 targets][16 queries] 16-bit, and K = the batch's 16 queries in ONE MFMA per
+// target block, the query tile's 8 queries as they stand (the pair format needs two MFMAs and duplicated queries).
+template <int NCT, bool F16, bool SPLIT = false, bool G16 = false>   // channel tiles of 32 (C_pad / 32, <= 4 per launch)
 __global__ __launch_bounds__(256, SPLIT ? 3 : 4) void k_grad_t_mfma(const bf16_t *__restrict__ Qz, long long ntq,
                                                         const unsigned long long *__restrict__ keys,
                                                         const int *__restrict__ starts, float *__restrict__ dT,
@@ -1275,13 +1358,15 @@ __global__ __launch_bounds__(256, SPLIT ? 3 : 4) void k_grad_t_mfma(const bf16_t
     starts += A.coff[l];
     __shared__ __attribute__((aligned(16))) bf16_t Ql[2][2048];     // [buf] query tile [128 ch][16] (swizzled)
     __shared__ __attribute__((aligned(16))) bf16_t Qll[SPLIT ? 2 : 1][SPLIT ? 2048 : 8];   // [buf] its lo tile
-    __shared__ __attribute__((aligned(16))) unsigned Gq[2][64][16];  // [buf][target][query] hi/lo pairs (swizzled)
+    // [buf][target][query] hi/lo pairs (swizzled); G16: [buf][target][16 queries] 16-bit in 8 dwords
+    __shared__ __attribute__((aligned(16))) unsigned Gq[2][64][G16 ? 8 : 16];
     __shared__ int tq[kTCap][16], tzr[kTCap][16];   // listed batch e, query j: query id (-1: none), origin z - oz0
     const int tid = threadIdx.x, lane = tid & 63, m = lane & 31, h = lane >> 5;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
     const int nh = A.nwh[l], nu = A.nwu[l], nv = A.nwv[l];
-    const long long nw3 = bw_nw3(A, l);
+    const int rz = gw_rz(nv);   // G16: values per window row
+    const long long nw3 = G16 ? (long long)nh * nu * (rz >> 1) : bw_nw3(A, l);   // dwords per query
     const int nbz = (Dl + 3) >> 2, nbx = (Wl + 3) >> 2, nby = (Hl + 3) >> 2;
     int t = brick;
     const int bz = t % nbz; t /= nbz;
@@ -1309,7 +1394,7 @@ __global__ __launch_bounds__(256, SPLIT ? 3 : 4) void k_grad_t_mfma(const bf16_t
     int e_row = 0, e_p = 0, e_base = 0, e_nk = 0;
     int cnt = 0;
     struct Set {
-        u32x4 q, ql, g;
+        u32x4 q, ql, g;   // (G16: g[0..1] = the 4 targets' 16-bit values)
         unsigned mk;   // bit k: target z tz0 + k inside the query's window row and the level
     };
     auto load = [&](int i, int n, Set &S) __attribute__((always_inline)) {   // batch min(i, n - 1): every load unconditional
@@ -1324,9 +1409,17 @@ __global__ __launch_bounds__(256, SPLIT ? 3 : 4) void k_grad_t_mfma(const bf16_t
         const int qq = tq[e][sj];
         const int pz0 = tz0 - tzr[e][sj] + nv - 1;
         const bool ok = qq >= 0 && yxok && pz0 > -4 && pz0 < nv;
-        // (4 consecutive window z: one 16-byte load; values outside the window row are masked at the store)
-        const unsigned *src = ok ? glp + (long long)qq * nw3 + (py * nu + px) * nv + pz0 : gzero;
-        __builtin_memcpy(&S.g, src, 16);
+        // (4 consecutive window z: one 16-byte load, G16 one 8-byte load; values outside the window row are masked
+        // at the store)
+        if constexpr (G16) {
+            const unsigned short *g16 = reinterpret_cast<const unsigned short *>(glp);
+            const unsigned short *src16 = ok ? g16 + 2 * (long long)qq * nw3 + (py * nu + px) * rz + pz0 + (pz0 & 1)
+                                             : reinterpret_cast<const unsigned short *>(gzero);
+            __builtin_memcpy(&S.g, src16, 8);
+        } else {
+            const unsigned *src = ok ? glp + (long long)qq * nw3 + (py * nu + px) * nv + pz0 : gzero;
+            __builtin_memcpy(&S.g, src, 16);
+        }
         unsigned mk = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) mk |= ((unsigned)(pz0 + k) < (unsigned)nv && tz0 + k < Dl) ? 1u << k : 0u;
@@ -1335,6 +1428,15 @@ __global__ __launch_bounds__(256, SPLIT ? 3 : 4) void k_grad_t_mfma(const bf16_t
     auto store = [&](int bb, const Set &S) __attribute__((always_inline)) {
         *reinterpret_cast<u32x4 *>(&Ql[bb][8 * tid]) = S.q;
         if constexpr (SPLIT) *reinterpret_cast<u32x4 *>(&Qll[bb][8 * tid]) = S.ql;
+        if constexpr (G16) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {   // target 4 sr + k, query sj: 8-query chunk (sj / 8) ^ (row >> 3 & 1)
+                const int tr = 4 * sr + k;
+                const unsigned short v = (S.mk >> k) & 1u ? (unsigned short)(S.g[k >> 1] >> (16 * (k & 1))) : 0;
+                reinterpret_cast<unsigned short *>(Gq[bb][tr])[8 * ((sj >> 3) ^ ((tr >> 3) & 1)) + (sj & 7)] = v;
+            }
+            return;
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {   // target 4 sr + k, query sj: chunk (sj / 4) ^ (row >> 2 & 3)
             const int tr = 4 * sr + k;
@@ -1344,6 +1446,17 @@ __global__ __launch_bounds__(256, SPLIT ? 3 : 4) void k_grad_t_mfma(const bf16_t
     auto compute = [&](int bb) __attribute__((always_inline)) {
         if (w >= NCT) return;
         const int r = 32 * w + m, rsw = (r >> 3) & 1;
+        if constexpr (G16) {   // K = the batch's 16 queries: B = this lane's queries 8 h .. 8 h + 7 of channel r
+            const bf16x8 bq = *reinterpret_cast<const bf16x8 *>(reinterpret_cast<const unsigned char *>(Ql[bb]) +
+                                                                 r * 32 + 16 * (h ^ rsw));
+#pragma unroll
+            for (int T = 0; T < 2; ++T) {
+                const int tr = 32 * T + m;
+                const bf16x8 ag = *reinterpret_cast<const bf16x8 *>(&Gq[bb][tr][4 * (h ^ ((tr >> 3) & 1))]);
+                acc[T] = mma32<F16>(ag, bq, acc[T]);
+            }
+            return;
+        }
 #pragma unroll
         for (int j = 0; j < 2; ++j) {   // queries 8 j .. 8 j + 7: K = 16 (query, hi/lo) pairs
             const u32x2 qv = *reinterpret_cast<const u32x2 *>(
@@ -1713,6 +1826,10 @@ void set_backward_mfma(int v) { g_bwd_mfma = v; }
 // row range, win_grad_needs_g64)
 static thread_local int g_bwd_g64 = 0;
 void set_backward_g64(int v) { g_bwd_g64 = v; }
+// 1 (default): bf16 / fp16 blocks store single 16-bit window gradients (kGwS16B / kGwS16H, round 5); 0: the hi/lo
+// pairs of round 4 (tuning "bwd_g16", for A/B and to keep the pair path tested on 16-bit blocks)
+static thread_local int g_bwd_g16 = 1;
+void set_backward_g16(int v) { g_bwd_g16 = v; }
 
 // dtype codes of the packed operands whose gradient sums run on the matrix cores (the rest: VALU)
 int backward_uses_mfma(int B, long long Nq, const dvc_layout &lay, int radius, int convention, int dtype) {
@@ -1762,26 +1879,32 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     const bool mfma = g_bwd_mfma && mfma_offsets_fit(A, P);
     const long long tz_lo = (long long)A.B * ngroups * P.tz0[A.L] * 2048;   // lo tiles: elements after the hi ones
     const long long qz_lo = (long long)P.ntq * ngroups * 2048;
-    const int fmt = mfma ? (F16 ? kGwF16 : kGwBf16) : kGwF32;
+    bool any_generic = false;
+    for (int l = 0; l < A.L; ++l) any_generic |= A.generic[l] != 0;
+    // single 16-bit window gradients (round 5) for bf16 / fp16 blocks on the matrix cores; the fp32 blocks' split
+    // operands keep the hi/lo pairs, and so do pyramids with a legacy W != D level (k_win_grad_generic's boxes)
+    const bool g16 = mfma && !SPLIT && !any_generic && g_bwd_g16;
+    const int fmt = g16 ? (F16 ? kGwS16H : kGwS16B) : mfma ? (F16 ? kGwF16 : kGwBf16) : kGwF32;
     const unsigned wgrid = (unsigned)((A.B * A.L * nqb + 3) / 4);
     {   // two lanes per query (k_win_grad_pairs)
-        using WG = WinGradPCfg<R>;
         const long long nqb2 = (A.Nq + 31) / 32;
-        const unsigned wg_grid = (unsigned)((A.B * A.L * nqb2 + WG::WAVES - 1) / WG::WAVES);
-        auto launch_wg = [&](auto kern) {
-            (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, WG::LDS);
-            kern<<<wg_grid, 64 * WG::WAVES, WG::LDS, s>>>(A);
+        const unsigned wg_grid = (unsigned)((A.B * A.L * nqb2 + 3) / 4);
+        auto launch_wg = [&](auto kern, int lds) {
+            (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+            kern<<<wg_grid, 256, lds, s>>>(A);
         };
+        static_assert(WinGradPCfg<R>::WAVES == 4 && WinGradPCfg<R, true>::WAVES == 4, "four waves per workgroup");
+        const int lp = WinGradPCfg<R>::LDS, l16 = WinGradPCfg<R, true>::LDS;
         const bool g64 = g_bwd_g64 || win_grad_needs_g64(A.Nq, R);
         switch (fmt) {
-        case kGwF16: g64 ? launch_wg(k_win_grad_pairs<R, kGwF16, true>) : launch_wg(k_win_grad_pairs<R, kGwF16>); break;
-        case kGwBf16: g64 ? launch_wg(k_win_grad_pairs<R, kGwBf16, true>) : launch_wg(k_win_grad_pairs<R, kGwBf16>); break;
-        default: g64 ? launch_wg(k_win_grad_pairs<R, kGwF32, true>) : launch_wg(k_win_grad_pairs<R, kGwF32>); break;
+        case kGwS16H: g64 ? launch_wg(k_win_grad_pairs<R, kGwS16H, true>, l16) : launch_wg(k_win_grad_pairs<R, kGwS16H>, l16); break;
+        case kGwS16B: g64 ? launch_wg(k_win_grad_pairs<R, kGwS16B, true>, l16) : launch_wg(k_win_grad_pairs<R, kGwS16B>, l16); break;
+        case kGwF16: g64 ? launch_wg(k_win_grad_pairs<R, kGwF16, true>, lp) : launch_wg(k_win_grad_pairs<R, kGwF16>, lp); break;
+        case kGwBf16: g64 ? launch_wg(k_win_grad_pairs<R, kGwBf16, true>, lp) : launch_wg(k_win_grad_pairs<R, kGwBf16>, lp); break;
+        default: g64 ? launch_wg(k_win_grad_pairs<R, kGwF32, true>, lp) : launch_wg(k_win_grad_pairs<R, kGwF32>, lp); break;
         }
     }
     if (!launched("win_grad")) return DVC_ERR_LAUNCH;
-    bool any_generic = false;
-    for (int l = 0; l < A.L; ++l) any_generic |= A.generic[l] != 0;
     if (any_generic) {
         switch (fmt) {
         case kGwF16: k_win_grad_generic<R, kGwF16><<<wgrid, 256, 0, s>>>(A); break;
@@ -1805,12 +1928,17 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
         for (int g = 0; g < ngroups; ++g) {
             BwdArgs Ag = A;
             Ag.cbase = 128 * g;
-            switch (std::min(128, A.Cp - Ag.cbase) / 32) {
-            case 1: k_grad_q_mfma<1, F16, SPLIT><<<grid, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo, sk, bs, ns, nsl_, lfirst); break;
-            case 2: k_grad_q_mfma<2, F16, SPLIT><<<grid, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo, sk, bs, ns, nsl_, lfirst); break;
-            case 3: k_grad_q_mfma<3, F16, SPLIT><<<grid, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo, sk, bs, ns, nsl_, lfirst); break;
-            default: k_grad_q_mfma<4, F16, SPLIT><<<grid, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo, sk, bs, ns, nsl_, lfirst); break;
-            }
+            auto go = [&](auto g16c) {
+                constexpr bool GG = decltype(g16c)::value && !SPLIT;
+                switch (std::min(128, A.Cp - Ag.cbase) / 32) {
+                case 1: k_grad_q_mfma<1, F16, SPLIT, GG><<<grid, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo, sk, bs, ns, nsl_, lfirst); break;
+                case 2: k_grad_q_mfma<2, F16, SPLIT, GG><<<grid, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo, sk, bs, ns, nsl_, lfirst); break;
+                case 3: k_grad_q_mfma<3, F16, SPLIT, GG><<<grid, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo, sk, bs, ns, nsl_, lfirst); break;
+                default: k_grad_q_mfma<4, F16, SPLIT, GG><<<grid, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo, sk, bs, ns, nsl_, lfirst); break;
+                }
+            };
+            if (g16) go(std::true_type{});
+            else go(std::false_type{});
         }
     };
     bool done_q = false;
@@ -1893,12 +2021,17 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
                 for (int cg = 0; cg < ngroups; ++cg) {
                     BwdArgs Ag = A;
                     Ag.cbase = 128 * cg;
-                    switch (std::min(128, A.Cp - Ag.cbase) / 32) {
-                    case 1: k_grad_t_mfma<1, F16, SPLIT><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b, qz_lo); break;
-                    case 2: k_grad_t_mfma<2, F16, SPLIT><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b, qz_lo); break;
-                    case 3: k_grad_t_mfma<3, F16, SPLIT><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b, qz_lo); break;
-                    default: k_grad_t_mfma<4, F16, SPLIT><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b, qz_lo); break;
-                    }
+                    auto go = [&](auto g16c) {
+                        constexpr bool GG = decltype(g16c)::value && !SPLIT;
+                        switch (std::min(128, A.Cp - Ag.cbase) / 32) {
+                        case 1: k_grad_t_mfma<1, F16, SPLIT, GG><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b, qz_lo); break;
+                        case 2: k_grad_t_mfma<2, F16, SPLIT, GG><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b, qz_lo); break;
+                        case 3: k_grad_t_mfma<3, F16, SPLIT, GG><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b, qz_lo); break;
+                        default: k_grad_t_mfma<4, F16, SPLIT, GG><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b, qz_lo); break;
+                        }
+                    };
+                    if (g16) go(std::true_type{});
+                    else go(std::false_type{});
                 }
                 done_t = true;
             }

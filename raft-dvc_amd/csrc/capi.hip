@@ -64,6 +64,7 @@ int backward_uses_mfma(int B, long long Nq, const dvc_layout &lay, int radius, i
 void set_backward_mfma(int v);
 bool win_grad_needs_g64(long long Nq, int radius);
 void set_backward_g64(int v);
+void set_backward_g16(int v);
 __global__ void k_coords_grid(float *, long long, int, int, int);
 template <bool DELTA, bool SUBGRID, int VEC, bool STAGED>
 __global__ void k_upflow(const float *, const float *, float *, float *, long long, int, int, int, int, int, int, int,
@@ -359,6 +360,11 @@ int dvc_set_tuning(const char *key, int value) {
     if (!strcmp(key, "bwd_mfma")) {   // 1 = gradient sums on the matrix cores (default), 0 = the VALU kernels
         if (value < 0 || value > 1) return fail(DVC_ERR_INVALID, "set_tuning: bwd_mfma %d", value);
         set_backward_mfma(value);
+        return DVC_OK;
+    }
+    if (!strcmp(key, "bwd_g16")) {   // 1 = single 16-bit window gradients for bf16 / fp16 blocks, 0 = hi/lo pairs
+        if (value < 0 || value > 1) return fail(DVC_ERR_INVALID, "set_tuning: bwd_g16 %d", value);
+        set_backward_g16(value);
         return DVC_OK;
     }
     if (!strcmp(key, "bwd_gout64")) {   // 1 = the window-gradient pass's 64-bit-addressed instance at every size

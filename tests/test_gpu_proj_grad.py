@@ -8,7 +8,8 @@ own output (y > 0): where the pre-activation is within the fp16 MFMA's ~1e-3 of 
 ReLU differently, which is a discontinuity, not an error of the gradient; the test checks that the decisions agree
 on >= 99.5 % of the outputs and then compares the gradients of the same piecewise-linear function.
 Shapes: grad_cfg2 (config #2's 16^3, C = 128, L = 4, r = 4, reference-seeded inputs) and a ragged 12x10x16 case.
-Tolerances (max|gpu - ref| / max|ref|): bf16 blocks 1e-2, fp16 (AMP) blocks 5e-3.
+Tolerances (max|gpu - ref| / max|ref|): bf16 blocks 1e-2, fp16 (AMP) blocks 5e-3, fp32 (materialised, the exact
+split convc1) 1e-5.
 """
 from __future__ import annotations
 
@@ -23,7 +24,7 @@ from oracle import oracle as orc
 pytestmark = pytest.mark.gpu
 
 DEV = torch.device("cuda:0")
-TOL = {"bf16": 1e-2, "fp16": 5e-3}
+TOL = {"bf16": 1e-2, "fp16": 5e-3, "fp32": 1e-5}
 
 
 def _case(name):
@@ -55,8 +56,8 @@ def _oracle(f1, f2, coords, w, b, gy, mask, L, r, legacy):
     return pre.detach().numpy(), t1.grad.numpy(), t2.grad.numpy(), tw.grad.numpy(), tb.grad.numpy()
 
 
-@pytest.mark.parametrize("kind", ["gemm", "fused"])
-@pytest.mark.parametrize("precision", ["bf16", "fp16"])
+@pytest.mark.parametrize("precision,kind", [("bf16", "gemm"), ("bf16", "fused"), ("fp16", "gemm"), ("fp16", "fused"),
+                                            ("fp32", "gemm")])
 @pytest.mark.parametrize("case", ["grad_cfg2", "ragged"])
 def test_lookup_convc1_grad(case, precision, kind):
     import dvccorr

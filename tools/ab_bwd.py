@@ -26,7 +26,11 @@ ap.add_argument("--precision", default="bf16")
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--save", default="")
 ap.add_argument("--compare", default="")
+ap.add_argument("--tune", default="", help="comma list key=value of dvc_set_tuning knobs (e.g. bwd_g16=0)")
 a = ap.parse_args()
+for kv in filter(None, a.tune.split(",")):
+    k, v = kv.split("=")
+    ops._lib.set_tuning(k, int(v))
 dev = torch.device("cuda:0")
 S, C, L, R = a.size, a.channels, a.levels, a.radius
 H, W, D = (int(v) for v in a.shape.split(",")) if a.shape else (S, S, S)
@@ -54,7 +58,7 @@ for _ in range(a.reps):
 d1b, d2b = ops.corr_backward(q, t, cf, gout, C, H, W, D, L, R, False, dt)
 torch.cuda.synchronize()
 rep = bool(torch.equal(d1, d1b) and torch.equal(d2, d2b))
-print(f"lib={os.path.basename(os.environ.get('DVCCORR_LIB', 'libdvccorr.so'))} size={S} C={C} {a.precision} "
+print(f"lib={os.path.basename(os.environ.get('DVCCORR_LIB', 'libdvccorr.so'))} tune={a.tune} size={S} C={C} {a.precision} "
       f"backward median {statistics.median(ts):.4f} ms min {min(ts):.4f} repeatable={rep}")
 if a.save:
     torch.save({"d1": d1.cpu(), "d2": d2.cpu()}, a.save)
