@@ -119,7 +119,10 @@ struct GtBlock {
 __device__ __forceinline__ GtBlock gt_block(const BwdArgs &A) {
     // (round 4: runs of 64 blocks per XCD -- the window gradients of a brick's queries are re-read by its
     // neighbours: L2 hit rate 0.21 and 1.7 GB of HBM reads per launch at config #3 with consecutive bricks on
-    // different XCDs; one contiguous run per XCD instead put level 0's heavy bricks on three XCDs: 286 -> 450 us)
+    // different XCDs; one contiguous run per XCD instead put level 0's heavy bricks on three XCDs: 286 -> 450 us.
+    // Round 5: each XCD's run as a 4x4x4 cube of bricks instead of a brick layer: bitwise equal, 0.5 % slower; the
+    // sorted dQ pass on a side stream beside this kernel: both kernels 1.4-1.8x longer, no net gain -- they share the
+    // memory system, not idle issue slots)
     const int bx = xcd_block_grouped<DVC_GT_XCD>((int)blockIdx.x, (int)gridDim.x);
     int l = 0;
     while (l + 1 < A.L && bx >= A.gt_blk0[l + 1]) ++l;
@@ -240,11 +243,15 @@ __host__ __device__ constexpr int gw_rz(int nv) { return (nv + 2) & ~1; }   // S
 // gradient column u = R is read by both halves: +11 % of the output-gradient reads).  Same arithmetic, same order,
 // bitwise-equal results (tools/ab_bwd.py --compare); 222 -> 214 us at config #3: the kernel moves its ~950 MB at
 // ~4.4 TB/s, the mixed read/write rate, so the occupancy bought little.
+// S16 image rows: 16-byte aligned with an ODD number of 16-byte units, so that the 32 queries' rows start on 16
+// different 4-bank groups (a power-of-two row put all 32 on the same banks: 88 % of the LDS cycles were conflicts;
+// fixing it did not move the kernel's time, which its HBM traffic sets)
+constexpr int sw_odd16(int d) { return ((((d + 3) >> 2) | 1) << 2); }
 template <int R, bool S16 = false> struct WinGradPCfg {
     static constexpr int NW = 2 * R + 2, HC = R + 1;        // window columns per half
     static constexpr int RZ2 = gw_rz(NW) / 2;               // S16: dwords per window row
     // LDS image row (dwords) per query: 16-byte aligned (+4: bank spread)
-    static constexpr int SW = S16 ? ((NW * RZ2 + 3) & ~3) + 4 : NW * NW + 4;
+    static constexpr int SW = S16 ? sw_odd16(NW * RZ2) : NW * NW + 4;
     static constexpr int WAVES = 4;
     static constexpr int LDS = WAVES * 32 * SW * 4;
 };

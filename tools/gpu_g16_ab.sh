@@ -1,8 +1,8 @@
 set -u
 O=gpurun_out/r5m; mkdir -p $O
 for p in bf16 fp16; do
-  timeout -k 10 120 python tools/ab_bwd.py --precision $p --tune bwd_g16=0 --save $O//tmp/base_$p.pt > $O/ab_$p.txt 2>&1 || { cat $O/ab_$p.txt; exit 1; }
-  timeout -k 10 120 python tools/ab_bwd.py --precision $p --tune bwd_g16=1 --compare $O//tmp/base_$p.pt >> $O/ab_$p.txt 2>&1 || { cat $O/ab_$p.txt; exit 1; }
+  timeout -k 10 120 python tools/ab_bwd.py --precision $p --tune bwd_g16=0 --save /tmp/base_$p.pt > $O/ab_$p.txt 2>&1 || { cat $O/ab_$p.txt; exit 1; }
+  timeout -k 10 120 python tools/ab_bwd.py --precision $p --tune bwd_g16=1 --compare /tmp/base_$p.pt >> $O/ab_$p.txt 2>&1 || { cat $O/ab_$p.txt; exit 1; }
   timeout -k 10 120 python tools/ab_bwd.py --precision $p --tune bwd_g16=0 >> $O/ab_$p.txt 2>&1 || exit 1
   timeout -k 10 120 python tools/ab_bwd.py --precision $p --tune bwd_g16=1 >> $O/ab_$p.txt 2>&1 || exit 1
   cat $O/ab_$p.txt
