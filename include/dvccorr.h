@@ -174,6 +174,11 @@ int dvc_corr_lookup_fused(const void *packed_q, const void *packed_t, const floa
  * both conventions on every level shape (legacy levels with W != D use a stretched
  * window box).  The workspace size covers either convention. */
 size_t dvc_corr_backward_workspace_bytes(int B, int64_t Nq, int C, int H, int W, int D, int num_levels, int radius);
+/* The workspace of dvc_corr_backward for one packed dtype: bf16 / fp16 operands need no lo tiles, so
+ * their workspace is smaller than the dtype-less query's (~88 MB less at config #3); 0 for a bad dtype.  Either
+ * query's size is enough for a call with that dtype. */
+size_t dvc_corr_backward_workspace_bytes_dtype(int B, int64_t Nq, int C, int H, int W, int D, int num_levels,
+                                               int radius, int dtype);
 int dvc_corr_backward(const void *packed_q, const void *packed_t, const float *coords, const float *grad_out,
                       float *grad_fmap1, float *grad_fmap2, void *workspace, int B, int64_t Nq, int C, int H, int W,
                       int D, int num_levels, int radius, int convention, int dtype, void *stream);

@@ -35,6 +35,7 @@
 #include <cmath>
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include "common.h"
 #include "lookup_common.h"
@@ -1073,15 +1074,55 @@ __global__ __launch_bounds__(256, kQOcc<SPLIT>) void k_grad_q_mfma(const bf16_t 
         }
 }
 
+template <int R>
+__device__ __forceinline__ long long bw_key_cell(const BwdArgs &A, int b, int l, long long q);
+
+// counting sort: the wave's lanes of one cell take consecutive arrival slots from ONE atomic per (wave, cell) --
+// consecutive queries share their coarse-level cells (a level-3 cell of config #3 holds 512), so per-key atomics
+// serialised on them -- and the lane-to-lane comparison runs over SGPR copies of the 64 cells, so the wave's atomics
+// go out together (a loop of one returning atomic per distinct cell waited ~64 round trips: 32 us for the key pass).
+// Each key keeps its slot (cell < 0: no key in the lane).
+__device__ __forceinline__ void keys_count(long long cell, int *__restrict__ cellcnt, int *__restrict__ slot) {
+    const int lane = threadIdx.x & 63;
+    int same = 0, rank = 0, leader = 64;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+        const long long cj = (long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(cell >> 32), j) << 32) |
+                                         (unsigned)__builtin_amdgcn_readlane((int)cell, j));
+        const bool eq = cj == cell;
+        same += eq ? 1 : 0;
+        rank += eq && j < lane ? 1 : 0;
+        leader = eq && leader == 64 ? j : leader;
+    }
+    int base = 0;
+    if (cell >= 0 && leader == lane) base = atomicAdd(cellcnt + cell, same);
+    base = __shfl(base, leader & 63);
+    if (cell >= 0) *slot = base + rank;
+}
+
 // ---------------------------------------------------------------------------------
 // 3. queries of (b, l) keyed by window-origin cell: o' = origin + nw - 1 per axis, in
 // [0, S_l + nw - 2] exactly when the window meets the level; others sort last.
 // ---------------------------------------------------------------------------------
 template <int R>
-__global__ __launch_bounds__(256) void k_bw_keys(BwdArgs A, int b, unsigned long long *__restrict__ keys) {
+__global__ __launch_bounds__(256) void k_bw_keys(BwdArgs A, int b, unsigned long long *__restrict__ keys,
+                                                 int *__restrict__ cellcnt, int *__restrict__ arrival) {
     const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
     const int l = (int)blockIdx.y;
+    if (cellcnt) {   // (counting sort: every lane takes part in the wave's per-cell aggregation)
+        long long cell = -1;
+        if (q < A.Nq) cell = bw_key_cell<R>(A, b, l, q);
+        keys_count(cell, cellcnt, arrival + (long long)l * A.Nq + q);
+        if (q < A.Nq) keys[(long long)l * A.Nq + q] = ((unsigned long long)cell << 32) | (unsigned long long)(unsigned)q;
+        return;
+    }
     if (q >= A.Nq) return;
+    const long long cell = bw_key_cell<R>(A, b, l, q);
+    keys[(long long)l * A.Nq + q] = ((unsigned long long)cell << 32) | (unsigned long long)(unsigned)q;
+}
+
+template <int R>
+__device__ __forceinline__ long long bw_key_cell(const BwdArgs &A, int b, int l, long long q) {
     float cy, cx, cz;
     load_coords(A.coords, b, A.Nq, q, cy, cx, cz);
     WinAxes ax;
@@ -1093,8 +1134,60 @@ __global__ __launch_bounds__(256) void k_bw_keys(BwdArgs A, int b, unsigned long
     const long long ncell = (long long)CY * CX * CZ;
     const bool in = !A.zero[l] && !ax.dead && (unsigned)oy < (unsigned)CY && (unsigned)ox < (unsigned)CX &&
                     (unsigned)oz < (unsigned)CZ;
-    const long long cell = A.coff[l] + (in ? ((long long)oy * CX + ox) * CZ + oz : ncell);
-    keys[(long long)l * A.Nq + q] = ((unsigned long long)cell << 32) | (unsigned long long)(unsigned)q;
+    return A.coff[l] + (in ? ((long long)oy * CX + ox) * CZ + oz : ncell);
+}
+
+// Counting sort of the keys by cell (round 5, replacing the radix sort + k_cell_starts, ~62 us at config #3): the
+// cells' key counts and each key's arrival slot in its cell (k_bw_keys, keys_count) are scanned into starts;
+// k_cell_scatter drops each key at start + slot (and clears the counts for the next batch element); k_cell_rank
+// then puts every key at start + (number of keys of its cell below it), i.e. ascending (cell, query) order: the
+// radix sort's output bit for bit (keys are unique), whatever the arrival order was.  The ranking compares a key
+// with its whole cell, staged in LDS for the 256 positions of a workgroup (cells of up to ~4 K keys; a larger cell
+// -- a pathological flow -- is read from memory, n^2 / 2 comparisons).
+__global__ __launch_bounds__(256) void k_cell_scatter(const unsigned long long *__restrict__ keys,
+                                                      const int *__restrict__ slot, long long n,
+                                                      const int *__restrict__ starts, int *__restrict__ cellcnt,
+                                                      unsigned long long *__restrict__ out) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long key = keys[i];
+    const long long c = (long long)(key >> 32);
+    out[starts[c] + slot[i]] = key;
+    cellcnt[c] = 0;
+}
+
+constexpr int kRankLds = 4096;   // keys staged per k_cell_rank workgroup
+__global__ __launch_bounds__(256) void k_cell_rank(const unsigned long long *__restrict__ in, long long n,
+                                                   const int *__restrict__ starts, unsigned long long *__restrict__ out) {
+    __shared__ unsigned long long win[kRankLds];
+    const long long p0 = (long long)blockIdx.x * 256, p = p0 + threadIdx.x;
+    // the cells of positions p0 .. p0 + 255 span [s0, e1)
+    const int s0 = starts[in[p0] >> 32], e1 = starts[(in[min(p0 + 255, n - 1)] >> 32) + 1];
+    const bool staged = e1 - s0 <= kRankLds;
+    if (staged)
+        for (int j = s0 + (int)threadIdx.x; j < e1; j += 256) win[j - s0] = in[j];
+    __syncthreads();
+    if (p >= n) return;
+    const unsigned long long key = in[p];
+    const long long c = (long long)(key >> 32);
+    const int s = starts[c], e = starts[c + 1];
+    int r = 0;
+    if (staged) {   // (16 independent LDS reads per step: a chain of single reads waited ~100 cycles per key)
+        const unsigned long long *wb = win + (s - s0);
+        const int len = e - s;
+        int j = 0;
+        for (; j + 16 <= len; j += 16) {
+            unsigned long long v[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = wb[j + k];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) r += v[k] < key ? 1 : 0;
+        }
+        for (; j < len; ++j) r += wb[j] < key ? 1 : 0;
+    } else {
+        for (int j = s; j < e; ++j) r += in[j] < key ? 1 : 0;
+    }
+    out[s + r] = key;
 }
 
 // starts[c] = first sorted index whose cell >= c, for c in [0, ncell]: one thread per cell, a binary
@@ -1561,6 +1654,191 @@ __global__ __launch_bounds__(256, SPLIT ? 3 : 4) void k_grad_t_mfma(const bf16_t
         }
 }
 
+// Round 5 (16-bit window gradients): DENSE batches.  k_grad_t_mfma forms its 16-query batches from 8-aligned sorted
+// positions inside one origin row, so a level-0 row of ~13 queries (config #3: 12 z-origins of ~1 query) fills two
+// batches -- ~290 batches per brick for ~108 of queries, and level 0 alone ran 195 us of the launch's 212.  Here the
+// brick's origin rows are concatenated (their sorted ranges, prefix-summed in LDS) and cut into batches of 16
+// consecutive queries of that concatenation, across rows; the batches are dealt round-robin to the brick's splits.
+// A batch's query tile is gathered from the packed query rows (thread (query j, channel octet r) loads 16 bytes) and
+// stored transposed into the [128 ch][16 q] tile the MFMA B operand reads, so k_qt_tiles is not needed either.  The
+// rest -- window-gradient staging, MFMAs, epilogue, split partials -- is k_grad_t_mfma<.., G16>'s.
+constexpr int kDenseRows = 320;   // origin rows per brick: (4 + 2r + 1)^2 <= 289 for r <= 6
+template <int NCT, bool F16>
+__global__ __launch_bounds__(256, 4) void k_grad_t_dense(const bf16_t *__restrict__ Qp,
+                                                         const unsigned long long *__restrict__ keys,
+                                                         const int *__restrict__ starts, float *__restrict__ dT,
+                                                         float *__restrict__ dTp, BwdArgs A, int b) {
+    const GtBlock gb = gt_block(A);
+    const int l = gb.l, nsplit = gb.nsplit, split = gb.split, brick = gb.brick;
+    starts += A.coff[l];
+    __shared__ __attribute__((aligned(16))) bf16_t Ql[2][2048];   // [buf] query tile [128 ch][16] (swizzled)
+    __shared__ __attribute__((aligned(16))) unsigned Gq[2][64][8];  // [buf][target][16 queries] 16-bit
+    __shared__ int rpre[kDenseRows + 1], rs0[kDenseRows];          // concatenation offset / first sorted position
+    __shared__ int tq[kTCap][16], tzr[kTCap][16], trw[kTCap][16];   // entry (batch e, query j): query, z, row
+    const int tid = threadIdx.x, lane = tid & 63, m = lane & 31, h = lane >> 5;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
+    const int nh = A.nwh[l], nu = A.nwu[l], nv = A.nwv[l];
+    const int rz = gw_rz(nv);
+    const long long nw3 = (long long)nh * nu * (rz >> 1);   // dwords per query
+    const int nbz = (Dl + 3) >> 2, nbx = (Wl + 3) >> 2, nby = (Hl + 3) >> 2;
+    int t = brick;
+    const int bz = t % nbz; t /= nbz;
+    const int bx = t % nbx;
+    const int by = t / nbx;
+    // staging role: query j of the batch; G: brick row r = (ty, tx), targets z = 4 bz .. 4 bz + 3; Q: channels 8 r ..
+    const int sj = tid & 15, sr = tid >> 4;
+    const int ty = by * 4 + (sr >> 2), tx = bx * 4 + (sr & 3);
+    const int tz0 = bz * 4;
+    const bool rval = ty < Hl && tx < Wl;
+    const int CX = Wl + nu - 1, CZ = Dl + nv - 1;
+    const int oy0 = by * 4, oy1 = min(by * 4 + 3, Hl - 1) + nh - 1;
+    const int ox0 = bx * 4, ox1 = min(bx * 4 + 3, Wl - 1) + nu - 1;
+    const int oz0 = bz * 4, oz1 = min(bz * 4 + 3, Dl - 1) + nv - 1;
+    const int nox = ox1 - ox0 + 1, nrows = (oy1 - oy0 + 1) * nox;
+    const unsigned short *g16 =
+        reinterpret_cast<const unsigned short *>(A.gwin + A.goff[l] + (long long)b * A.Nq * nw3);
+    const unsigned *gzero = reinterpret_cast<const unsigned *>(A.gwin) - 64;   // the zeroed guard
+    const bool qch = A.cbase + 8 * sr < A.Cp;   // this thread's channel octet exists
+    const bf16_t *qrow = Qp + (long long)b * A.Nq * A.Cp + A.cbase + 8 * sr;
+    // the rows' sorted ranges and their prefix (wave 0, 64 rows at a time)
+    if (w == 0) {
+        int run = 0;
+        for (int g0 = 0; g0 < nrows; g0 += 64) {
+            const int row = g0 + lane;
+            int cnt = 0;
+            if (row < nrows) {
+                const long long cb = ((long long)(oy0 + row / nox) * CX + (ox0 + row % nox)) * CZ;
+                const int s0 = starts[cb + oz0];
+                cnt = starts[cb + oz1 + 1] - s0;
+                rs0[row] = s0;
+            }
+            int inc = cnt;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int v = __shfl_up(inc, d);
+                if (lane >= d) inc += v;
+            }
+            if (row < nrows) rpre[row] = run + inc - cnt;
+            run += __builtin_amdgcn_readlane(inc, 63);
+        }
+        if (lane == 0) rpre[nrows] = run;
+    }
+    __syncthreads();
+    const int total = rpre[nrows];
+    const int nb = (total + 15) >> 4;                          // batches of the brick
+    const int nbs = nb > split ? (nb - split + nsplit - 1) / nsplit : 0;   // this split's: split, split + nsplit, ..
+    f32x16 acc[2];
+#pragma unroll
+    for (int T = 0; T < 2; ++T)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[T][i] = 0.0f;
+    struct Set {
+        u32x4 q, g;   // this thread's 8 channels of query j; its 4 targets' 16-bit values in g[0..1]
+        unsigned mk;  // bit k: target z tz0 + k inside the query's window row and the level
+    };
+    auto load = [&](int i, int n, Set &S) __attribute__((always_inline)) {   // batch min(i, n - 1), unconditional
+        const int e = min(i, n - 1);
+        const int qq = tq[e][sj], row = trw[e][sj];
+        const int oy = oy0 + row / nox, ox = ox0 + row % nox;
+        const int py = ty - oy + nh - 1, px = tx - ox + nu - 1;
+        const bool yxok = rval && (unsigned)py < (unsigned)nh && (unsigned)px < (unsigned)nu;
+        const int pz0 = tz0 - tzr[e][sj] + nv - 1;
+        const bool ok = qq >= 0 && yxok && pz0 > -4 && pz0 < nv;
+        const unsigned short *src16 = ok ? g16 + 2 * (long long)qq * nw3 + (py * nu + px) * rz + pz0 + (pz0 & 1)
+                                         : reinterpret_cast<const unsigned short *>(gzero);
+        __builtin_memcpy(&S.g, src16, 8);
+        const bf16_t *qs = qq >= 0 && qch ? qrow + (long long)qq * A.Cp : reinterpret_cast<const bf16_t *>(gzero);
+        __builtin_memcpy(&S.q, qs, 16);
+        unsigned mk = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) mk |= ((unsigned)(pz0 + k) < (unsigned)nv && tz0 + k < Dl) ? 1u << k : 0u;
+        S.mk = mk;
+    };
+    auto store = [&](int bb, const Set &S) __attribute__((always_inline)) {
+        // query tile: channel c = 8 sr + k, query sj at byte c * 32 + 16 ((sj / 8) ^ (c / 8 & 1)) + 2 (sj % 8)
+        unsigned short *qd = reinterpret_cast<unsigned short *>(Ql[bb]) + (8 * sr) * 16 + 8 * ((sj >> 3) ^ (sr & 1)) +
+                             (sj & 7);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) qd[16 * k] = (unsigned short)(S.q[k >> 1] >> (16 * (k & 1)));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {   // target 4 sr + k, query sj: 8-query chunk (sj / 8) ^ (row >> 3 & 1)
+            const int tr = 4 * sr + k;
+            const unsigned short v = (S.mk >> k) & 1u ? (unsigned short)(S.g[k >> 1] >> (16 * (k & 1))) : 0;
+            reinterpret_cast<unsigned short *>(Gq[bb][tr])[8 * ((sj >> 3) ^ ((tr >> 3) & 1)) + (sj & 7)] = v;
+        }
+    };
+    auto compute = [&](int bb) __attribute__((always_inline)) {
+        if (w >= NCT) return;
+        const int r = 32 * w + m, rsw = (r >> 3) & 1;
+        const bf16x8 bq = *reinterpret_cast<const bf16x8 *>(reinterpret_cast<const unsigned char *>(Ql[bb]) +
+                                                             r * 32 + 16 * (h ^ rsw));
+#pragma unroll
+        for (int T = 0; T < 2; ++T) {
+            const int tr = 32 * T + m;
+            const bf16x8 ag = *reinterpret_cast<const bf16x8 *>(&Gq[bb][tr][4 * (h ^ ((tr >> 3) & 1))]);
+            acc[T] = mma32<F16>(ag, bq, acc[T]);
+        }
+    };
+    for (int g0 = 0; g0 < nbs; g0 += kTCap) {
+        const int n = min(kTCap, nbs - g0);
+        __syncthreads();   // the previous group's table and tiles have been read
+        for (int e = tid >> 4; e < kTCap; e += 16) {   // entry (batch e of the group, query sj)
+            const int v = 16 * (split + (g0 + e) * nsplit) + sj;   // index into the concatenated rows
+            int qq = -1, zr = 0, row = 0;
+            if (e < n && v < total) {
+                int lo = 0, hi = nrows - 1;   // the row holding v: last row with rpre[row] <= v
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (rpre[mid] <= v) lo = mid;
+                    else hi = mid - 1;
+                }
+                row = lo;
+                const unsigned long long key = keys[rs0[row] + (v - rpre[row])];
+                const long long cb = ((long long)(oy0 + row / nox) * CX + (ox0 + row % nox)) * CZ + A.coff[l];
+                qq = (int)(unsigned)(key & 0xffffffffu);
+                zr = (int)((long long)(key >> 32) - cb);   // origin z - oz0 (global cells hold coff[l])
+            }
+            tq[e][sj] = qq;
+            tzr[e][sj] = zr;
+            trw[e][sj] = row;
+        }
+        __syncthreads();
+        Set S0, S1, S2;
+        load(0, n, S0);
+        load(1, n, S1);
+        load(2, n, S2);
+        auto step = [&](int i, Set &S) __attribute__((always_inline)) {
+            store(i & 1, S);
+            __syncthreads();   // batch i staged; every wave is done with batch i - 2 (same buffer)
+            load(i + 3, n, S);
+            if (i < n) compute(i & 1);
+        };
+        for (int i = 0; i < n; i += 3) {
+            step(i, S0);
+            step(i + 1, S1);
+            step(i + 2, S2);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the tail's clamped loads)
+    }
+    if (w >= NCT) return;
+    const float sc = A.scale;
+    const int ch = A.cbase + 32 * w + m;
+#pragma unroll
+    for (int T = 0; T < 2; ++T)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int ti = 32 * T + 8 * (i >> 2) + 4 * h + (i & 3);
+            const int y = by * 4 + (ti >> 4), x = bx * 4 + ((ti >> 2) & 3), z = bz * 4 + (ti & 3);
+            if (nsplit > 1) {
+                dTp[A.gt_poff[l] + (((long long)split * nbz * nbx * nby + brick) * 64 + ti) * A.Cp + ch] = acc[T][i];
+            } else if (y < Hl && x < Wl && z < Dl) {
+                dT[((long long)b * A.row_stride + A.off[l] + ((long long)y * Wl + x) * Dpl + z) * A.Cp + ch] =
+                    acc[T][i] * sc;
+            }
+        }
+}
+
 // dT rows of level l <- scale * sum over the nsplit partials (split order: deterministic).  One thread per
 // (brick target, channel pair).
 __global__ __launch_bounds__(256) void k_grad_t_reduce(const float *__restrict__ dTp, float *__restrict__ dT,
@@ -1691,6 +1969,7 @@ static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct BwdPlan {
     size_t gwin, dq, dt, keys, starts, temp, part, qt, ttr, total;
+    size_t cnt_off;   // the cell counts of the counting sort: bytes into the starts region
     long long coff[DVC_MAX_LEVELS + 1];   // first window-origin cell of each level in the merged key space
     int sp[DVC_MAX_LEVELS];               // k_grad_t splits per brick
     long long poff[DVC_MAX_LEVELS];       // split-partial offsets (floats)
@@ -1741,7 +2020,9 @@ static long long level_cells(const dvc_layout &lay, int l, const int nw[3]) {
     return (long long)(lay.H[l] + nw[0] - 1) * (lay.W[l] + nw[1] - 1) * (lay.D[l] + nw[2] - 1);
 }
 
-static void bwd_plan(int B, long long Nq, const dvc_layout &lay, int radius, bool legacy, BwdPlan &P) {
+// dtype < 0: the largest plan of the three dtypes (the dtype-less workspace query); a dtype's own plan has the same
+// offsets up to the MFMA tiles (qt, ttr: the last regions), which only fp32 doubles -- so it fits either allocation
+static void bwd_plan(int B, long long Nq, const dvc_layout &lay, int radius, bool legacy, BwdPlan &P, int dtype = -1) {
     size_t gw = 0;
     long long cells = 0;
     size_t part = 0;
@@ -1768,31 +2049,35 @@ static void bwd_plan(int B, long long Nq, const dvc_layout &lay, int radius, boo
     P.dq = al256((size_t)std::max(grad_q_parts(L), gq_sorted_slots(L)) * B * Nq * lay.c_pad * sizeof(float));
     P.dt = al256((size_t)B * lay.row_stride * lay.c_pad * sizeof(float));
     P.keys = al256((size_t)nkeys * sizeof(unsigned long long));
-    P.starts = al256((size_t)(cells + 1) * sizeof(int));
-    size_t tb = 0;
+    P.cnt_off = al256((size_t)(cells + 1) * sizeof(int));
+    P.starts = 2 * P.cnt_off + al256((size_t)nkeys * sizeof(int));   // starts, the per-cell key counts, key slots
+    size_t tb = 0, tsc = 0;
     (void)rocprim::radix_sort_keys(nullptr, tb, (unsigned long long *)nullptr, (unsigned long long *)nullptr,
                                    (size_t)nkeys, 0u, 64u, (hipStream_t)0);
-    P.temp = al256(tb);
+    (void)rocprim::exclusive_scan(nullptr, tsc, (int *)nullptr, (int *)nullptr, 0, (size_t)(cells + 1),
+                                  rocprim::plus<int>(), (hipStream_t)0);
+    P.temp = al256(std::max(tb, tsc));
     P.part = al256(std::max<size_t>(part, 256));
     P.ntq = (nkeys + 7) / 8 + 1;
     // the MFMA path's query / target tiles, sized always (the workspace query has no dtype): twice, for the fp32
     // blocks' hi and lo tiles
-    P.qt = al256(2 * (size_t)P.ntq * ((lay.c_pad + 127) / 128) * 4096);
+    const size_t split = dtype == DVC_BF16 || dtype == DVC_F16 ? 1 : 2;   // fp32: hi and lo tiles
+    P.qt = al256(split * (size_t)P.ntq * ((lay.c_pad + 127) / 128) * 4096);
     long long nt = 0;
     for (int l = 0; l < L; ++l) {
         P.tz0[l] = nt;
         nt += (long long)lay.H[l] * lay.W[l] * (lay.Dp[l] / 8);
     }
     P.tz0[L] = nt;
-    P.ttr = al256(2 * (size_t)B * ((lay.c_pad + 127) / 128) * nt * 4096);
+    P.ttr = al256(split * (size_t)B * ((lay.c_pad + 127) / 128) * nt * 4096);
     P.total = P.gwin + P.dq + P.dt + 2 * P.keys + P.starts + P.temp + P.part + P.qt + P.ttr;
 }
 
 // workspace for either convention (the legacy plan is larger only when a level has W != D)
-size_t backward_workspace_bytes(int B, long long Nq, const dvc_layout &lay, int radius) {
+size_t backward_workspace_bytes(int B, long long Nq, const dvc_layout &lay, int radius, int dtype) {
     BwdPlan P, Q;
-    bwd_plan(B, Nq, lay, radius, false, P);
-    bwd_plan(B, Nq, lay, radius, true, Q);
+    bwd_plan(B, Nq, lay, radius, false, P, dtype);
+    bwd_plan(B, Nq, lay, radius, true, Q, dtype);
     return std::max(P.total, Q.total);
 }
 
@@ -1837,6 +2122,12 @@ void set_backward_g64(int v) { g_bwd_g64 = v; }
 // pairs of round 4 (tuning "bwd_g16", for A/B and to keep the pair path tested on 16-bit blocks)
 static thread_local int g_bwd_g16 = 1;
 void set_backward_g16(int v) { g_bwd_g16 = v; }
+// 1 (default): k_grad_t_dense's batches across origin rows for 16-bit blocks; 0: k_grad_t_mfma's per-row batches
+static thread_local int g_bwd_dense = 1;
+void set_backward_dense(int v) { g_bwd_dense = v; }
+// 1 (default): the keys' counting sort (k_cell_scatter / k_cell_rank, round 5); 0: rocprim's radix sort + k_cell_starts
+static thread_local int g_bwd_sort = 1;
+void set_backward_sort(int v) { g_bwd_sort = v; }
 
 // dtype codes of the packed operands whose gradient sums run on the matrix cores (the rest: VALU)
 int backward_uses_mfma(int B, long long Nq, const dvc_layout &lay, int radius, int convention, int dtype) {
@@ -1852,6 +2143,7 @@ int backward_uses_mfma(int B, long long Nq, const dvc_layout &lay, int radius, i
 template <typename TT, int R>
 static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &lay, const BwdPlan &P,
                       unsigned char *ws, float *g1, float *g2, int C, hipStream_t s, char *err, size_t errlen) {
+    A.gwin = (float *)(ws + 256);
     float *dq = (float *)(ws + P.gwin);
     float *dt = (float *)(ws + P.gwin + P.dq);
     unsigned long long *kin = (unsigned long long *)(ws + P.gwin + P.dq + P.dt);
@@ -1861,7 +2153,6 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     float *dtp = (float *)(ws + P.gwin + P.dq + P.dt + 2 * P.keys + P.starts + P.temp);
     bf16_t *qt = (bf16_t *)(ws + P.gwin + P.dq + P.dt + 2 * P.keys + P.starts + P.temp + P.part);
     bf16_t *ttr = (bf16_t *)(ws + P.gwin + P.dq + P.dt + 2 * P.keys + P.starts + P.temp + P.part + P.qt);
-    A.gwin = (float *)(ws + 256);
     // the 256-byte guard before the window gradients is the zero source of the MFMA kernels' LDS-DMA gathers
     if (hipMemsetAsync(ws, 0, 256, s) != hipSuccess) {
         snprintf(err, errlen, "corr_backward: guard clear failed");
@@ -1975,6 +2266,10 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     // target gradients: per batch element, the queries of every level in window-origin order (one key
     // space, one sort), then one k_grad_t launch over every level's (brick, split) workgroups, coarse levels'
     // split partials reduced by one launch
+    // dense batches across origin rows (k_grad_t_dense) for 16-bit window gradients
+    bool dense = g16 && g_bwd_dense;
+    for (int l = 0; l < A.L; ++l)
+        dense = dense && (long long)(3 + A.nwh[l]) * (3 + A.nwu[l]) <= kDenseRows;
     int nblk = 0;
     long long nred = 0;
     for (int l = 0; l < A.L; ++l) {
@@ -1994,36 +2289,76 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     const long long nkeys = (long long)A.L * A.Nq;
     unsigned bits = 1;
     while ((1LL << bits) <= ncell) ++bits;
+    // counting sort (default) or the radix sort of rounds 3-4 (tuning "bwd_sort" 0): the same sorted keys
+    const bool counting = g_bwd_sort != 0;
+    int *cellcnt = reinterpret_cast<int *>(reinterpret_cast<unsigned char *>(starts) + P.cnt_off);
+    int *slot = reinterpret_cast<int *>(reinterpret_cast<unsigned char *>(starts) + 2 * P.cnt_off);   // per key
+    const unsigned long long *ks = counting ? kin : kout;   // the sorted keys
+    if (counting && hipMemsetAsync(cellcnt, 0, (size_t)(ncell + 2) * sizeof(int), s) != hipSuccess) {
+        snprintf(err, errlen, "corr_backward: cell count clear failed");
+        return DVC_ERR_RUNTIME;
+    }
     for (int b = 0; b < A.B; ++b) {
-        k_bw_keys<R><<<dim3((unsigned)((A.Nq + 255) / 256), (unsigned)A.L), 256, 0, s>>>(A, b, kin);
+        k_bw_keys<R><<<dim3((unsigned)((A.Nq + 255) / 256), (unsigned)A.L), 256, 0, s>>>(
+            A, b, kin, counting ? cellcnt : nullptr, slot);
         if (!launched("keys")) return DVC_ERR_LAUNCH;
         size_t tb = P.temp;
-        // (the cell bits only: the keys enter in (level, query) order and the sort is stable, so within a cell the
-        // queries stay in ascending order -- the order of the full keys -- in 2-3 digit passes instead of 6-7)
-        if (rocprim::radix_sort_keys(temp, tb, kin, kout, (size_t)nkeys, 32u, 32u + bits, s) != hipSuccess) {
-            snprintf(err, errlen, "corr_backward: radix sort failed");
-            return DVC_ERR_RUNTIME;
+        if (counting) {
+            // starts[c] = keys of cells < c, for c in [0, ncell + 1]
+            if (rocprim::exclusive_scan(temp, tb, cellcnt, starts, 0, (size_t)(ncell + 2), rocprim::plus<int>(), s) !=
+                hipSuccess) {
+                snprintf(err, errlen, "corr_backward: cell scan failed");
+                return DVC_ERR_RUNTIME;
+            }
+            const unsigned kb = (unsigned)((nkeys + 255) / 256);
+            k_cell_scatter<<<kb, 256, 0, s>>>(kin, slot, nkeys, starts, cellcnt, kout);
+            k_cell_rank<<<kb, 256, 0, s>>>(kout, nkeys, starts, kin);
+            if (!launched("cell_sort")) return DVC_ERR_LAUNCH;
+        } else {
+            // (the cell bits only: the keys enter in (level, query) order and the sort is stable, so within a cell
+            // the queries stay in ascending order -- the order of the full keys -- in 2-3 digit passes, not 6-7)
+            if (rocprim::radix_sort_keys(temp, tb, kin, kout, (size_t)nkeys, 32u, 32u + bits, s) != hipSuccess) {
+                snprintf(err, errlen, "corr_backward: radix sort failed");
+                return DVC_ERR_RUNTIME;
+            }
+            k_cell_starts<<<(unsigned)((ncell + 1 + 255) / 256), 256, 0, s>>>(kout, nkeys, ncell, starts);
+            if (!launched("cell_starts")) return DVC_ERR_LAUNCH;
         }
-        k_cell_starts<<<(unsigned)((ncell + 1 + 255) / 256), 256, 0, s>>>(kout, nkeys, ncell, starts);
-        if (!launched("cell_starts")) return DVC_ERR_LAUNCH;
         if (qsorted) {   // level l's keys are the l-th Nq sorted ones (its cells come after level l - 1's); the
                          // coarser levels' boxes of this batch element in the same launch
             const int ns = (int)((A.Nq + 63) / 64);
             launch_q(dim3((unsigned)std::max<long long>(ns, A.L > nsl ? boxes / A.B : 0),
-                          (unsigned)(nsl + (A.L > nsl ? 1 : 0))), kout, b, ns, nsl, nsl);
+                          (unsigned)(nsl + (A.L > nsl ? 1 : 0))), ks, b, ns, nsl, nsl);
             if (!launched("grad_q_sorted")) return DVC_ERR_LAUNCH;
         }
         if (nblk == 0) continue;
         bool done_t = false;
         if constexpr (k16) {
             if (mfma) {
-                // matrix-core path: sorted + transposed query rows, then 16-query MFMA batches
+                // matrix-core path: sorted + transposed query rows, then 16-query MFMA batches (dense: the query
+                // rows gathered per batch instead)
+                if (dense) {
+                    for (int cg = 0; cg < ngroups; ++cg) {
+                        BwdArgs Ag = A;
+                        Ag.cbase = 128 * cg;
+                        const bf16_t *Qb = reinterpret_cast<const bf16_t *>(Q);
+                        switch (std::min(128, A.Cp - Ag.cbase) / 32) {
+                        case 1: k_grad_t_dense<1, F16><<<nblk, 256, 0, s>>>(Qb, ks, starts, dt, dtp, Ag, b); break;
+                        case 2: k_grad_t_dense<2, F16><<<nblk, 256, 0, s>>>(Qb, ks, starts, dt, dtp, Ag, b); break;
+                        case 3: k_grad_t_dense<3, F16><<<nblk, 256, 0, s>>>(Qb, ks, starts, dt, dtp, Ag, b); break;
+                        default: k_grad_t_dense<4, F16><<<nblk, 256, 0, s>>>(Qb, ks, starts, dt, dtp, Ag, b); break;
+                        }
+                    }
+                    done_t = true;
+                }
+            }
+            if (mfma && !done_t) {
                 if constexpr (SPLIT)
                     k_qt_tiles<float><<<dim3((unsigned)((P.ntq + kQtPer - 1) / kQtPer), (unsigned)ngroups), 256, 0, s>>>(
-                        Q, kout, qt, A.Nq, nkeys, A.Cp, b, qz_lo, P.ntq);
+                        Q, ks, qt, A.Nq, nkeys, A.Cp, b, qz_lo, P.ntq);
                 else
                     k_qt_tiles<bf16_t><<<dim3((unsigned)((P.ntq + kQtPer - 1) / kQtPer), (unsigned)ngroups), 256, 0, s>>>(
-                        reinterpret_cast<const bf16_t *>(Q), kout, qt, A.Nq, nkeys, A.Cp, b, 0, P.ntq);
+                        reinterpret_cast<const bf16_t *>(Q), ks, qt, A.Nq, nkeys, A.Cp, b, 0, P.ntq);
                 if (!launched("qt_tiles")) return DVC_ERR_LAUNCH;
                 for (int cg = 0; cg < ngroups; ++cg) {
                     BwdArgs Ag = A;
@@ -2031,10 +2366,10 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
                     auto go = [&](auto g16c) {
                         constexpr bool GG = decltype(g16c)::value && !SPLIT;
                         switch (std::min(128, A.Cp - Ag.cbase) / 32) {
-                        case 1: k_grad_t_mfma<1, F16, SPLIT, GG><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b, qz_lo); break;
-                        case 2: k_grad_t_mfma<2, F16, SPLIT, GG><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b, qz_lo); break;
-                        case 3: k_grad_t_mfma<3, F16, SPLIT, GG><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b, qz_lo); break;
-                        default: k_grad_t_mfma<4, F16, SPLIT, GG><<<nblk, 256, 0, s>>>(qt, P.ntq, kout, starts, dt, dtp, Ag, b, qz_lo); break;
+                        case 1: k_grad_t_mfma<1, F16, SPLIT, GG><<<nblk, 256, 0, s>>>(qt, P.ntq, ks, starts, dt, dtp, Ag, b, qz_lo); break;
+                        case 2: k_grad_t_mfma<2, F16, SPLIT, GG><<<nblk, 256, 0, s>>>(qt, P.ntq, ks, starts, dt, dtp, Ag, b, qz_lo); break;
+                        case 3: k_grad_t_mfma<3, F16, SPLIT, GG><<<nblk, 256, 0, s>>>(qt, P.ntq, ks, starts, dt, dtp, Ag, b, qz_lo); break;
+                        default: k_grad_t_mfma<4, F16, SPLIT, GG><<<nblk, 256, 0, s>>>(qt, P.ntq, ks, starts, dt, dtp, Ag, b, qz_lo); break;
                         }
                     };
                     if (g16) go(std::true_type{});
@@ -2047,7 +2382,7 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
             for (int cg = 0; cg < ngroups; ++cg) {
                 BwdArgs Ag = A;
                 Ag.cbase = 128 * cg;
-                k_grad_t<TT, R><<<nblk, 256, 0, s>>>(Q, kout, starts, dt, dtp, Ag, b);
+                k_grad_t<TT, R><<<nblk, 256, 0, s>>>(Q, ks, starts, dt, dtp, Ag, b);
             }
         }
         if (!launched("grad_t")) return DVC_ERR_LAUNCH;
@@ -2099,7 +2434,7 @@ int corr_backward(const void *packed_q, const void *packed_t, const float *coord
     }
     const bool legacy = convention == DVC_LEGACY;
     BwdPlan P;
-    bwd_plan(B, Nq, lay, radius, legacy, P);
+    bwd_plan(B, Nq, lay, radius, legacy, P, dtype);
     // merged key space: every level's cells (+ one outside cell each) in 31 bits, and the sorted positions of
     // all levels' queries (int cell starts) below 2^31
     if (P.coff[lay.num_levels] >= (1LL << 31) - 1 || (long long)lay.num_levels * Nq >= (1LL << 31) - 1) {

@@ -59,12 +59,14 @@ int corr_backward(const void *packed_q, const void *packed_t, const float *coord
                   float *grad_fmap1, float *grad_fmap2, void *workspace, int B, long long Nq, int C,
                   const dvc_layout &lay, int radius, int convention, int dtype, hipStream_t s, char *err,
                   size_t errlen);
-size_t backward_workspace_bytes(int B, long long Nq, const dvc_layout &lay, int radius);
+size_t backward_workspace_bytes(int B, long long Nq, const dvc_layout &lay, int radius, int dtype);
 int backward_uses_mfma(int B, long long Nq, const dvc_layout &lay, int radius, int convention, int dtype);
 void set_backward_mfma(int v);
 bool win_grad_needs_g64(long long Nq, int radius);
 void set_backward_g64(int v);
 void set_backward_g16(int v);
+void set_backward_sort(int v);
+void set_backward_dense(int v);
 __global__ void k_coords_grid(float *, long long, int, int, int);
 template <bool DELTA, bool SUBGRID, int VEC, bool STAGED>
 __global__ void k_upflow(const float *, const float *, float *, float *, long long, int, int, int, int, int, int, int,
@@ -365,6 +367,16 @@ int dvc_set_tuning(const char *key, int value) {
     if (!strcmp(key, "bwd_g16")) {   // 1 = single 16-bit window gradients for bf16 / fp16 blocks, 0 = hi/lo pairs
         if (value < 0 || value > 1) return fail(DVC_ERR_INVALID, "set_tuning: bwd_g16 %d", value);
         set_backward_g16(value);
+        return DVC_OK;
+    }
+    if (!strcmp(key, "bwd_dense")) {   // 1 = dense 16-query batches across origin rows (16-bit blocks), 0 = per-row batches
+        if (value < 0 || value > 1) return fail(DVC_ERR_INVALID, "set_tuning: bwd_dense %d", value);
+        set_backward_dense(value);
+        return DVC_OK;
+    }
+    if (!strcmp(key, "bwd_sort")) {   // 1 = counting sort of the target-gradient keys (default), 0 = rocprim radix sort
+        if (value < 0 || value > 1) return fail(DVC_ERR_INVALID, "set_tuning: bwd_sort %d", value);
+        set_backward_sort(value);
         return DVC_OK;
     }
     if (!strcmp(key, "bwd_gout64")) {   // 1 = the window-gradient pass's 64-bit-addressed instance at every size
@@ -881,7 +893,16 @@ size_t dvc_corr_backward_workspace_bytes(int B, int64_t Nq, int C, int H, int W,
     dvc_layout lay;
     if (dvc_layout_init(H, W, D, num_levels, C, &lay)) return 0;
     if (B < 1 || Nq < 1 || radius < 1 || radius > 6) return 0;
-    return backward_workspace_bytes(B, Nq, lay, radius);
+    return backward_workspace_bytes(B, Nq, lay, radius, -1);
+}
+
+size_t dvc_corr_backward_workspace_bytes_dtype(int B, int64_t Nq, int C, int H, int W, int D, int num_levels,
+                                               int radius, int dtype) {
+    dvc_layout lay;
+    if (dvc_layout_init(H, W, D, num_levels, C, &lay)) return 0;
+    if (B < 1 || Nq < 1 || radius < 1 || radius > 6) return 0;
+    if (dtype != DVC_BF16 && dtype != DVC_F32 && dtype != DVC_F16) return 0;
+    return backward_workspace_bytes(B, Nq, lay, radius, dtype);
 }
 
 int dvc_corr_backward(const void *packed_q, const void *packed_t, const float *coords, const float *grad_out,

@@ -25,7 +25,8 @@ EXPORTED = (
     "dvc_layout_init", "dvc_pack_workspace_bytes", "dvc_pack_queries", "dvc_pack_targets", "dvc_corr_build",
     "dvc_corr_pool", "dvc_corr_lookup", "dvc_lookup_fused_workspace_bytes", "dvc_corr_lookup_fused",
     "dvc_sample3d", "dvc_set_tuning", "dvc_last_error", "dvc_version", "dvc_abi_version",
-    "dvc_corr_backward_workspace_bytes", "dvc_corr_backward", "dvc_proj_packed_bytes", "dvc_proj_pack", "dvc_proj_pack_exact",
+    "dvc_corr_backward_workspace_bytes", "dvc_corr_backward_workspace_bytes_dtype", "dvc_corr_backward",
+    "dvc_proj_packed_bytes", "dvc_proj_pack", "dvc_proj_pack_exact",
     "dvc_corr_lookup_proj", "dvc_lookup_fused_proj_workspace_bytes", "dvc_corr_lookup_fused_proj",
     "dvc_coords_grid", "dvc_upflow", "dvc_flow_step", "dvc_bricked_levels", "dvc_corr_backward_mfma", "dvc_corr_backward_gout64",
 )
@@ -83,6 +84,7 @@ def lib() -> ctypes.CDLL:
         "dvc_corr_lookup_fused": (i32, [vp, vp, vp, vp, vp, i32, i64, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
         "dvc_sample3d": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i64, i32, vp]),
         "dvc_corr_backward_workspace_bytes": (sz, [i32, i64, i32, i32, i32, i32, i32, i32]),
+        "dvc_corr_backward_workspace_bytes_dtype": (sz, [i32, i64, i32, i32, i32, i32, i32, i32, i32]),
         "dvc_corr_backward": (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i64, i32, i32, i32, i32, i32, i32, i32, i32,
                                     vp]),
         "dvc_corr_backward_mfma": (i32, [i32, i64, i32, i32, i32, i32, i32, i32, i32, i32]),

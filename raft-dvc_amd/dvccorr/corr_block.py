@@ -191,7 +191,14 @@ def _check_fmaps(fmap1: torch.Tensor, fmap2: torch.Tensor) -> None:
 
 
 class CorrBlock(_Block):
-    """All-pairs 3-D correlation pyramid + radius-r trilinear lookup (materialised)."""
+    """All-pairs 3-D correlation pyramid + radius-r trilinear lookup (materialised).
+
+    Gradient precision (dvc_corr_backward, include/dvccorr.h): bf16 / fp16 blocks sum the gradients on the matrix
+    cores from 16-bit window gradients (the one fp16 rounding of d(corr) the reference's AMP backward applies,
+    trainer.py:249-257).  fp32 blocks run the same kernels on bf16 hi/lo splits of every operand, ~2^-16 relative
+    per product -- not the exact fp32 sums of the reference's autograd: the golden gradients agree to <= 1e-5
+    (tests/test_gpu_backward.py, GRAD_TOL).  dvccorr._lib.set_tuning("bwd_mfma", 0) selects the exact fp32 VALU kernels
+    (per calling thread)."""
 
     def __init__(self, fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int = 4, radius: int = 4,
                  legacy_wd_swap: bool = False, *, precision: Optional[str] = None, build: str = "gemm",

@@ -274,7 +274,7 @@ def corr_backward(packed_q: torch.Tensor, packed_t: torch.Tensor, coords: torch.
     dev = packed_q.device
     d1 = torch.empty((B, C, Nq), dtype=torch.float32, device=dev)
     d2 = torch.empty((B, C, H, W, D), dtype=torch.float32, device=dev)
-    nws = lib().dvc_corr_backward_workspace_bytes(B, Nq, C, H, W, D, num_levels, radius)
+    nws = lib().dvc_corr_backward_workspace_bytes_dtype(B, Nq, C, H, W, D, num_levels, radius, dtype)
     ws = torch.empty((max(nws, 256),), dtype=torch.uint8, device=dev)
     check(lib().dvc_corr_backward(_ptr(packed_q), _ptr(packed_t), _ptr(c), _ptr(g), _ptr(d1), _ptr(d2), _ptr(ws), B,
                                   Nq, C, H, W, D, num_levels, radius, DVC_LEGACY if legacy else DVC_FIXED, dtype,

@@ -137,6 +137,15 @@ def test_backward_validation_without_gpu():
     # rows; twice again for the fp32 blocks' hi and lo tiles, round 4) -- ~265 MB above the window gradients at #3
     nws = L.dvc_corr_backward_workspace_bytes(1, 32768, 128, 32, 32, 32, 4, 4)
     assert nws >= 4 * 32768 * 1000 * 4 and nws < 4 * 32768 * 1000 * 4 + 300 * 2 ** 20
+    # the dtype's own workspace: fp32 = the dtype-less query (hi + lo tiles); bf16 / fp16 without the lo
+    # tiles: ntq = L*Nq/8 + 1 query tiles and B * H*W*(D/8) target tiles per level of 4 KB each, ~88 MB at #3
+    f32 = L.dvc_corr_backward_workspace_bytes_dtype(1, 32768, 128, 32, 32, 32, 4, 4, _lib.DVC_F32)
+    assert f32 == nws
+    tiles = (4 * 32768 // 8 + 1 + sum((32 >> l) ** 2 * max(1, (32 >> l) // 8) for l in range(4))) * 4096
+    for dt in (_lib.DVC_BF16, _lib.DVC_F16):
+        low = L.dvc_corr_backward_workspace_bytes_dtype(1, 32768, 128, 32, 32, 32, 4, 4, dt)
+        assert 0 <= nws - low - tiles < 4096, (nws - low, tiles)
+    assert L.dvc_corr_backward_workspace_bytes_dtype(1, 32768, 128, 32, 32, 32, 4, 4, 7) == 0
 
 
 def test_backward_path_selection_without_gpu():

@@ -330,3 +330,37 @@ def test_grad_stale_workspace(precision):
         outs.append((d1.clone(), d2.clone()))
     for d1, d2 in outs[1:]:
         assert torch.equal(d1, outs[0][0]) and torch.equal(d2, outs[0][1]), precision
+
+
+@pytest.mark.parametrize("shape,C,L,r,legacy,scale,B", [
+    ((16, 16, 16), 64, 4, 4, False, 3.0, 1),    # config #2's pyramid: coarse cells of 8 / 64 / 512 queries
+    ((8, 8, 8), 32, 4, 3, False, 2.0, 1),       # a one-voxel level: all its keys in the outside cell
+    ((12, 10, 16), 32, 3, 4, False, 3.0, 2),    # ragged, two batch elements
+    ((8, 12, 16), 32, 2, 2, True, 2.0, 1),      # legacy W != D: stretched windows (generic levels)
+    ((24, 24, 24), 32, 2, 2, False, 60.0, 1),   # flows far off the volume: outside cells of > 4 K keys (unstaged)
+])
+def test_grad_counting_sort_matches_radix(shape, C, L, r, legacy, scale, B):
+    """The target-gradient pass's counting sort (k_bw_keys' per-(wave, cell) slots, k_cell_scatter, k_cell_rank;
+    round 5) against rocprim's stable radix sort + k_cell_starts (tuning "bwd_sort" 0): both gradients bit for bit,
+    for every dtype, over the cell populations a sort meets -- near-empty level-0 cells, 512-query coarse cells,
+    one-voxel levels, legacy stretched windows, a second batch element and outside cells holding most queries."""
+    from dvccorr import _lib, ops
+    H, W, D = shape
+    seed = 8100 + H + 3 * L
+    f1 = torch.from_numpy(prng.normal(seed, (B, C, H, W, D))).to(DEV)
+    f2 = torch.from_numpy(prng.normal(seed + 1, (B, C, H, W, D))).to(DEV)
+    coords = torch.from_numpy(prng.flow_coords(seed + 2, B, H, W, D, scale)).to(DEV).reshape(B, 3, -1)
+    G = torch.from_numpy(prng.normal(seed + 3, (B, L * (2 * r + 1) ** 3, H * W * D))).to(DEV)
+    for precision in ("bf16", "fp16", "fp32"):
+        dt = ops.dtype_code(precision)
+        q = ops.pack_queries(f1.reshape(B, C, -1), dt)
+        t = ops.pack_targets(f2, L, dt)
+        got = ops.corr_backward(q, t, coords, G, C, H, W, D, L, r, legacy, dt)
+        _lib.set_tuning("bwd_sort", 0)
+        try:
+            ref = ops.corr_backward(q, t, coords, G, C, H, W, D, L, r, legacy, dt)
+            torch.cuda.synchronize()
+        finally:
+            _lib.set_tuning("bwd_sort", 1)
+        for a, b_ in zip(got, ref):
+            assert torch.equal(a, b_), precision
