@@ -744,10 +744,18 @@ constexpr int kQRows = 1024;   // batches listed at a time (a box's union at +-2
 #define DVC_QSTAGES 4
 #endif
 constexpr int kQStages = DVC_QSTAGES;   // LDS stages of the batch pipeline (kQStages - 2 in flight across the barrier)
-// workgroups per CU the LDS allows (kQStages x 8 / 12 KB stages + the batch list, of 160 KB), the launch-bounds hint
-template <bool SPLIT> constexpr int kQOcc = (160 * 1024) / (kQStages * (SPLIT ? 12288 : 8192) + 4 * 1024 + 16) < 4
-                                                ? (160 * 1024) / (kQStages * (SPLIT ? 12288 : 8192) + 4 * 1024 + 16)
-                                                : 4;
+// G16 (16-bit window gradients, round 5): 6 KB stages (4 KB target tile + 2 KB G tile; waves 2-3's empty DMAs land in
+// one spare 2 KB region outside the stages), so more stages fit the same LDS
+#ifndef DVC_QSTAGES16
+#define DVC_QSTAGES16 4
+#endif
+template <bool SPLIT, bool G16> constexpr int kQNst = G16 && !SPLIT ? DVC_QSTAGES16 : kQStages;
+template <bool SPLIT, bool G16> constexpr int kQStage = SPLIT ? 12288 : G16 ? 6144 : 8192;
+template <bool SPLIT, bool G16> constexpr int kQLds = kQNst<SPLIT, G16> * kQStage<SPLIT, G16> + (G16 && !SPLIT ? 2048 : 0);
+// workgroups per CU the LDS allows (the stages + the batch list, of 160 KB; at most 5), the launch-bounds hint
+template <bool SPLIT, bool G16> constexpr int kQOcc = (160 * 1024) / (kQLds<SPLIT, G16> + 4 * 1024 + 16) < 5
+                                                          ? (160 * 1024) / (kQLds<SPLIT, G16> + 4 * 1024 + 16)
+                                                          : 5;
 constexpr unsigned kOOB = 0x80000000u;   // a buffer offset past every range (reads 0)
 // diagnostics builds only (tools/build_variant.sh -DDVC_GQ_ABL=n): 1 no MFMAs, 2 no G DMAs, 4 no T DMAs
 #ifndef DVC_GQ_ABL
@@ -816,13 +824,13 @@ __device__ __forceinline__ bf16x8 dup_bf16x4(u32x2 v) {
 // into a spare region so that every wave counts the same DMAs), K = the batch's 16 z in ONE MFMA per query block
 // (the pair format needs two), and the B operand is the target tile's 8 z as they stand.
 template <int NCT, bool F16, bool SPLIT = false, bool G16 = false>   // channel tiles of 32 (C_pad / 32, <= 4 per launch)
-__global__ __launch_bounds__(256, kQOcc<SPLIT>) void k_grad_q_mfma(const bf16_t *__restrict__ Tz, float *__restrict__ dQp,
+__global__ __launch_bounds__(256, (kQOcc<SPLIT, G16>)) void k_grad_q_mfma(const bf16_t *__restrict__ Tz, float *__restrict__ dQp,
                                                         long long part_stride, BwdArgs A, long long tz_lo,
                                                         const unsigned long long *__restrict__ skeys, int bsort,
                                                         int ns, int nsl, int lfirst) {
-    // bytes per stage: T tile (4 KB, 16-bit) + G tile (4 KB, hi/lo pairs) [+ T lo tile (4 KB)]
-    constexpr int STAGE = SPLIT ? 12288 : 8192;
-    __shared__ __attribute__((aligned(16))) unsigned char stg[kQStages * STAGE];
+    // bytes per stage: T tile (4 KB, 16-bit) + G tile (4 KB, hi/lo pairs; G16: 2 KB) [+ T lo tile (4 KB)]
+    constexpr int STAGE = kQStage<SPLIT, G16>, NST = kQNst<SPLIT, G16>;
+    __shared__ __attribute__((aligned(16))) unsigned char stg[kQLds<SPLIT, G16>];
     __shared__ unsigned qrows[kQRows + 2];           // batches (y | x << 11 | z0 << 22), count, next row
     const int tid = threadIdx.x, lane = tid & 63, m = lane & 31, h = lane >> 5;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -949,8 +957,9 @@ __global__ __launch_bounds__(256, kQOcc<SPLIT>) void k_grad_q_mfma(const bf16_t 
                 const int wy = y - goh, wx = x - gou, wz = z0 - gov;
                 if constexpr (G16) {   // wz = the chunk's first element in the row (even)
                     const bool ok = (unsigned)wy < (unsigned)nh && (unsigned)wx < (unsigned)nu && wz > -8 && wz < rz;
+                    // (waves 2-3: the spare region after the stages)
                     blds(rs_g, ok ? (unsigned)(2 * gqo + (wy * nu + wx) * rz + wz) * 2u + 16u : kOOB, 0u,
-                         sb + 4096 + 1024 * w, W16{});
+                         w < 2 ? sb + 4096 + 1024 * w : sbase + NST * STAGE + 1024 * (w - 2), W16{});
                 } else {
                     const bool ok = (unsigned)wy < (unsigned)nh && (unsigned)wx < (unsigned)nu && wz > -4 && wz < nv;
                     blds(rs_g, ok ? (unsigned)(gqo + (wy * nu + wx) * nv + wz) * 4u + 16u : kOOB, 0u,
@@ -986,17 +995,17 @@ __global__ __launch_bounds__(256, kQOcc<SPLIT>) void k_grad_q_mfma(const bf16_t 
             if (nit == 0) continue;
             // batches 0 .. kQStages - 2 in flight (past the end: the last batch again, into a stage never read)
 #pragma unroll
-            for (int k = 0; k < kQStages - 1; ++k) issue(min(k, nit - 1), k);
+            for (int k = 0; k < NST - 1; ++k) issue(min(k, nit - 1), k);
             for (int it = 0; it < nit; ++it) {
                 // batch it has landed (this thread's DMAs; kQStages - 2 newer batches may fly), then every thread's
                 // has, and every wave is done with batch it - 1, whose stage the next DMA refills
                 constexpr int kDma = ((DVC_GQ_ABL & 4) ? 0 : (SPLIT ? 2 : 1)) + ((DVC_GQ_ABL & 2) ? 0 : 1);   // DMAs per batch
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kDma * (kQStages - 2)) : "memory");
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kDma * (NST - 2)) : "memory");
                 __builtin_amdgcn_s_barrier();
                 asm volatile("" ::: "memory");
-                issue(min(it + kQStages - 1, nit - 1), (it + kQStages - 1) % kQStages);
+                issue(min(it + NST - 1, nit - 1), (it + NST - 1) % NST);
                 if (G16 && w < NCT && !(DVC_GQ_ABL & 1)) {
-                    const unsigned char *sb = stg + (it % kQStages) * STAGE;
+                    const unsigned char *sb = stg + (it % NST) * STAGE;
                     const int r = 32 * w + m, rsw = (r >> 3) & 1;
                     const int bz0 = (int)(__builtin_amdgcn_readfirstlane(qrows[it]) >> 22);   // the batch's z0
                     // B: this lane's 8 targets z = 8 h .. 8 h + 7 of channel r
@@ -1017,7 +1026,7 @@ __global__ __launch_bounds__(256, kQOcc<SPLIT>) void k_grad_q_mfma(const bf16_t 
                         acc[T] = mma32<F16>(__builtin_bit_cast(bf16x8, av), bt, acc[T]);
                     }
                 } else if (w < NCT && !(DVC_GQ_ABL & 1)) {
-                    const unsigned char *sb = stg + (it % kQStages) * STAGE;
+                    const unsigned char *sb = stg + (it % NST) * STAGE;
                     const int r = 32 * w + m, rsw = (r >> 3) & 1;
                     const int bz0 = (int)(__builtin_amdgcn_readfirstlane(qrows[it]) >> 22);   // the batch's z0
 #pragma unroll
@@ -1662,9 +1671,12 @@ __global__ __launch_bounds__(256, SPLIT ? 3 : 4) void k_grad_t_mfma(const bf16_t
 // A batch's query tile is gathered from the packed query rows (thread (query j, channel octet r) loads 16 bytes) and
 // stored transposed into the [128 ch][16 q] tile the MFMA B operand reads, so k_qt_tiles is not needed either.  The
 // rest -- window-gradient staging, MFMAs, epilogue, split partials -- is k_grad_t_mfma<.., G16>'s.
+#ifndef DVC_DENSE_OCC
+#define DVC_DENSE_OCC 4   // workgroups per CU k_grad_t_dense is compiled for
+#endif
 constexpr int kDenseRows = 320;   // origin rows per brick: (4 + 2r + 1)^2 <= 289 for r <= 6
 template <int NCT, bool F16>
-__global__ __launch_bounds__(256, 4) void k_grad_t_dense(const bf16_t *__restrict__ Qp,
+__global__ __launch_bounds__(256, DVC_DENSE_OCC) void k_grad_t_dense(const bf16_t *__restrict__ Qp,
                                                          const unsigned long long *__restrict__ keys,
                                                          const int *__restrict__ starts, float *__restrict__ dT,
                                                          float *__restrict__ dTp, BwdArgs A, int b) {
