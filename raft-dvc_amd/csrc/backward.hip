@@ -2137,6 +2137,30 @@ void set_backward_g16(int v) { g_bwd_g16 = v; }
 // 1 (default): k_grad_t_dense's batches across origin rows for 16-bit blocks; 0: k_grad_t_mfma's per-row batches
 static thread_local int g_bwd_dense = 1;
 void set_backward_dense(int v) { g_bwd_dense = v; }
+// 1 (default): batch element 0's key sort on a side stream beside the window gradients (tuning "bwd_side")
+static thread_local int g_bwd_side = 1;
+void set_backward_side(int v) { g_bwd_side = v; }
+struct BwdSide {
+    int dev = -1;
+    hipStream_t st = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+// one side stream and its fork / join events per host thread and device, created on first use (never destroyed)
+static BwdSide *bwd_side_stream() {
+    static thread_local BwdSide sides[16];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+    BwdSide &sd = sides[dev];
+    if (sd.dev == dev) return &sd;
+    int least = 0, greatest = 0;   // (the highest priority: the small launches get their slots promptly)
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
+    if (hipStreamCreateWithPriority(&sd.st, hipStreamNonBlocking, greatest) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&sd.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&sd.join, hipEventDisableTiming) != hipSuccess)
+        return nullptr;
+    sd.dev = dev;
+    return &sd;
+}
 // 1 (default): the keys' counting sort (k_cell_scatter / k_cell_rank, round 5); 0: rocprim's radix sort + k_cell_starts
 static thread_local int g_bwd_sort = 1;
 void set_backward_sort(int v) { g_bwd_sort = v; }
@@ -2195,6 +2219,90 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     // operands keep the hi/lo pairs, and so do pyramids with a legacy W != D level (k_win_grad_generic's boxes)
     const bool g16 = mfma && !SPLIT && !any_generic && g_bwd_g16;
     const int fmt = g16 ? (F16 ? kGwS16H : kGwS16B) : mfma ? (F16 ? kGwF16 : kGwBf16) : kGwF32;
+    // target gradients: per batch element, the queries of every level in window-origin order (one key
+    // space, one sort), then one k_grad_t launch over every level's (brick, split) workgroups, coarse levels'
+    // split partials reduced by one launch
+    // dense batches across origin rows (k_grad_t_dense) for 16-bit window gradients
+    bool dense = g16 && g_bwd_dense;
+    for (int l = 0; l < A.L; ++l)
+        dense = dense && (long long)(3 + A.nwh[l]) * (3 + A.nwu[l]) <= kDenseRows;
+    int nblk = 0;
+    long long nred = 0;
+    for (int l = 0; l < A.L; ++l) {
+        const long long bricks = (long long)((A.H[l] + 3) / 4) * ((A.W[l] + 3) / 4) * ((A.D[l] + 3) / 4);
+        A.coff[l] = P.coff[l];
+        A.gt_sp[l] = P.sp[l];
+        A.gt_poff[l] = P.poff[l];
+        A.gt_blk0[l] = nblk;
+        A.gt_r0[l] = nred;
+        if (A.zero[l]) continue;   // a size-1 level gets no gradient (its dT rows are never read)
+        nblk += (int)(bricks * P.sp[l]);
+        if (P.sp[l] > 1) nred += bricks * 64 * (A.Cp / 2);
+    }
+    A.gt_blk0[A.L] = nblk;
+    A.gt_r0[A.L] = nred;
+    const long long ncell = P.coff[A.L] - 1;   // the last level's outside cell
+    const long long nkeys = (long long)A.L * A.Nq;
+    unsigned bits = 1;
+    while ((1LL << bits) <= ncell) ++bits;
+    // counting sort (default) or the radix sort of rounds 3-4 (tuning "bwd_sort" 0): the same sorted keys
+    const bool counting = g_bwd_sort != 0;
+    int *cellcnt = reinterpret_cast<int *>(reinterpret_cast<unsigned char *>(starts) + P.cnt_off);
+    int *slot = reinterpret_cast<int *>(reinterpret_cast<unsigned char *>(starts) + 2 * P.cnt_off);   // per key
+    const unsigned long long *ks = counting ? kin : kout;   // the sorted keys
+    if (counting && hipMemsetAsync(cellcnt, 0, (size_t)(ncell + 2) * sizeof(int), s) != hipSuccess) {
+        snprintf(err, errlen, "corr_backward: cell count clear failed");
+        return DVC_ERR_RUNTIME;
+    }
+    // the key sort of batch element b on stream st (counting sort, or the radix sort + k_cell_starts)
+    auto sort_keys = [&](int b, hipStream_t st) -> int {
+        k_bw_keys<R><<<dim3((unsigned)((A.Nq + 255) / 256), (unsigned)A.L), 256, 0, st>>>(
+            A, b, kin, counting ? cellcnt : nullptr, slot);
+        if (!launched("keys")) return DVC_ERR_LAUNCH;
+        size_t tb = P.temp;
+        if (counting) {
+            // starts[c] = keys of cells < c, for c in [0, ncell + 1]
+            if (rocprim::exclusive_scan(temp, tb, cellcnt, starts, 0, (size_t)(ncell + 2), rocprim::plus<int>(), st) !=
+                hipSuccess) {
+                snprintf(err, errlen, "corr_backward: cell scan failed");
+                return DVC_ERR_RUNTIME;
+            }
+            const unsigned kb = (unsigned)((nkeys + 255) / 256);
+            k_cell_scatter<<<kb, 256, 0, st>>>(kin, slot, nkeys, starts, cellcnt, kout);
+            k_cell_rank<<<kb, 256, 0, st>>>(kout, nkeys, starts, kin);
+            if (!launched("cell_sort")) return DVC_ERR_LAUNCH;
+        } else {
+            // (the cell bits only: the keys enter in (level, query) order and the sort is stable, so within a cell
+            // the queries stay in ascending order -- the order of the full keys -- in 2-3 digit passes, not 6-7)
+            if (rocprim::radix_sort_keys(temp, tb, kin, kout, (size_t)nkeys, 32u, 32u + bits, st) != hipSuccess) {
+                snprintf(err, errlen, "corr_backward: radix sort failed");
+                return DVC_ERR_RUNTIME;
+            }
+            k_cell_starts<<<(unsigned)((ncell + 1 + 255) / 256), 256, 0, st>>>(kout, nkeys, ncell, starts);
+            if (!launched("cell_starts")) return DVC_ERR_LAUNCH;
+        }
+        return DVC_OK;
+    };
+    // Round 5: batch element 0's sort needs only the coordinates, so it runs on a side stream beside the window
+    // gradients and the target tiles (its ~35 us of small launches hid under k_win_grad_pairs); the main stream
+    // waits for it before the first consumer of the sorted keys.  Not while the stream is being captured.
+    BwdSide *side = g_bwd_side ? bwd_side_stream() : nullptr;
+    if (side) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) side = nullptr;
+    }
+    if (side) {
+        if (hipEventRecord(side->fork, s) != hipSuccess || hipStreamWaitEvent(side->st, side->fork, 0) != hipSuccess) {
+            snprintf(err, errlen, "corr_backward: side stream fork failed");
+            return DVC_ERR_RUNTIME;
+        }
+        const int rc = sort_keys(0, side->st);
+        if (rc != DVC_OK) return rc;
+        if (hipEventRecord(side->join, side->st) != hipSuccess) {
+            snprintf(err, errlen, "corr_backward: side stream join failed");
+            return DVC_ERR_RUNTIME;
+        }
+    }
     const unsigned wgrid = (unsigned)((A.B * A.L * nqb + 3) / 4);
     {   // two lanes per query (k_win_grad_pairs)
         const long long nqb2 = (A.Nq + 31) / 32;
@@ -2255,13 +2363,19 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     if constexpr (k16) {
         if (mfma) {
             for (int l = 0; l <= A.L; ++l) A.tz0[l] = P.tz0[l];
+            // (the sorted path's first consumer waits for the side stream anyway: the tiles go there too)
+            const hipStream_t ts = side && qsorted ? side->st : s;
             if constexpr (SPLIT)
-                k_tile_targets<float><<<dim3((unsigned)P.tz0[A.L], (unsigned)ngroups, (unsigned)A.B), 256, 0, s>>>(
+                k_tile_targets<float><<<dim3((unsigned)P.tz0[A.L], (unsigned)ngroups, (unsigned)A.B), 256, 0, ts>>>(
                     Tt, ttr, A, tz_lo);
             else
-                k_tile_targets<bf16_t><<<dim3((unsigned)P.tz0[A.L], (unsigned)ngroups, (unsigned)A.B), 256, 0, s>>>(
+                k_tile_targets<bf16_t><<<dim3((unsigned)P.tz0[A.L], (unsigned)ngroups, (unsigned)A.B), 256, 0, ts>>>(
                     reinterpret_cast<const bf16_t *>(Tt), ttr, A, 0);
             if (!launched("tile_targets")) return DVC_ERR_LAUNCH;
+            if (ts != s && hipEventRecord(side->join, ts) != hipSuccess) {
+                snprintf(err, errlen, "corr_backward: side stream join failed");
+                return DVC_ERR_RUNTIME;
+            }
             // (qsorted: after each batch element's sort, below)
             if (!qsorted) launch_q(dim3((unsigned)boxes, (unsigned)qparts), nullptr, -1, 0, 0, 0);
             done_q = true;
@@ -2275,66 +2389,15 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
         }
     }
     if (!launched("grad_q")) return DVC_ERR_LAUNCH;
-    // target gradients: per batch element, the queries of every level in window-origin order (one key
-    // space, one sort), then one k_grad_t launch over every level's (brick, split) workgroups, coarse levels'
-    // split partials reduced by one launch
-    // dense batches across origin rows (k_grad_t_dense) for 16-bit window gradients
-    bool dense = g16 && g_bwd_dense;
-    for (int l = 0; l < A.L; ++l)
-        dense = dense && (long long)(3 + A.nwh[l]) * (3 + A.nwu[l]) <= kDenseRows;
-    int nblk = 0;
-    long long nred = 0;
-    for (int l = 0; l < A.L; ++l) {
-        const long long bricks = (long long)((A.H[l] + 3) / 4) * ((A.W[l] + 3) / 4) * ((A.D[l] + 3) / 4);
-        A.coff[l] = P.coff[l];
-        A.gt_sp[l] = P.sp[l];
-        A.gt_poff[l] = P.poff[l];
-        A.gt_blk0[l] = nblk;
-        A.gt_r0[l] = nred;
-        if (A.zero[l]) continue;   // a size-1 level gets no gradient (its dT rows are never read)
-        nblk += (int)(bricks * P.sp[l]);
-        if (P.sp[l] > 1) nred += bricks * 64 * (A.Cp / 2);
-    }
-    A.gt_blk0[A.L] = nblk;
-    A.gt_r0[A.L] = nred;
-    const long long ncell = P.coff[A.L] - 1;   // the last level's outside cell
-    const long long nkeys = (long long)A.L * A.Nq;
-    unsigned bits = 1;
-    while ((1LL << bits) <= ncell) ++bits;
-    // counting sort (default) or the radix sort of rounds 3-4 (tuning "bwd_sort" 0): the same sorted keys
-    const bool counting = g_bwd_sort != 0;
-    int *cellcnt = reinterpret_cast<int *>(reinterpret_cast<unsigned char *>(starts) + P.cnt_off);
-    int *slot = reinterpret_cast<int *>(reinterpret_cast<unsigned char *>(starts) + 2 * P.cnt_off);   // per key
-    const unsigned long long *ks = counting ? kin : kout;   // the sorted keys
-    if (counting && hipMemsetAsync(cellcnt, 0, (size_t)(ncell + 2) * sizeof(int), s) != hipSuccess) {
-        snprintf(err, errlen, "corr_backward: cell count clear failed");
-        return DVC_ERR_RUNTIME;
-    }
     for (int b = 0; b < A.B; ++b) {
-        k_bw_keys<R><<<dim3((unsigned)((A.Nq + 255) / 256), (unsigned)A.L), 256, 0, s>>>(
-            A, b, kin, counting ? cellcnt : nullptr, slot);
-        if (!launched("keys")) return DVC_ERR_LAUNCH;
-        size_t tb = P.temp;
-        if (counting) {
-            // starts[c] = keys of cells < c, for c in [0, ncell + 1]
-            if (rocprim::exclusive_scan(temp, tb, cellcnt, starts, 0, (size_t)(ncell + 2), rocprim::plus<int>(), s) !=
-                hipSuccess) {
-                snprintf(err, errlen, "corr_backward: cell scan failed");
+        if (b == 0 && side) {   // (sorted on the side stream)
+            if (hipStreamWaitEvent(s, side->join, 0) != hipSuccess) {
+                snprintf(err, errlen, "corr_backward: side stream wait failed");
                 return DVC_ERR_RUNTIME;
             }
-            const unsigned kb = (unsigned)((nkeys + 255) / 256);
-            k_cell_scatter<<<kb, 256, 0, s>>>(kin, slot, nkeys, starts, cellcnt, kout);
-            k_cell_rank<<<kb, 256, 0, s>>>(kout, nkeys, starts, kin);
-            if (!launched("cell_sort")) return DVC_ERR_LAUNCH;
         } else {
-            // (the cell bits only: the keys enter in (level, query) order and the sort is stable, so within a cell
-            // the queries stay in ascending order -- the order of the full keys -- in 2-3 digit passes, not 6-7)
-            if (rocprim::radix_sort_keys(temp, tb, kin, kout, (size_t)nkeys, 32u, 32u + bits, s) != hipSuccess) {
-                snprintf(err, errlen, "corr_backward: radix sort failed");
-                return DVC_ERR_RUNTIME;
-            }
-            k_cell_starts<<<(unsigned)((ncell + 1 + 255) / 256), 256, 0, s>>>(kout, nkeys, ncell, starts);
-            if (!launched("cell_starts")) return DVC_ERR_LAUNCH;
+            const int rc = sort_keys(b, s);
+            if (rc != DVC_OK) return rc;
         }
         if (qsorted) {   // level l's keys are the l-th Nq sorted ones (its cells come after level l - 1's); the
                          // coarser levels' boxes of this batch element in the same launch
