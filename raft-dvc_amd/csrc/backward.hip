@@ -2011,9 +2011,14 @@ static void win_dims(const dvc_layout &lay, int l, int radius, bool legacy, int 
 // row per wave and split
 // splits per brick: ~512 workgroups per level, each wave of a split owning >= ~1 chunk of 64 queries on
 // average (the chunks, not the origin rows, are dealt to the waves)
-static int grad_t_splits(const dvc_layout &lay, int l, long long Nq) {
+// (tuning "bwd_gt_wg": the workgroups per level aimed at, 64 .. 512; the workspace is sized for 512.  Round 5,
+// dense batches at config #3: 128 / 256 / 384 / 512 -> 0.80 / 0.69 / 0.65 / 0.615 ms; 768 / 1024 (level 0 in two
+// splits, sized for the test only) 0.67 / 0.66)
+static thread_local int g_gt_wg = 512;
+void set_backward_gt_wg(int v) { g_gt_wg = v; }
+static int grad_t_splits(const dvc_layout &lay, int l, long long Nq, int target = 512) {
     const long long bricks = (long long)((lay.H[l] + 3) / 4) * ((lay.W[l] + 3) / 4) * ((lay.D[l] + 3) / 4);
-    long long sp = (512 + bricks - 1) / bricks;
+    long long sp = (target + bricks - 1) / bricks;
     sp = std::min(sp, std::max(1LL, Nq / 256));
     return (int)std::max(1LL, std::min(sp, 256LL));
 }
@@ -2046,11 +2051,12 @@ static void bwd_plan(int B, long long Nq, const dvc_layout &lay, int radius, boo
         gw += (size_t)B * Nq * P.nw[l][0] * P.nw[l][1] * P.nw[l][2] * sizeof(float);
         P.coff[l] = cells;
         cells += level_cells(lay, l, P.nw[l]) + 1;   // + the level's "outside" cell
-        P.sp[l] = grad_t_splits(lay, l, Nq);
+        P.sp[l] = grad_t_splits(lay, l, Nq, std::min(g_gt_wg, 512));
         const long long bricks = (long long)((lay.H[l] + 3) / 4) * ((lay.W[l] + 3) / 4) * ((lay.D[l] + 3) / 4);
         P.poff[l] = (long long)(part / sizeof(float));
-        if (P.sp[l] > 1 && !lay.zero_level[l])
-            part += (size_t)P.sp[l] * (size_t)bricks * 64 * (size_t)lay.c_pad * sizeof(float);
+        const int spm = grad_t_splits(lay, l, Nq);   // (the workspace: sized for the default, largest target)
+        if (spm > 1 && !lay.zero_level[l])
+            part += (size_t)spm * (size_t)bricks * 64 * (size_t)lay.c_pad * sizeof(float);
     }
     P.coff[L] = cells;
     // the target-gradient pass sorts the keys of all L levels of one batch element at once
