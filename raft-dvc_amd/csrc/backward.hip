@@ -2146,10 +2146,12 @@ void set_backward_dense(int v) { g_bwd_dense = v; }
 // 1 (default): batch element 0's key sort on a side stream beside the window gradients (tuning "bwd_side")
 static thread_local int g_bwd_side = 1;
 void set_backward_side(int v) { g_bwd_side = v; }
+static thread_local int g_bwd_side_q = 0;
+void set_backward_side_q(int v) { g_bwd_side_q = v; }
 struct BwdSide {
     int dev = -1;
     hipStream_t st = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr, wg = nullptr, jq = nullptr;
 };
 // one side stream and its fork / join events per host thread and device, created on first use (never destroyed)
 static BwdSide *bwd_side_stream() {
@@ -2162,7 +2164,9 @@ static BwdSide *bwd_side_stream() {
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
     if (hipStreamCreateWithPriority(&sd.st, hipStreamNonBlocking, greatest) != hipSuccess) return nullptr;
     if (hipEventCreateWithFlags(&sd.fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&sd.join, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&sd.join, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&sd.wg, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&sd.jq, hipEventDisableTiming) != hipSuccess)
         return nullptr;
     sd.dev = dev;
     return &sd;
@@ -2348,17 +2352,17 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     // one k_grad_q_mfma launch per 128-channel group: grid, sorted keys and batch element (or -1: every batch
     // element's boxes), sorted groups per level and sorted levels at the start of the grid, first level of the
     // boxes (0: the level groups)
-    auto launch_q = [&](dim3 grid, const unsigned long long *sk, int bs, int ns, int nsl_, int lfirst) {
+    auto launch_q = [&](hipStream_t st, dim3 grid, const unsigned long long *sk, int bs, int ns, int nsl_, int lfirst) {
         for (int g = 0; g < ngroups; ++g) {
             BwdArgs Ag = A;
             Ag.cbase = 128 * g;
             auto go = [&](auto g16c) {
                 constexpr bool GG = decltype(g16c)::value && !SPLIT;
                 switch (std::min(128, A.Cp - Ag.cbase) / 32) {
-                case 1: k_grad_q_mfma<1, F16, SPLIT, GG><<<grid, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo, sk, bs, ns, nsl_, lfirst); break;
-                case 2: k_grad_q_mfma<2, F16, SPLIT, GG><<<grid, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo, sk, bs, ns, nsl_, lfirst); break;
-                case 3: k_grad_q_mfma<3, F16, SPLIT, GG><<<grid, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo, sk, bs, ns, nsl_, lfirst); break;
-                default: k_grad_q_mfma<4, F16, SPLIT, GG><<<grid, 256, 0, s>>>(ttr, dq, qstride, Ag, tz_lo, sk, bs, ns, nsl_, lfirst); break;
+                case 1: k_grad_q_mfma<1, F16, SPLIT, GG><<<grid, 256, 0, st>>>(ttr, dq, qstride, Ag, tz_lo, sk, bs, ns, nsl_, lfirst); break;
+                case 2: k_grad_q_mfma<2, F16, SPLIT, GG><<<grid, 256, 0, st>>>(ttr, dq, qstride, Ag, tz_lo, sk, bs, ns, nsl_, lfirst); break;
+                case 3: k_grad_q_mfma<3, F16, SPLIT, GG><<<grid, 256, 0, st>>>(ttr, dq, qstride, Ag, tz_lo, sk, bs, ns, nsl_, lfirst); break;
+                default: k_grad_q_mfma<4, F16, SPLIT, GG><<<grid, 256, 0, st>>>(ttr, dq, qstride, Ag, tz_lo, sk, bs, ns, nsl_, lfirst); break;
                 }
             };
             if (g16) go(std::true_type{});
@@ -2383,7 +2387,7 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
                 return DVC_ERR_RUNTIME;
             }
             // (qsorted: after each batch element's sort, below)
-            if (!qsorted) launch_q(dim3((unsigned)boxes, (unsigned)qparts), nullptr, -1, 0, 0, 0);
+            if (!qsorted) launch_q(s, dim3((unsigned)boxes, (unsigned)qparts), nullptr, -1, 0, 0, 0);
             done_q = true;
         }
     }
@@ -2395,7 +2399,18 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
         }
     }
     if (!launched("grad_q")) return DVC_ERR_LAUNCH;
+    // (tuning "bwd_side_q": batch element 0's sorted dQ pass on the side stream too, beside the target gradients;
+    // it waits for the window gradients, the main stream for it before the next sort and the dQ unpack)
+    const bool qside = side && qsorted && g_bwd_side_q;
+    if (qside && (hipEventRecord(side->wg, s) != hipSuccess || hipStreamWaitEvent(side->st, side->wg, 0) != hipSuccess)) {
+        snprintf(err, errlen, "corr_backward: side stream fork failed");
+        return DVC_ERR_RUNTIME;
+    }
     for (int b = 0; b < A.B; ++b) {
+        if (b == 1 && qside && hipStreamWaitEvent(s, side->jq, 0) != hipSuccess) {
+            snprintf(err, errlen, "corr_backward: side stream wait failed");
+            return DVC_ERR_RUNTIME;
+        }
         if (b == 0 && side) {   // (sorted on the side stream)
             if (hipStreamWaitEvent(s, side->join, 0) != hipSuccess) {
                 snprintf(err, errlen, "corr_backward: side stream wait failed");
@@ -2408,9 +2423,14 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
         if (qsorted) {   // level l's keys are the l-th Nq sorted ones (its cells come after level l - 1's); the
                          // coarser levels' boxes of this batch element in the same launch
             const int ns = (int)((A.Nq + 63) / 64);
-            launch_q(dim3((unsigned)std::max<long long>(ns, A.L > nsl ? boxes / A.B : 0),
-                          (unsigned)(nsl + (A.L > nsl ? 1 : 0))), ks, b, ns, nsl, nsl);
+            const bool on_side = qside && b == 0;
+            launch_q(on_side ? side->st : s, dim3((unsigned)std::max<long long>(ns, A.L > nsl ? boxes / A.B : 0),
+                                                 (unsigned)(nsl + (A.L > nsl ? 1 : 0))), ks, b, ns, nsl, nsl);
             if (!launched("grad_q_sorted")) return DVC_ERR_LAUNCH;
+            if (on_side && hipEventRecord(side->jq, side->st) != hipSuccess) {
+                snprintf(err, errlen, "corr_backward: side stream join failed");
+                return DVC_ERR_RUNTIME;
+            }
         }
         if (nblk == 0) continue;
         bool done_t = false;
@@ -2471,6 +2491,10 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
             k_grad_t_reduce<<<(unsigned)((nred + 255) / 256), 256, 0, s>>>(dtp, dt, A, b);
             if (!launched("grad_t_reduce")) return DVC_ERR_LAUNCH;
         }
+    }
+    if (qside && A.B == 1 && hipStreamWaitEvent(s, side->jq, 0) != hipSuccess) {
+        snprintf(err, errlen, "corr_backward: side stream wait failed");
+        return DVC_ERR_RUNTIME;
     }
     // dfmap1 (B, C, Nq) <- dQ
     UnpackArgs U{};
