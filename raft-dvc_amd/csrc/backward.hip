@@ -2146,7 +2146,7 @@ void set_backward_dense(int v) { g_bwd_dense = v; }
 // 1 (default): batch element 0's key sort on a side stream beside the window gradients (tuning "bwd_side")
 static thread_local int g_bwd_side = 1;
 void set_backward_side(int v) { g_bwd_side = v; }
-static thread_local int g_bwd_side_q = 0;
+static thread_local int g_bwd_side_q = 1;
 void set_backward_side_q(int v) { g_bwd_side_q = v; }
 struct BwdSide {
     int dev = -1;
