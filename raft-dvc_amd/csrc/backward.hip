@@ -2492,18 +2492,21 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
             if (!launched("grad_t_reduce")) return DVC_ERR_LAUNCH;
         }
     }
-    if (qside && A.B == 1 && hipStreamWaitEvent(s, side->jq, 0) != hipSuccess) {
-        snprintf(err, errlen, "corr_backward: side stream wait failed");
-        return DVC_ERR_RUNTIME;
-    }
+    // (one batch element with the dQ pass on the side stream: its unpack follows it there, beside the target
+    // gradients' reduction and unpack, and the main stream joins at the end)
+    const bool uside = qside && A.B == 1;
     // dfmap1 (B, C, Nq) <- dQ
     UnpackArgs U{};
     U.src = dq; U.dst = g1; U.src_bstride = A.Nq; U.N = A.Nq; U.C = C; U.Cp = A.Cp; U.W = A.Wq; U.D = A.Dq;
     U.ns = 1; U.Hs[0] = A.Hq; U.Ws[0] = A.Wq; U.Ds[0] = A.Dq; U.Dps[0] = A.Dq; U.offs[0] = 0; U.wts[0] = 1.0f;
     U.nsum = qparts; U.sstride = qstride;
     dim3 g1grid((unsigned)((A.Nq + 63) / 64), (unsigned)((C + 63) / 64), (unsigned)A.B);
-    launch_unpack(U, g1grid, s);
+    launch_unpack(U, g1grid, uside ? side->st : s);
     if (!launched("unpack_q")) return DVC_ERR_LAUNCH;
+    if (uside && hipEventRecord(side->jq, side->st) != hipSuccess) {
+        snprintf(err, errlen, "corr_backward: side stream join failed");
+        return DVC_ERR_RUNTIME;
+    }
     // dfmap2 (B, C, H, W, D) <- sum_l 8^-l dT_l (floor-mode avg_pool3d adjoint)
     UnpackArgs V{};
     V.src = dt; V.dst = g2; V.src_bstride = lay.row_stride; V.C = C; V.Cp = A.Cp; V.W = lay.W[0]; V.D = lay.D[0];
@@ -2521,6 +2524,10 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     dim3 g2grid((unsigned)((V.N + 63) / 64), (unsigned)((C + 63) / 64), (unsigned)A.B);
     launch_unpack(V, g2grid, s);
     if (!launched("unpack_t")) return DVC_ERR_LAUNCH;
+    if (qside && hipStreamWaitEvent(s, side->jq, 0) != hipSuccess) {   // (every side-stream launch has joined)
+        snprintf(err, errlen, "corr_backward: side stream wait failed");
+        return DVC_ERR_RUNTIME;
+    }
     return DVC_OK;
 }
 
