@@ -364,3 +364,40 @@ def test_grad_counting_sort_matches_radix(shape, C, L, r, legacy, scale, B):
             _lib.set_tuning("bwd_sort", 1)
         for a, b_ in zip(got, ref):
             assert torch.equal(a, b_), precision
+
+
+@pytest.mark.parametrize("precision,tol", [("bf16", BF16_TOL), ("fp16", FP16_TOL)])
+def test_grad_cfg4_slab(precision, tol):
+    """Config #4 at full size (64^3 fmaps, C = 128, L = 4, r = 4, +-2-voxel flows; 262 K queries: the split counts,
+    sorted groups, dense target batches and counting sort at 8x config #3's query count), on the on-the-fly block
+    (the materialised 64^3 pyramid is 157 GB), with an output gradient nonzero on one ragged 512-row slab.  Against
+    autograd through oracle/torch_cpu.py's build_rows / lookup_rows on that slab, as test_grad_cfg3_slab."""
+    import dvccorr
+    from oracle import torch_cpu
+    B, C, S, L, r = 1, 128, 64, 4, 4
+    N, n3 = S ** 3, (2 * r + 1) ** 3
+    q0, q1 = 150001, 150001 + 512
+    f1 = prng.normal(7101, (B, C, S, S, S))
+    f2 = prng.normal(7102, (B, C, S, S, S))
+    coords = prng.flow_coords(7103, B, S, S, S, 2.0)
+    Gs = prng.normal(7104, (B, L * n3, q1 - q0))
+    t1 = torch.from_numpy(f1).requires_grad_(True)
+    t2 = torch.from_numpy(f2).requires_grad_(True)
+    pyr = torch_cpu.build_rows(t1, t2, L, q0, q1)
+    out = torch_cpu.lookup_rows(pyr, torch.from_numpy(coords), r, False, q0, q1)
+    (out * torch.from_numpy(Gs)).sum().backward()
+    ref1 = t1.grad.numpy().reshape(B, C, N)[:, :, q0:q1]
+    ref2 = t2.grad.numpy()
+    del pyr, out, t1, t2
+    g1 = torch.from_numpy(f1).to(DEV).requires_grad_(True)
+    g2 = torch.from_numpy(f2).to(DEV).requires_grad_(True)
+    blk = dvccorr.CorrBlockFused(g1, g2, L, r, precision=precision)
+    G = torch.zeros((B, L * n3, N), device=DEV)
+    G[:, :, q0:q1] = torch.from_numpy(Gs).to(DEV)
+    (blk(torch.from_numpy(coords).to(DEV)) * G.view(B, L * n3, S, S, S)).sum().backward()
+    d1 = g1.grad.reshape(B, C, N)
+    assert bool(torch.isfinite(d1).all()) and bool(torch.isfinite(g2.grad).all())
+    assert not bool(d1[:, :, :q0].any()) and not bool(d1[:, :, q1:].any())
+    e1 = orc.rel_err(d1[:, :, q0:q1].cpu().numpy(), ref1)
+    e2 = orc.rel_err(g2.grad.cpu().numpy(), ref2)
+    assert e1 <= tol and e2 <= tol, (precision, e1, e2)
