@@ -622,7 +622,7 @@ def backward_timing(args, f1, f2, coords, dims, dev, stream, precision=None):
     nbytes = gout.numel() * 4 + cf.numel() * 4 + (q.numel() + t.numel()) * esz + 2 * B * C * Nq * 4
     flops = 2.0 * 2 * C * (2 * R + 2) ** 3 * L * B * Nq
     mfma = bool(_lib.lib().dvc_corr_backward_mfma(B, Nq, C, S, S, S, L, R, 0, dt))
-    gt = "k_grad_t_dense" if precision in ("bf16", "fp16") else "k_qt_tiles + k_grad_t_mfma"
+    gt = "k_grad_t_dense"
     kern = (f"k_win_grad + k_grad_q_mfma + counting sort + {gt} + k_unpack_sum (dvc_corr_backward, {precision} "
             f"operands on v_mfma_f32_32x32x16_{'f16' if precision == 'fp16' else 'bf16'})" if mfma else
             f"k_win_grad + k_grad_q + counting sort + k_grad_t + k_unpack_sum (dvc_corr_backward, {precision} operands, "

@@ -1671,12 +1671,15 @@ __global__ __launch_bounds__(256, SPLIT ? 3 : 4) void k_grad_t_mfma(const bf16_t
 // A batch's query tile is gathered from the packed query rows (thread (query j, channel octet r) loads 16 bytes) and
 // stored transposed into the [128 ch][16 q] tile the MFMA B operand reads, so k_qt_tiles is not needed either.  The
 // rest -- window-gradient staging, MFMAs, epilogue, split partials -- is k_grad_t_mfma<.., G16>'s.
+// SPLIT (fp32 blocks, round 5): the window gradients as hi/lo pairs and the gathered fp32 query rows split into bf16
+// hi and lo tiles (split_bf16, as k_qt_tiles<float>), both multiplied -- k_grad_t_mfma<.., SPLIT>'s operands, without
+// k_qt_tiles and with dense batches.
 #ifndef DVC_DENSE_OCC
 #define DVC_DENSE_OCC 4   // workgroups per CU k_grad_t_dense is compiled for
 #endif
 constexpr int kDenseRows = 320;   // origin rows per brick: (4 + 2r + 1)^2 <= 289 for r <= 6
-template <int NCT, bool F16>
-__global__ __launch_bounds__(256, DVC_DENSE_OCC) void k_grad_t_dense(const bf16_t *__restrict__ Qp,
+template <int NCT, bool F16, bool SPLIT = false>
+__global__ __launch_bounds__(256, SPLIT ? 3 : DVC_DENSE_OCC) void k_grad_t_dense(const void *__restrict__ Qpv,
                                                          const unsigned long long *__restrict__ keys,
                                                          const int *__restrict__ starts, float *__restrict__ dT,
                                                          float *__restrict__ dTp, BwdArgs A, int b) {
@@ -1684,7 +1687,9 @@ __global__ __launch_bounds__(256, DVC_DENSE_OCC) void k_grad_t_dense(const bf16_
     const int l = gb.l, nsplit = gb.nsplit, split = gb.split, brick = gb.brick;
     starts += A.coff[l];
     __shared__ __attribute__((aligned(16))) bf16_t Ql[2][2048];   // [buf] query tile [128 ch][16] (swizzled)
-    __shared__ __attribute__((aligned(16))) unsigned Gq[2][64][8];  // [buf][target][16 queries] 16-bit
+    __shared__ __attribute__((aligned(16))) bf16_t Qll[SPLIT ? 2 : 1][SPLIT ? 2048 : 8];   // [buf] its lo tile
+    // [buf][target][16 queries] 16-bit (SPLIT: hi/lo pairs, swizzled in 4-query chunks)
+    __shared__ __attribute__((aligned(16))) unsigned Gq[2][64][SPLIT ? 16 : 8];
     __shared__ int rpre[kDenseRows + 1], rs0[kDenseRows];          // concatenation offset / first sorted position
     __shared__ int tq[kTCap][16], tzr[kTCap][16], trw[kTCap][16];   // entry (batch e, query j): query, z, row
     const int tid = threadIdx.x, lane = tid & 63, m = lane & 31, h = lane >> 5;
@@ -1692,7 +1697,7 @@ __global__ __launch_bounds__(256, DVC_DENSE_OCC) void k_grad_t_dense(const bf16_
     const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
     const int nh = A.nwh[l], nu = A.nwu[l], nv = A.nwv[l];
     const int rz = gw_rz(nv);
-    const long long nw3 = (long long)nh * nu * (rz >> 1);   // dwords per query
+    const long long nw3 = SPLIT ? bw_nw3(A, l) : (long long)nh * nu * (rz >> 1);   // dwords per query
     const int nbz = (Dl + 3) >> 2, nbx = (Wl + 3) >> 2, nby = (Hl + 3) >> 2;
     int t = brick;
     const int bz = t % nbz; t /= nbz;
@@ -1708,11 +1713,12 @@ __global__ __launch_bounds__(256, DVC_DENSE_OCC) void k_grad_t_dense(const bf16_
     const int ox0 = bx * 4, ox1 = min(bx * 4 + 3, Wl - 1) + nu - 1;
     const int oz0 = bz * 4, oz1 = min(bz * 4 + 3, Dl - 1) + nv - 1;
     const int nox = ox1 - ox0 + 1, nrows = (oy1 - oy0 + 1) * nox;
-    const unsigned short *g16 =
-        reinterpret_cast<const unsigned short *>(A.gwin + A.goff[l] + (long long)b * A.Nq * nw3);
+    const unsigned *glp = reinterpret_cast<const unsigned *>(A.gwin + A.goff[l] + (long long)b * A.Nq * nw3);
+    const unsigned short *g16 = reinterpret_cast<const unsigned short *>(glp);
     const unsigned *gzero = reinterpret_cast<const unsigned *>(A.gwin) - 64;   // the zeroed guard
     const bool qch = A.cbase + 8 * sr < A.Cp;   // this thread's channel octet exists
-    const bf16_t *qrow = Qp + (long long)b * A.Nq * A.Cp + A.cbase + 8 * sr;
+    using QT = typename std::conditional<SPLIT, float, bf16_t>::type;
+    const QT *qrow = reinterpret_cast<const QT *>(Qpv) + (long long)b * A.Nq * A.Cp + A.cbase + 8 * sr;
     // the rows' sorted ranges and their prefix (wave 0, 64 rows at a time)
     if (w == 0) {
         int run = 0;
@@ -1746,8 +1752,9 @@ __global__ __launch_bounds__(256, DVC_DENSE_OCC) void k_grad_t_dense(const bf16_
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[T][i] = 0.0f;
     struct Set {
-        u32x4 q, g;   // this thread's 8 channels of query j; its 4 targets' 16-bit values in g[0..1]
-        unsigned mk;  // bit k: target z tz0 + k inside the query's window row and the level
+        u32x4 q, ql, g;   // this thread's 8 channels of query j (SPLIT: hi, lo); its 4 targets' values (16-bit in
+                          // g[0..1]; SPLIT: hi/lo pairs)
+        unsigned mk;      // bit k: target z tz0 + k inside the query's window row and the level
     };
     auto load = [&](int i, int n, Set &S) __attribute__((always_inline)) {   // batch min(i, n - 1), unconditional
         const int e = min(i, n - 1);
@@ -1757,11 +1764,24 @@ __global__ __launch_bounds__(256, DVC_DENSE_OCC) void k_grad_t_dense(const bf16_
         const bool yxok = rval && (unsigned)py < (unsigned)nh && (unsigned)px < (unsigned)nu;
         const int pz0 = tz0 - tzr[e][sj] + nv - 1;
         const bool ok = qq >= 0 && yxok && pz0 > -4 && pz0 < nv;
-        const unsigned short *src16 = ok ? g16 + 2 * (long long)qq * nw3 + (py * nu + px) * rz + pz0 + (pz0 & 1)
-                                         : reinterpret_cast<const unsigned short *>(gzero);
-        __builtin_memcpy(&S.g, src16, 8);
-        const bf16_t *qs = qq >= 0 && qch ? qrow + (long long)qq * A.Cp : reinterpret_cast<const bf16_t *>(gzero);
-        __builtin_memcpy(&S.q, qs, 16);
+        if constexpr (SPLIT) {
+            const unsigned *src = ok ? glp + (long long)qq * nw3 + (py * nu + px) * nv + pz0 : gzero;
+            __builtin_memcpy(&S.g, src, 16);
+            float qf[8];
+            const float *qs = qq >= 0 && qch ? qrow + (long long)qq * A.Cp : reinterpret_cast<const float *>(gzero);
+            __builtin_memcpy(qf, qs, 32);
+            bf16_t hi[8], lo[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) split_bf16(qf[k], hi[k], lo[k]);
+            __builtin_memcpy(&S.q, hi, 16);
+            __builtin_memcpy(&S.ql, lo, 16);
+        } else {
+            const unsigned short *src16 = ok ? g16 + 2 * (long long)qq * nw3 + (py * nu + px) * rz + pz0 + (pz0 & 1)
+                                             : reinterpret_cast<const unsigned short *>(gzero);
+            __builtin_memcpy(&S.g, src16, 8);
+            const QT *qs = qq >= 0 && qch ? qrow + (long long)qq * A.Cp : reinterpret_cast<const QT *>(gzero);
+            __builtin_memcpy(&S.q, qs, 16);
+        }
         unsigned mk = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) mk |= ((unsigned)(pz0 + k) < (unsigned)nv && tz0 + k < Dl) ? 1u << k : 0u;
@@ -1773,6 +1793,17 @@ __global__ __launch_bounds__(256, DVC_DENSE_OCC) void k_grad_t_dense(const bf16_
                              (sj & 7);
 #pragma unroll
         for (int k = 0; k < 8; ++k) qd[16 * k] = (unsigned short)(S.q[k >> 1] >> (16 * (k & 1)));
+        if constexpr (SPLIT) {
+            unsigned short *qdl = qd + (reinterpret_cast<unsigned short *>(Qll[bb]) - reinterpret_cast<unsigned short *>(Ql[bb]));
+#pragma unroll
+            for (int k = 0; k < 8; ++k) qdl[16 * k] = (unsigned short)(S.ql[k >> 1] >> (16 * (k & 1)));
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {   // target 4 sr + k, query sj: chunk (sj / 4) ^ (row >> 2 & 3)
+                const int tr = 4 * sr + k;
+                Gq[bb][tr][4 * ((sj >> 2) ^ ((tr >> 2) & 3)) + (sj & 3)] = (S.mk >> k) & 1u ? S.g[k] : 0u;
+            }
+            return;
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {   // target 4 sr + k, query sj: 8-query chunk (sj / 8) ^ (row >> 3 & 1)
             const int tr = 4 * sr + k;
@@ -1783,6 +1814,23 @@ __global__ __launch_bounds__(256, DVC_DENSE_OCC) void k_grad_t_dense(const bf16_
     auto compute = [&](int bb) __attribute__((always_inline)) {
         if (w >= NCT) return;
         const int r = 32 * w + m, rsw = (r >> 3) & 1;
+        if constexpr (SPLIT) {   // k_grad_t_mfma<.., SPLIT>'s pair MFMAs: K = 16 (query, hi/lo) pairs, queries 8 j ..
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const bf16x8 bq = dup_bf16x4(*reinterpret_cast<const u32x2 *>(
+                    reinterpret_cast<const unsigned char *>(Ql[bb]) + r * 32 + 16 * (j ^ rsw) + 8 * h));
+                const bf16x8 bql = dup_bf16x4(*reinterpret_cast<const u32x2 *>(
+                    reinterpret_cast<const unsigned char *>(Qll[bb]) + r * 32 + 16 * (j ^ rsw) + 8 * h));
+#pragma unroll
+                for (int T = 0; T < 2; ++T) {
+                    const int tr = 32 * T + m;
+                    const bf16x8 ag = *reinterpret_cast<const bf16x8 *>(&Gq[bb][tr][4 * ((2 * j + h) ^ ((tr >> 2) & 3))]);
+                    acc[T] = mma32<false>(ag, bq, acc[T]);
+                    acc[T] = mma32<false>(ag, bql, acc[T]);
+                }
+            }
+            return;
+        }
         const bf16x8 bq = *reinterpret_cast<const bf16x8 *>(reinterpret_cast<const unsigned char *>(Ql[bb]) +
                                                              r * 32 + 16 * (h ^ rsw));
 #pragma unroll
@@ -2232,8 +2280,8 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     // target gradients: per batch element, the queries of every level in window-origin order (one key
     // space, one sort), then one k_grad_t launch over every level's (brick, split) workgroups, coarse levels'
     // split partials reduced by one launch
-    // dense batches across origin rows (k_grad_t_dense) for 16-bit window gradients
-    bool dense = g16 && g_bwd_dense;
+    // dense batches across origin rows (k_grad_t_dense): 16-bit window gradients, or fp32 blocks' pairs (SPLIT)
+    bool dense = (g16 || (mfma && SPLIT && !any_generic)) && g_bwd_dense;
     for (int l = 0; l < A.L; ++l)
         dense = dense && (long long)(3 + A.nwh[l]) * (3 + A.nwu[l]) <= kDenseRows;
     int nblk = 0;
@@ -2442,12 +2490,12 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
                     for (int cg = 0; cg < ngroups; ++cg) {
                         BwdArgs Ag = A;
                         Ag.cbase = 128 * cg;
-                        const bf16_t *Qb = reinterpret_cast<const bf16_t *>(Q);
+                        const void *Qb = Q;
                         switch (std::min(128, A.Cp - Ag.cbase) / 32) {
-                        case 1: k_grad_t_dense<1, F16><<<nblk, 256, 0, s>>>(Qb, ks, starts, dt, dtp, Ag, b); break;
-                        case 2: k_grad_t_dense<2, F16><<<nblk, 256, 0, s>>>(Qb, ks, starts, dt, dtp, Ag, b); break;
-                        case 3: k_grad_t_dense<3, F16><<<nblk, 256, 0, s>>>(Qb, ks, starts, dt, dtp, Ag, b); break;
-                        default: k_grad_t_dense<4, F16><<<nblk, 256, 0, s>>>(Qb, ks, starts, dt, dtp, Ag, b); break;
+                        case 1: k_grad_t_dense<1, F16, SPLIT><<<nblk, 256, 0, s>>>(Qb, ks, starts, dt, dtp, Ag, b); break;
+                        case 2: k_grad_t_dense<2, F16, SPLIT><<<nblk, 256, 0, s>>>(Qb, ks, starts, dt, dtp, Ag, b); break;
+                        case 3: k_grad_t_dense<3, F16, SPLIT><<<nblk, 256, 0, s>>>(Qb, ks, starts, dt, dtp, Ag, b); break;
+                        default: k_grad_t_dense<4, F16, SPLIT><<<nblk, 256, 0, s>>>(Qb, ks, starts, dt, dtp, Ag, b); break;
                         }
                     }
                     done_t = true;
