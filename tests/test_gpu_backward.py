@@ -401,3 +401,22 @@ def test_grad_cfg4_slab(precision, tol):
     e1 = orc.rel_err(d1[:, :, q0:q1].cpu().numpy(), ref1)
     e2 = orc.rel_err(g2.grad.cpu().numpy(), ref2)
     assert e1 <= tol and e2 <= tol, (precision, e1, e2)
+
+
+@pytest.mark.parametrize("knobs", [{"bwd_dense": 0}, {"bwd_side": 0}, {"bwd_side_q": 0}, {"bwd_sort": 0},
+                                   {"bwd_g16": 0, "bwd_dense": 0}])
+@pytest.mark.parametrize("precision,tol", [("bf16", BF16_TOL), ("fp16", FP16_TOL), ("fp32", GRAD_TOL)])
+def test_grad_round5_paths_off(knobs, precision, tol):
+    """The round-5 backward paths switched off one at a time (tuning knobs, thread-local): the per-row target
+    batches (k_qt_tiles + k_grad_t_mfma), the in-order stream, the dQ pass on the main stream, rocprim's radix sort,
+    and the hi/lo window-gradient pairs -- each still passes the C = 128, L = 4, r = 4 golden vectors (grad_cfg2),
+    so the fallbacks stay tested while the defaults move on."""
+    from dvccorr import _lib
+    defaults = {"bwd_dense": 1, "bwd_side": 1, "bwd_side_q": 1, "bwd_sort": 1, "bwd_g16": 1}
+    for k, v in knobs.items():
+        _lib.set_tuning(k, v)
+    try:
+        _check_golden("grad_cfg2", "gemm", precision, tol)
+    finally:
+        for k in knobs:
+            _lib.set_tuning(k, defaults[k])
