@@ -191,6 +191,9 @@ struct ProjCfg {
 // (ACH + 1 window planes), for launches whose (tile, level) pairs alone cannot fill the chip.
 // SPOL >= 0 (diagnostics, tuning "lookup_stpol"): the output stores' cache-policy bits instead of NT's
 // (16 = sc1: the line is not kept in the XCD's L2, which the plane loads then have to themselves).
+#ifndef DVC_PROJ_ABL
+#define DVC_PROJ_ABL 0
+#endif
 template <typename T, int R, bool NT, int ABL, int PROJ, int ACH, int NWV = 0, int SPOL = -1>
 __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)), PROJ == 2 ? 1 : 2) void k_lookup_tile(
     LookupArgs A) {
@@ -243,10 +246,17 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
                     // this row's weight block, [wave slice ks][16-channel tile ot][lane] x 8 fp16
                     const f16x8 *wr = wp + (long long)(l * n + a) * NWP * OT * 64;
                     f16x8 wa[NWP][OT], wal[PROJ == 2 ? NWP : 1][OT];
+#if DVC_PROJ_ABL & 1   // (diagnostics build only: no weight loads)
+#pragma unroll
+                    for (int ks = 0; ks < NWP; ++ks)
+#pragma unroll
+                        for (int ot = 0; ot < OT; ++ot) wa[ks][ot] = f16x8{} + (_Float16)(float)(a + ks + ot);
+#else
 #pragma unroll
                     for (int ks = 0; ks < NWP; ++ks)
 #pragma unroll
                         for (int ot = 0; ot < OT; ++ot) wa[ks][ot] = wr[(ks * OT + ot) * 64];
+#endif
                     if constexpr (PROJ == 2) {
 #pragma unroll
                         for (int ks = 0; ks < NWP; ++ks)
@@ -279,6 +289,9 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
                         }
                         continue;
                     }
+#if DVC_PROJ_ABL & 2   // (diagnostics build only: no MFMAs)
+                    continue;
+#endif
 #pragma unroll
                     for (int ks = 0; ks < NWP; ++ks) {
                         f16x8 xb[4];
