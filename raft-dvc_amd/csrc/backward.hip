@@ -2248,7 +2248,7 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     bf16_t *qt = (bf16_t *)(ws + P.gwin + P.dq + P.dt + 2 * P.keys + P.starts + P.temp + P.part);
     bf16_t *ttr = (bf16_t *)(ws + P.gwin + P.dq + P.dt + 2 * P.keys + P.starts + P.temp + P.part + P.qt);
     // the 256-byte guard before the window gradients is the zero source of the MFMA kernels' LDS-DMA gathers
-    if (hipMemsetAsync(ws, 0, 256, s) != hipSuccess) {
+    if (zero_async(ws, 256, s) != hipSuccess) {
         snprintf(err, errlen, "corr_backward: guard clear failed");
         return DVC_ERR_RUNTIME;
     }
@@ -2308,7 +2308,7 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     int *cellcnt = reinterpret_cast<int *>(reinterpret_cast<unsigned char *>(starts) + P.cnt_off);
     int *slot = reinterpret_cast<int *>(reinterpret_cast<unsigned char *>(starts) + 2 * P.cnt_off);   // per key
     const unsigned long long *ks = counting ? kin : kout;   // the sorted keys
-    if (counting && hipMemsetAsync(cellcnt, 0, (size_t)(ncell + 2) * sizeof(int), s) != hipSuccess) {
+    if (counting && zero_async(cellcnt, (size_t)(ncell + 2) * sizeof(int), s) != hipSuccess) {
         snprintf(err, errlen, "corr_backward: cell count clear failed");
         return DVC_ERR_RUNTIME;
     }

@@ -566,7 +566,7 @@ int dvc_pack_targets(const float *fmap2, void *packed, float *workspace, int B, 
         }
         return check_launch("pack_targets");
     }
-    if (hipMemsetAsync(packed, 0, (size_t)B * lay.row_stride * Cp * esz, s) != hipSuccess)
+    if (zero_async(packed, (size_t)B * lay.row_stride * Cp * esz, s) != hipSuccess)
         return fail(DVC_ERR_RUNTIME, "pack_targets: memset failed");
     const float *src = fmap2;
     float *ws = workspace;

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "dvccorr.h"
 
 // DVC_DIAG = 1: the diagnostics library (libdvccorr_diag.so, `make diag`) -- ablation, timeline and store-policy
@@ -156,6 +158,22 @@ __device__ __forceinline__ float tri_sample(const T *lvl, int Hl, int Wl, int Dl
                 acc += StoreT<T>::load(lvl + ((long long)y * Wl + x) * Dpl + z) * w;
             }
     return acc;
+}
+
+// Stream-ordered zero fill of `bytes` (a multiple of 4) by a kernel.  Round 5: a backward captured in a HIP graph
+// (torch.cuda.CUDAGraph) and replayed twice returned garbage d fmap2 from the second replay on -- the zero guard
+// and the cell counts its hipMemsetAsync calls clear were not cleared again (tools/graph_bwd_diag.py) -- so the
+// library's clears are kernels, which every replay runs in stream order.
+template <typename = void>
+__global__ __launch_bounds__(256) void k_zero_dwords(unsigned *__restrict__ p, long long n) {
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) p[i] = 0u;
+}
+inline hipError_t zero_async(void *p, size_t bytes, hipStream_t s) {
+    const long long n = (long long)(bytes / 4);
+    if (n <= 0) return hipSuccess;
+    const long long blocks = std::min<long long>((n + 255) / 256, 8192);
+    k_zero_dwords<><<<(unsigned)blocks, 256, 0, s>>>(reinterpret_cast<unsigned *>(p), n);
+    return hipGetLastError();
 }
 
 }  // namespace dvc

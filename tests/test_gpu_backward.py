@@ -420,3 +420,36 @@ def test_grad_round5_paths_off(knobs, precision, tol):
     finally:
         for k in knobs:
             _lib.set_tuning(k, defaults[k])
+
+
+def test_graph_captured_backward():
+    """dvc_corr_backward captured in a HIP graph (torch.cuda.CUDAGraph over the C ABI; while the stream is being
+    captured the backward keeps every launch on it instead of forking its side stream) and replayed twice, the second
+    time on a new output gradient, gives the eager (side-stream) gradients bit for bit.  (Round 5: with the zero guard
+    and the cell counts cleared by hipMemsetAsync, replays after the first returned garbage d fmap2 -- the clears are
+    kernels now, common.h zero_async.)"""
+    from dvccorr import ops
+    S, C, L, r = 16, 64, 4, 4
+    f1 = torch.from_numpy(prng.normal(950, (1, C, S, S, S))).to(DEV)
+    f2 = torch.from_numpy(prng.normal(951, (1, C, S, S, S))).to(DEV)
+    coords = torch.from_numpy(prng.flow_coords(952, 1, S, S, S, 2.0)).to(DEV).reshape(1, 3, -1)
+    G = torch.from_numpy(prng.normal(953, (1, L * (2 * r + 1) ** 3, S ** 3))).to(DEV)
+    dt = ops.dtype_code("bf16")
+    q = ops.pack_queries(f1.reshape(1, C, -1), dt)
+    t = ops.pack_targets(f2, L, dt)
+    run = lambda g: ops.corr_backward(q, t, coords, g, C, S, S, S, L, r, False, dt)   # noqa: E731
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        run(G)   # warm-up outside capture
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        g1, g2 = run(G)
+    graph.replay()
+    G.copy_(torch.from_numpy(prng.normal(954, tuple(G.shape))).to(DEV))
+    graph.replay()   # (a second replay: the clears of the zero guard and the cell counts must run again)
+    torch.cuda.synchronize()
+    e1, e2 = run(G)
+    torch.cuda.synchronize()
+    assert torch.equal(g1, e1) and torch.equal(g2, e2)
