@@ -749,6 +749,10 @@ constexpr int kQStages = DVC_QSTAGES;   // LDS stages of the batch pipeline (kQS
 #ifndef DVC_QSTAGES16
 #define DVC_QSTAGES16 4
 #endif
+// G16: batches per barrier (1: a barrier per batch; QP > 1 waits for QP batches at once, NST - 2 QP in flight then)
+#ifndef DVC_QPAIR
+#define DVC_QPAIR 1
+#endif
 template <bool SPLIT, bool G16> constexpr int kQNst = G16 && !SPLIT ? DVC_QSTAGES16 : kQStages;
 template <bool SPLIT, bool G16> constexpr int kQStage = SPLIT ? 12288 : G16 ? 6144 : 8192;
 template <bool SPLIT, bool G16> constexpr int kQLds = kQNst<SPLIT, G16> * kQStage<SPLIT, G16> + (G16 && !SPLIT ? 2048 : 0);
@@ -830,6 +834,8 @@ __global__ __launch_bounds__(256, (kQOcc<SPLIT, G16>)) void k_grad_q_mfma(const 
                                                         int ns, int nsl, int lfirst) {
     // bytes per stage: T tile (4 KB, 16-bit) + G tile (4 KB, hi/lo pairs; G16: 2 KB) [+ T lo tile (4 KB)]
     constexpr int STAGE = kQStage<SPLIT, G16>, NST = kQNst<SPLIT, G16>;
+    constexpr int QP = G16 && !SPLIT ? DVC_QPAIR : 1;   // batches per barrier
+    static_assert(NST >= 2 * QP && QP >= 1, "k_grad_q_mfma: NST >= 2 QP stages");
     __shared__ __attribute__((aligned(16))) unsigned char stg[kQLds<SPLIT, G16>];
     __shared__ unsigned qrows[kQRows + 2];           // batches (y | x << 11 | z0 << 22), count, next row
     const int tid = threadIdx.x, lane = tid & 63, m = lane & 31, h = lane >> 5;
@@ -993,17 +999,23 @@ __global__ __launch_bounds__(256, (kQOcc<SPLIT, G16>)) void k_grad_q_mfma(const 
             const int nit = (int)qrows[kQRows];
             rnext = (int)qrows[kQRows + 1];
             if (nit == 0) continue;
-            // batches 0 .. kQStages - 2 in flight (past the end: the last batch again, into a stage never read)
+            // batches 0 .. NST - QP - 1 in flight (past the end: the last batch again, into a stage never read)
 #pragma unroll
-            for (int k = 0; k < NST - 1; ++k) issue(min(k, nit - 1), k);
-            for (int it = 0; it < nit; ++it) {
-                // batch it has landed (this thread's DMAs; kQStages - 2 newer batches may fly), then every thread's
-                // has, and every wave is done with batch it - 1, whose stage the next DMA refills
+            for (int k = 0; k < NST - QP; ++k) issue(min(k, nit - 1), k);
+            for (int it0 = 0; it0 < nit; it0 += QP) {
+                // batches it0 .. it0 + QP - 1 have landed (this thread's DMAs; NST - 2 QP newer batches may fly), then
+                // every thread's have, and every wave is done with the QP batches before, whose stages the next DMAs
+                // refill
                 constexpr int kDma = ((DVC_GQ_ABL & 4) ? 0 : (SPLIT ? 2 : 1)) + ((DVC_GQ_ABL & 2) ? 0 : 1);   // DMAs per batch
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kDma * (NST - 2)) : "memory");
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kDma * (NST - 2 * QP)) : "memory");
                 __builtin_amdgcn_s_barrier();
                 asm volatile("" ::: "memory");
-                issue(min(it + NST - 1, nit - 1), (it + NST - 1) % NST);
+#pragma unroll
+                for (int p = 0; p < QP; ++p) issue(min(it0 + NST - QP + p, nit - 1), (it0 + NST - QP + p) % NST);
+#pragma unroll
+              for (int p = 0; p < QP; ++p) {
+                const int it = it0 + p;
+                if (QP > 1 && it >= nit) break;
                 if (G16 && w < NCT && !(DVC_GQ_ABL & 1)) {
                     const unsigned char *sb = stg + (it % NST) * STAGE;
                     const int r = 32 * w + m, rsw = (r >> 3) & 1;
@@ -1051,6 +1063,7 @@ __global__ __launch_bounds__(256, (kQOcc<SPLIT, G16>)) void k_grad_q_mfma(const 
                         }
                     }
                 }
+              }
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tail's duplicate DMAs have landed
         }
