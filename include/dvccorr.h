@@ -172,7 +172,11 @@ int dvc_corr_lookup_fused(const void *packed_q, const void *packed_t, const floa
  * radius 1..6, any C (the gradient sums run per 128-channel group), Nq a multiple of W*D
  * (DVC_ERR_UNSUPPORTED otherwise);
  * both conventions on every level shape (legacy levels with W != D use a stretched
- * window box).  The workspace size covers either convention. */
+ * window box).  The workspace size covers either convention.  The call may fork part of its
+ * work onto a library-owned high-priority stream (fork / join events, joined before it returns
+ * to the caller's stream) except while the caller's stream is being captured into a HIP graph:
+ * then every launch stays on that stream and the captured graph replays bitwise equal to the
+ * eager call (its workspace clears are kernels, not memset nodes). */
 size_t dvc_corr_backward_workspace_bytes(int B, int64_t Nq, int C, int H, int W, int D, int num_levels, int radius);
 /* The workspace of dvc_corr_backward for one packed dtype: bf16 / fp16 operands need no lo tiles, so
  * their workspace is smaller than the dtype-less query's (~88 MB less at config #3); 0 for a bad dtype.  Either
@@ -184,8 +188,8 @@ int dvc_corr_backward(const void *packed_q, const void *packed_t, const float *c
                       int D, int num_levels, int radius, int convention, int dtype, void *stream);
 /* Pure host function: 1 when dvc_corr_backward runs this shape's gradient sums on the matrix cores
  * (bf16 operands on v_mfma_f32_32x32x16_bf16, fp16 on _f16, fp32 operands split into bf16 hi/lo
- * tiles and multiplied twice, ~2^-16 relative per operand; the window gradients entering as hi/lo
- * pairs), 0 when it takes the VALU kernels (a volume whose MFMA-kernel buffer offsets would exceed
+ * tiles and multiplied twice, ~2^-16 relative per operand; the window gradients enter as one
+ * 16-bit value each for bf16 / fp16 and as bf16 hi/lo pairs for fp32), 0 when it takes the VALU kernels (a volume whose MFMA-kernel buffer offsets would exceed
  * 31 bits: level-0 fmaps of about 154^3 and up).  The answer also follows the CALLING THREAD's
  * dvc_set_tuning("bwd_mfma", v) knob (0: VALU kernels for every dtype).  Same results either way
  * within the dtype's tolerance. */
