@@ -230,13 +230,16 @@ class Runner:
         return None
 
     def compute(self, ev=None, stream=None, slot=0):
-        from dvccorr.sharded import HipRows, assemble_slabs, gather_slabs
+        from dvccorr.sharded import HipRows, gather_slabs
         a = self.args
-        f2 = assemble_slabs(self.bufs[slot], self.H) if self.world > 1 else self.f2_slab
         if ev is not None:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-        rows = HipRows(self.f1_flat, f2, a.levels, a.radius, False, a.precision, a.impl)
+        if self.world > 1:   # the targets packed straight from the all-gather's receive buffer (no assembled fmap2)
+            rows = HipRows(self.f1_flat, None, a.levels, a.radius, False, a.precision, a.impl,
+                           gathered=(self.bufs[slot], self.H))
+        else:
+            rows = HipRows(self.f1_flat, self.f2_slab, a.levels, a.radius, False, a.precision, a.impl)
         if ev is not None:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record(stream)

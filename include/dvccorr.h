@@ -135,6 +135,15 @@ int dvc_pack_queries(const float *fmap1, void *packed, int B, int C, int64_t Nq,
 int dvc_pack_targets(const float *fmap2, void *packed, float *workspace, int B, int C, int H, int W, int D,
                      int num_levels, int dtype, void *stream);
 
+/* dvc_pack_targets straight from an H-slab all-gather's receive buffer (the multi-GPU path,
+ * dvccorr/sharded.py): gathered = world slabs of (B, C, maxh, W, D) float32, maxh = ceil(H / world),
+ * slab r holding fmap2's planes [h0(r), h0(r + 1)) of the balanced split (h0(r) = r (H / world) +
+ * min(r, H % world)) in its first planes.  Same packed output, bit for bit, as dvc_pack_targets of the
+ * assembled fmap2, without assembling it (a copy of fmap2 per forward).  1 <= world <= H; the
+ * single-pass pack only (num_levels <= 4, DVC_ERR_UNSUPPORTED otherwise); no workspace. */
+int dvc_pack_targets_gathered(const float *gathered, int world, void *packed, int B, int C, int H, int W, int D,
+                              int num_levels, int dtype, void *stream);
+
 /* corr[b][q][col] = (sum_c q[b][q][c] * t[b][col][c]) * (1/sqrt(C)) for col in
  * [col_begin, col_end), stored as store_dtype.  in_dtype selects the MFMA path:
  * DVC_BF16 -> v_mfma_f32_32x32x16_bf16, DVC_F32 -> v_mfma_f32_32x32x2_f32.

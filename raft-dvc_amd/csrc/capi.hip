@@ -18,13 +18,6 @@ namespace dvc {
 __global__ void k_pool_fmap(const float *, float *, long long, int, int, int, int, int, int);
 template <typename T>
 __global__ void k_pack_rows(const float *, T *, int, int, long long, long long, int, int, long long, long long);
-struct PyrGeo {
-    int L, C, Cp, H[4], W[4], D[4], Dp[4];
-    long long off[4];
-    long long row_stride;
-    int ncx, ncy, ncz;
-    int brick;   // bit l: level l in (1, 8, 8) bricks (DVC_BRICKED)
-};
 template <typename T, int CG> __global__ void k_pack_pyramid(const float *, T *, PyrGeo);
 template <typename T> __global__ void k_pack_queries(const float *, T *, int, int, long long);
 template <int NCH, bool STORE_F32, int ABL>
@@ -524,6 +517,53 @@ int dvc_pack_queries(const float *fmap1, void *packed, int B, int C, int64_t Nq,
     return check_launch("pack_queries");
 }
 
+// k_pack_pyramid over nslab H-slabs of maxh planes (PyrGeo, common.h); nslab = 1, maxh = H: the plain fmap2
+static int pack_pyramid_launch(const float *src, int nslab, int maxh, void *packed, const dvc_layout &lay, int B, int C,
+                               int H, int W, int D, int num_levels, int dtype, bool bricked, hipStream_t s) {
+    PyrGeo g;
+    memset(&g, 0, sizeof(g));
+    g.L = num_levels; g.C = C; g.Cp = lay.c_pad; g.row_stride = lay.row_stride;
+    for (int l = 0; l < num_levels; ++l) {
+        g.H[l] = lay.H[l]; g.W[l] = lay.W[l]; g.D[l] = lay.D[l]; g.Dp[l] = lay.Dp[l]; g.off[l] = lay.offset[l];
+    }
+    g.ncy = (H + 7) / 8; g.ncx = (W + 7) / 8; g.ncz = (D + 7) / 8;
+    g.brick = bricked ? dvc_bricked_levels(&lay) : 0;
+    g.B = B; g.nslab = nslab; g.maxh = maxh; g.sbase = H / nslab; g.srem = H % nslab;
+    const int Cp = lay.c_pad;
+    const long long ncells = (long long)g.ncy * g.ncx * g.ncz;
+    const bool cg32 = ncells * ceil_div(Cp, 32) * B >= 2048;   // 32 channels per workgroup on big volumes
+    dim3 grid((unsigned)(8 * ceil_div(ncells, 8)), (unsigned)ceil_div(Cp, cg32 ? 32 : 16), (unsigned)B);
+    if (dtype == DVC_BF16) {
+        if (cg32) k_pack_pyramid<bf16_t, 32><<<grid, 256, 0, s>>>(src, (bf16_t *)packed, g);
+        else k_pack_pyramid<bf16_t, 16><<<grid, 256, 0, s>>>(src, (bf16_t *)packed, g);
+    } else if (dtype == DVC_F16) {
+        if (cg32) k_pack_pyramid<f16_t, 32><<<grid, 256, 0, s>>>(src, (f16_t *)packed, g);
+        else k_pack_pyramid<f16_t, 16><<<grid, 256, 0, s>>>(src, (f16_t *)packed, g);
+    } else {
+        if (cg32) k_pack_pyramid<float, 32><<<grid, 256, 0, s>>>(src, (float *)packed, g);
+        else k_pack_pyramid<float, 16><<<grid, 256, 0, s>>>(src, (float *)packed, g);
+    }
+    return check_launch("pack_targets");
+}
+
+int dvc_pack_targets_gathered(const float *gathered, int world, void *packed, int B, int C, int H, int W, int D,
+                              int num_levels, int dtype, void *stream) {
+    dvc_layout lay;
+    int rc = dvc_layout_init(H, W, D, num_levels, C, &lay);
+    if (rc) return rc;
+    const bool bricked = (dtype & DVC_BRICKED) != 0;
+    dtype &= ~DVC_BRICKED;
+    if (!gathered || !packed) return fail(DVC_ERR_INVALID, "pack_targets_gathered: null pointer");
+    if (B < 1 || world < 1 || world > H)
+        return fail(DVC_ERR_INVALID, "pack_targets_gathered: B=%d world=%d H=%d", B, world, H);
+    if (dtype != DVC_BF16 && dtype != DVC_F32 && dtype != DVC_F16)
+        return fail(DVC_ERR_INVALID, "pack_targets_gathered: bad dtype %d", dtype);
+    if (num_levels > 4 || g_pack_variant != 1)
+        return fail(DVC_ERR_UNSUPPORTED, "pack_targets_gathered: needs the single-pass pack (num_levels <= 4)");
+    return pack_pyramid_launch(gathered, world, (H + world - 1) / world, packed, lay, B, C, H, W, D, num_levels, dtype,
+                               bricked, (hipStream_t)stream);
+}
+
 int dvc_pack_targets(const float *fmap2, void *packed, float *workspace, int B, int C, int H, int W, int D,
                      int num_levels, int dtype, void *stream) {
     dvc_layout lay;
@@ -541,31 +581,9 @@ int dvc_pack_targets(const float *fmap2, void *packed, float *workspace, int B, 
     hipStream_t s = (hipStream_t)stream;
     const int Cp = lay.c_pad;
     const size_t esz = dtype == DVC_F32 ? 4 : 2;
-    if (num_levels <= 4 && g_pack_variant == 1) {   // one pass: every level of an 8^3 cell pooled in LDS (k_pack_pyramid,
-                                                     // which also zeroes the z-padding and tail rows)
-        PyrGeo g;
-        memset(&g, 0, sizeof(g));
-        g.L = num_levels; g.C = C; g.Cp = Cp; g.row_stride = lay.row_stride;
-        for (int l = 0; l < num_levels; ++l) {
-            g.H[l] = lay.H[l]; g.W[l] = lay.W[l]; g.D[l] = lay.D[l]; g.Dp[l] = lay.Dp[l]; g.off[l] = lay.offset[l];
-        }
-        g.ncy = (H + 7) / 8; g.ncx = (W + 7) / 8; g.ncz = (D + 7) / 8;
-        g.brick = bricked ? dvc_bricked_levels(&lay) : 0;
-        const long long ncells = (long long)g.ncy * g.ncx * g.ncz;
-        const bool cg32 = ncells * ceil_div(Cp, 32) * B >= 2048;   // 32 channels per workgroup on big volumes
-        dim3 grid((unsigned)(8 * ceil_div(ncells, 8)), (unsigned)ceil_div(Cp, cg32 ? 32 : 16), (unsigned)B);
-        if (dtype == DVC_BF16) {
-            if (cg32) k_pack_pyramid<bf16_t, 32><<<grid, 256, 0, s>>>(fmap2, (bf16_t *)packed, g);
-            else k_pack_pyramid<bf16_t, 16><<<grid, 256, 0, s>>>(fmap2, (bf16_t *)packed, g);
-        } else if (dtype == DVC_F16) {
-            if (cg32) k_pack_pyramid<f16_t, 32><<<grid, 256, 0, s>>>(fmap2, (f16_t *)packed, g);
-            else k_pack_pyramid<f16_t, 16><<<grid, 256, 0, s>>>(fmap2, (f16_t *)packed, g);
-        } else {
-            if (cg32) k_pack_pyramid<float, 32><<<grid, 256, 0, s>>>(fmap2, (float *)packed, g);
-            else k_pack_pyramid<float, 16><<<grid, 256, 0, s>>>(fmap2, (float *)packed, g);
-        }
-        return check_launch("pack_targets");
-    }
+    if (num_levels <= 4 && g_pack_variant == 1)   // one pass: every level of an 8^3 cell pooled in LDS (k_pack_pyramid,
+                                                   // which also zeroes the z-padding and tail rows)
+        return pack_pyramid_launch(fmap2, 1, H, packed, lay, B, C, H, W, D, num_levels, dtype, bricked, s);
     if (zero_async(packed, (size_t)B * lay.row_stride * Cp * esz, s) != hipSuccess)
         return fail(DVC_ERR_RUNTIME, "pack_targets: memset failed");
     const float *src = fmap2;

@@ -160,6 +160,19 @@ __device__ __forceinline__ float tri_sample(const T *lvl, int Hl, int Wl, int Dl
     return acc;
 }
 
+// Geometry of k_pack_pyramid (pack.hip): every packed target level of fmap2 in one pass.  The source is nslab
+// H-slabs of (B, C, maxh, W, D) float32, slab r holding planes [h0(r), h0(r + 1)) of the balanced split
+// h0(r) = r sbase + min(r, srem) (dvccorr/sharded.py slab_bounds) zero-padded to maxh planes: an all-gather's receive
+// buffer as it lands.  One slab (nslab = 1, maxh = H) is the plain (B, C, H, W, D) tensor.
+struct PyrGeo {
+    int L, C, Cp, H[4], W[4], D[4], Dp[4];
+    long long off[4];
+    long long row_stride;
+    int ncx, ncy, ncz;   // cells per axis (level 0, ceil)
+    int brick;           // bit l: level l in (1, 8, 8) bricks (DVC_BRICKED, include/dvccorr.h)
+    int B, nslab, maxh, sbase, srem;
+};
+
 // Stream-ordered zero fill of `bytes` (a multiple of 4) by a kernel.  Round 5: a backward captured in a HIP graph
 // (torch.cuda.CUDAGraph) and replayed twice returned garbage d fmap2 from the second replay on -- the zero guard
 // and the cell counts its hipMemsetAsync calls clear were not cleared again (tools/graph_bwd_diag.py) -- so the

@@ -108,13 +108,7 @@ __global__ __launch_bounds__(256) void k_pack_rows(const float *__restrict__ src
 // children exist.  Padding rows (z >= D_l, row tail) are the caller's memset.
 constexpr int kPyrE = 8;   // cell edge
 
-struct PyrGeo {
-    int L, C, Cp, H[4], W[4], D[4], Dp[4];
-    long long off[4];
-    long long row_stride;
-    int ncx, ncy, ncz;   // cells per axis (level 0, ceil)
-    int brick;           // bit l: level l in (1, 8, 8) bricks (DVC_BRICKED, include/dvccorr.h)
-};
+// (PyrGeo: common.h)
 
 // Packed-target row of level-l voxel (Y, X, Z): linear (Y W + X) Dp + Z, or its (1, 8, 8) brick slot.
 __device__ __forceinline__ long long pyr_row(const PyrGeo &g, int l, int Y, int X, int Z) {
@@ -148,8 +142,8 @@ __global__ __launch_bounds__(256) void k_pack_pyramid(const float *__restrict__ 
     const int cx = cell % g.ncx;
     const int cy = cell / g.ncx;
     const int y0 = cy * kPyrE, x0 = cx * kPyrE, z0 = cz * kPyrE;
-    const long long npos = (long long)g.H[0] * g.W[0] * g.D[0];
-    const float *sb = src + (long long)b * g.C * npos;
+    // one slab's plane block of one (batch element, channel); the plain tensor is one slab of H planes
+    const long long slab = (long long)g.maxh * g.W[0] * g.D[0];
     // load: 4-voxel z-runs; idx -> (channel k, run v4 = (dy, dx, dz / 4)), every load issued before the
     // LDS writes (16-byte loads when D % 4 == 0: the runs are then 16-byte aligned)
     constexpr int NLD = kPyrCG * 128 / 256;
@@ -162,7 +156,14 @@ __global__ __launch_bounds__(256) void k_pack_pyramid(const float *__restrict__ 
         const int dz = v & 7, dx = (v >> 3) & 7, dy = v >> 6;
         const int c = cg * kPyrCG + k, y = y0 + dy, x = x0 + dx, z = z0 + dz;
         const bool in = c < g.C && y < g.H[0] && x < g.W[0];
-        const float *p = sb + (long long)c * npos + ((long long)y * g.W[0] + x) * g.D[0] + z;
+        // the slab holding plane y (balanced split: the first srem slabs hold sbase + 1 planes)
+        int sr = 0, sy = y;
+        if (g.nslab > 1) {
+            const int big = g.srem * (g.sbase + 1);
+            sr = y < big ? y / (g.sbase + 1) : g.srem + (y - big) / g.sbase;
+            sy = y - (sr * g.sbase + min(sr, g.srem));
+        }
+        const float *p = src + (((long long)sr * g.B + b) * g.C + c) * slab + ((long long)sy * g.W[0] + x) * g.D[0] + z;
         float4 r = float4{0.f, 0.f, 0.f, 0.f};
         if (in && vec && z + 3 < g.D[0]) {
             r = *reinterpret_cast<const float4 *>(p);

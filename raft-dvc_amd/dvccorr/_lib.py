@@ -22,7 +22,8 @@ MAX_LEVELS = 8
 
 # Every symbol include/dvccorr.h declares (checked by tests/test_capi_cpu.py).
 EXPORTED = (
-    "dvc_layout_init", "dvc_pack_workspace_bytes", "dvc_pack_queries", "dvc_pack_targets", "dvc_corr_build",
+    "dvc_layout_init", "dvc_pack_workspace_bytes", "dvc_pack_queries", "dvc_pack_targets", "dvc_pack_targets_gathered",
+    "dvc_corr_build",
     "dvc_corr_pool", "dvc_corr_lookup", "dvc_lookup_fused_workspace_bytes", "dvc_corr_lookup_fused",
     "dvc_sample3d", "dvc_set_tuning", "dvc_last_error", "dvc_version", "dvc_abi_version",
     "dvc_corr_backward_workspace_bytes", "dvc_corr_backward_workspace_bytes_dtype", "dvc_corr_backward",
@@ -77,6 +78,7 @@ def lib() -> ctypes.CDLL:
         "dvc_pack_workspace_bytes": (sz, [i32, i32, i32, i32, i32, i32]),
         "dvc_pack_queries": (i32, [vp, vp, i32, i32, i64, i32, vp]),
         "dvc_pack_targets": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp]),
+        "dvc_pack_targets_gathered": (i32, [vp, i32, vp, i32, i32, i32, i32, i32, i32, i32, vp]),
         "dvc_corr_build": (i32, [vp, vp, vp, i32, i64, i32, i32, i32, i32, i32, i32, i32, i64, i64, vp]),
         "dvc_corr_pool": (i32, [vp, i32, i64, i32, i32, i32, i32, i32, i32, vp]),
         "dvc_corr_lookup": (i32, [vp, vp, vp, i32, i64, i32, i32, i32, i32, i32, i32, i32, vp]),

@@ -104,6 +104,23 @@ def pack_targets(fmap2: torch.Tensor, num_levels: int, dtype: int, out: torch.Te
     return _mark(out, dtype)
 
 
+def pack_targets_gathered(gathered: torch.Tensor, H: int, num_levels: int, dtype: int) -> torch.Tensor:
+    """pack_targets of the fmap2 an H-slab all-gather delivers, read from its receive buffer
+    gathered (world, B, C, ceil(H / world), W, D) without assembling fmap2 (dvc_pack_targets_gathered;
+    sharded.all_gather_slab's buffer, slab r = slab_bounds(H, world, r), zero-padded)."""
+    _need_cuda(gathered)
+    if gathered.dtype != torch.float32 or not gathered.is_contiguous() or gathered.dim() != 6:
+        raise ValueError("pack_targets_gathered: expected a contiguous float32 (world, B, C, maxh, W, D) buffer")
+    world, B, C, maxh, W, D = gathered.shape
+    if maxh != -(-H // world):
+        raise ValueError(f"pack_targets_gathered: slab height {maxh} != ceil({H} / {world})")
+    lay = layout(H, W, D, num_levels, C)
+    out = torch.empty((B, lay.row_stride, lay.c_pad), dtype=_TORCH_DT[dtype], device=gathered.device)
+    check(lib().dvc_pack_targets_gathered(_ptr(gathered), world, _ptr(out), B, C, H, W, D, num_levels, dtype,
+                                          _stream(gathered)), "pack_targets_gathered")
+    return _mark(out, dtype)
+
+
 GUARD_BYTES = 256   # DVC_CORR_GUARD_BYTES
 
 
@@ -334,7 +351,7 @@ def flow_step(coords1: torch.Tensor, delta_flow, target_shape):
     return new, up
 
 
-__all__ = ["pack_queries", "pack_targets", "build", "pool", "lookup", "lookup_fused", "lookup_fused_proj", "corr_backward", "sample3d",
+__all__ = ["pack_queries", "pack_targets", "pack_targets_gathered", "build", "pool", "lookup", "lookup_fused", "lookup_fused_proj", "corr_backward", "sample3d",
            "proj_pack", "proj_pack_cached", "lookup_proj",
            "coords_grid", "upflow", "flow_step",
            "fused_workspace", "dtype_code", "layout", "bricked_levels", "DVC_BRICKED", "_lib"]

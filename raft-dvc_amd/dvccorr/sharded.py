@@ -108,9 +108,17 @@ def gather_slabs(slab: torch.Tensor, H: int, group=None, dim: int = 2) -> torch.
 class HipRows:
     """Default backend: this rank's query rows against the full target pyramid on the GPU."""
 
-    def __init__(self, q_flat: torch.Tensor, fmap2: torch.Tensor, num_levels: int, radius: int, legacy: bool,
-                 precision: str, impl: str, q_offset: int = 0):
-        B, C, H, W, D = fmap2.shape
+    def __init__(self, q_flat: torch.Tensor, fmap2: Optional[torch.Tensor], num_levels: int, radius: int, legacy: bool,
+                 precision: str, impl: str, q_offset: int = 0, gathered=None):
+        # gathered = (all_gather_slab's receive buffer, H): the targets are packed straight from the slabs
+        # (dvc_pack_targets_gathered) instead of from an assembled copy of fmap2; fmap2 is then unused
+        if gathered is not None and num_levels > 4:    # (the gathered pack is the single-pass one)
+            fmap2, gathered = assemble_slabs(*gathered), None
+        if gathered is not None:
+            _, B, C, _, W, D = gathered[0].shape
+            H = gathered[1]
+        else:
+            B, C, H, W, D = fmap2.shape
         self.dims = (C, H, W, D)
         self.L, self.R, self.legacy, self.impl = num_levels, radius, legacy, impl
         self.dt = ops.dtype_code(precision)
@@ -119,7 +127,10 @@ class HipRows:
         lay = layout(H, W, D, num_levels, C)
         self.ldt = self.dt | (brick_flag(lay, radius, legacy, True) if impl == "materialised" else 0)
         self.q = ops.pack_queries(q_flat, self.dt)
-        self.t = ops.pack_targets(fmap2, num_levels, self.ldt)
+        if gathered is not None:
+            self.t = ops.pack_targets_gathered(gathered[0], H, num_levels, self.ldt)
+        else:
+            self.t = ops.pack_targets(fmap2, num_levels, self.ldt)
         if impl == "materialised":
             self.corr = ops.build(self.q, self.t, C, H, W, D, num_levels, self.dt, self.dt)
         elif impl == "fused":
@@ -196,9 +207,16 @@ class ShardedCorrBlock:
         if build_events is not None and stream is not None:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-        fmap2 = gather_slabs(fmap2_slab, H, group)           # the one data-path collective per forward
-        self.rows = backend(fmap1_slab.reshape(B, C, Hs * W * D), fmap2, num_levels, radius, legacy_wd_swap,
-                            precision, impl, q_offset=h0 * W * D)
+        q_flat = fmap1_slab.reshape(B, C, Hs * W * D)
+        if backend is HipRows and self.world > 1 and fmap2_slab.is_cuda:
+            # the one data-path collective per forward; the targets are packed from its receive buffer
+            buf = all_gather_slab(fmap2_slab.float(), H, group)
+            self.rows = HipRows(q_flat, None, num_levels, radius, legacy_wd_swap, precision, impl, q_offset=h0 * W * D,
+                                gathered=(buf, H))
+        else:
+            fmap2 = gather_slabs(fmap2_slab, H, group)       # the one data-path collective per forward
+            self.rows = backend(q_flat, fmap2, num_levels, radius, legacy_wd_swap, precision, impl,
+                                q_offset=h0 * W * D)
         if build_events is not None and stream is not None:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record(stream)

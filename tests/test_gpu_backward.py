@@ -453,3 +453,37 @@ def test_graph_captured_backward():
     e1, e2 = run(G)
     torch.cuda.synchronize()
     assert torch.equal(g1, e1) and torch.equal(g2, e2)
+
+
+@pytest.mark.gpu
+def test_graph_captured_backward_poisoned_workspace():
+    """A caller-owned workspace filled with NaN before the capture and again between replays: every replay clears
+    what it needs (the zero guard, the cell counts) itself, so the replayed gradients equal the eager ones bit for
+    bit and the guard reads zero after each replay (tools/graph_bwd_diag.py's check, round 5)."""
+    from dvccorr import ops
+    from dvccorr.ops import _ptr, _stream, lib
+    S, C, L, r = 16, 64, 4, 4
+    B, Nq = 1, S ** 3
+    f1 = torch.from_numpy(prng.normal(960, (1, C, S, S, S))).to(DEV)
+    f2 = torch.from_numpy(prng.normal(961, (1, C, S, S, S))).to(DEV)
+    coords = torch.from_numpy(prng.flow_coords(962, 1, S, S, S, 2.0)).to(DEV).reshape(1, 3, -1).contiguous()
+    G = torch.from_numpy(prng.normal(963, (1, L * (2 * r + 1) ** 3, Nq))).to(DEV).contiguous()
+    dt = ops.dtype_code("bf16")
+    q = ops.pack_queries(f1.reshape(1, C, -1), dt)
+    t = ops.pack_targets(f2, L, dt)
+    nws = lib().dvc_corr_backward_workspace_bytes_dtype(B, Nq, C, S, S, S, L, r, dt)
+    ws = torch.full((nws // 4 + 64,), float("nan"), device=DEV)
+    d1 = torch.empty((B, C, Nq), device=DEV)
+    d2 = torch.empty((B, C, S, S, S), device=DEV)
+    e1, e2 = ops.corr_backward(q, t, coords, G, C, S, S, S, L, r, False, dt)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=torch.cuda.Stream()):
+        ops.check(lib().dvc_corr_backward(_ptr(q), _ptr(t), _ptr(coords), _ptr(G), _ptr(d1), _ptr(d2), _ptr(ws), B,
+                                          Nq, C, S, S, S, L, r, 0, dt, _stream(q)), "corr_backward")
+    for _ in range(2):
+        ws.fill_(float("nan"))
+        graph.replay()
+        torch.cuda.synchronize()
+        assert bool((ws[:64] == 0).all())
+        assert torch.equal(d1, e1) and torch.equal(d2, e2)

@@ -340,3 +340,52 @@ def test_single_pass_pack_matches_per_level(shape, C, L):
             _lib.set_tuning("pack_variant", 1)
         torch.cuda.synchronize()
         assert torch.equal(new, old), (shape, C, L, prec)
+
+
+@pytest.mark.parametrize("shape,C,L,world", [((32, 32, 32), 128, 4, 8), ((32, 32, 32), 128, 4, 1),
+                                             ((33, 20, 17), 40, 4, 5), ((16, 16, 16), 64, 3, 3),
+                                             ((9, 7, 8), 16, 2, 9), ((64, 24, 40), 256, 4, 7)])
+def test_pack_targets_gathered_matches_assembled(shape, C, L, world):
+    """dvc_pack_targets_gathered (the targets packed straight from an H-slab all-gather's receive buffer, the
+    multi-GPU forward) writes exactly the bytes of dvc_pack_targets on the assembled fmap2: balanced splits with
+    and without a remainder (padded slabs), one plane per rank, B = 2, every dtype, bricked levels."""
+    from dvccorr import ops
+    from dvccorr.sharded import assemble_slabs, slab_bounds
+    from dvccorr.corr_block import brick_flag
+    H, W, D = shape
+    g = torch.Generator(device="cpu").manual_seed(H * W + D + C + L + world)
+    f2 = torch.randn(2, C, H, W, D, generator=g).to(DEV)
+    maxh = -(-H // world)
+    buf = torch.full((world, 2, C, maxh, W, D), float("nan"), device=DEV)   # pad planes must never be read
+    for r in range(world):
+        h0, h1 = slab_bounds(H, world, r)
+        buf[r, :, :, :h1 - h0] = f2[:, :, h0:h1]
+    assert torch.equal(assemble_slabs(torch.nan_to_num(buf), H), f2)
+    lay = ops.layout(H, W, D, L, C)
+    for prec in ("bf16", "fp16", "fp32"):
+        for brick in (0, brick_flag(lay, 4, False, True)):
+            dt = ops.dtype_code(prec) | brick
+            got = ops.pack_targets_gathered(buf, H, L, dt)
+            ref = ops.pack_targets(f2, L, dt)
+            torch.cuda.synchronize()
+            assert torch.equal(got, ref), (shape, C, L, world, prec, brick)
+
+
+def test_hiprows_gathered_lookup_matches():
+    """One rank's HipRows built from the all-gather buffer (gathered=) looks up the same values, bit for bit, as
+    HipRows on the assembled fmap2 (config #3's 8-way slab, bf16)."""
+    from dvccorr.sharded import HipRows, slab_bounds
+    S, C, L, r, world, rank = 32, 128, 4, 4, 8, 3
+    f1, f2, c = _inputs(77, C, S)
+    h0, h1 = slab_bounds(S, world, rank)
+    buf = torch.zeros((world, 1, C, -(-S // world), S, S), device=DEV)
+    for k in range(world):
+        a, b = slab_bounds(S, world, k)
+        buf[k, :, :, :b - a] = f2[:, :, a:b]
+    q = f1[:, :, h0:h1].reshape(1, C, -1).contiguous()
+    cs = c[:, :, h0:h1].reshape(1, 3, -1).contiguous()
+    with torch.no_grad():
+        ref = HipRows(q, f2, L, r, False, "bf16", "materialised", q_offset=h0 * S * S).lookup(cs)
+        got = HipRows(q, None, L, r, False, "bf16", "materialised", q_offset=h0 * S * S, gathered=(buf, S)).lookup(cs)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
