@@ -95,6 +95,19 @@ def test_validation_errors_without_gpu():
     assert L.dvc_lookup_fused_workspace_bytes(1, 100000, 2, 4) == 65536 * 10 * 10 * 12 * 4
 
 
+def test_pack_targets_gathered_validation_without_gpu():
+    """dvc_pack_targets_gathered's host checks (before any HIP call): null pointers, world outside [1, H] and a bad
+    dtype are invalid; more than four levels (the single-pass pack only) is unsupported."""
+    from dvccorr import _lib
+    L = _lib.lib()
+    p = ctypes.c_void_p(16)
+    assert L.dvc_pack_targets_gathered(None, 2, p, 1, 16, 32, 32, 32, 4, _lib.DVC_BF16, None) == _lib.DVC_ERR_INVALID
+    assert L.dvc_pack_targets_gathered(p, 0, p, 1, 16, 32, 32, 32, 4, _lib.DVC_BF16, None) == _lib.DVC_ERR_INVALID
+    assert L.dvc_pack_targets_gathered(p, 33, p, 1, 16, 32, 32, 32, 4, _lib.DVC_BF16, None) == _lib.DVC_ERR_INVALID
+    assert L.dvc_pack_targets_gathered(p, 2, p, 1, 16, 32, 32, 32, 4, 7, None) == _lib.DVC_ERR_INVALID
+    assert L.dvc_pack_targets_gathered(p, 2, p, 1, 16, 64, 64, 64, 5, _lib.DVC_BF16, None) == _lib.DVC_ERR_UNSUPPORTED
+
+
 def test_product_path_refuses_cpu_tensors():
     import dvccorr
     f = torch.randn(1, 16, 8, 8, 8)
