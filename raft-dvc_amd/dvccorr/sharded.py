@@ -126,6 +126,8 @@ class HipRows:
         from .corr_block import brick_flag
         lay = layout(H, W, D, num_levels, C)
         self.ldt = self.dt | (brick_flag(lay, radius, legacy, True) if impl == "materialised" else 0)
+        # (one stream: the query pack on a forked side stream beside the target pack was slower, 0.394-0.396 vs
+        # 0.373-0.375 ms per 8-way slab step, profiles/r05/r05_ab_pack_side.txt)
         self.q = ops.pack_queries(q_flat, self.dt)
         if gathered is not None:
             self.t = ops.pack_targets_gathered(gathered[0], H, num_levels, self.ldt)
@@ -134,7 +136,7 @@ class HipRows:
         if impl == "materialised":
             self.corr = ops.build(self.q, self.t, C, H, W, D, num_levels, self.dt, self.dt)
         elif impl == "fused":
-            self.ws = ops.fused_workspace(B, q_flat.shape[2], num_levels, radius, fmap2.device)
+            self.ws = ops.fused_workspace(B, q_flat.shape[2], num_levels, radius, q_flat.device)
         else:
             raise ValueError(f"impl must be 'materialised' or 'fused', got {impl!r}")
 
