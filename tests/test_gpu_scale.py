@@ -371,9 +371,10 @@ def test_pack_targets_gathered_matches_assembled(shape, C, L, world):
             assert torch.equal(got, ref), (shape, C, L, world, prec, brick)
 
 
-def test_hiprows_gathered_lookup_matches():
+@pytest.mark.parametrize("impl", ["materialised", "fused"])
+def test_hiprows_gathered_lookup_matches(impl):
     """One rank's HipRows built from the all-gather buffer (gathered=) looks up the same values, bit for bit, as
-    HipRows on the assembled fmap2 (config #3's 8-way slab, bf16)."""
+    HipRows on the assembled fmap2 (config #3's 8-way slab, bf16), materialised and on the fly."""
     from dvccorr.sharded import HipRows, slab_bounds
     S, C, L, r, world, rank = 32, 128, 4, 4, 8, 3
     f1, f2, c = _inputs(77, C, S)
@@ -385,7 +386,7 @@ def test_hiprows_gathered_lookup_matches():
     q = f1[:, :, h0:h1].reshape(1, C, -1).contiguous()
     cs = c[:, :, h0:h1].reshape(1, 3, -1).contiguous()
     with torch.no_grad():
-        ref = HipRows(q, f2, L, r, False, "bf16", "materialised", q_offset=h0 * S * S).lookup(cs)
-        got = HipRows(q, None, L, r, False, "bf16", "materialised", q_offset=h0 * S * S, gathered=(buf, S)).lookup(cs)
+        ref = HipRows(q, f2, L, r, False, "bf16", impl, q_offset=h0 * S * S).lookup(cs)
+        got = HipRows(q, None, L, r, False, "bf16", impl, q_offset=h0 * S * S, gathered=(buf, S)).lookup(cs)
     torch.cuda.synchronize()
     assert torch.equal(got, ref)
