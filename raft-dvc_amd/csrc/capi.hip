@@ -100,6 +100,7 @@ static thread_local int g_upflow_wgs = 1 << 30;   // k_upflow grid cap (workgrou
                                                   // workgroup per item, 178 -> 152 us at the #5 tail (tools/ab_upflow.py)
 static thread_local int g_upflow_staged = 1;      // 1 = k_upflow stages an item's low-res box in LDS (all ratios <= 1)
 static thread_local int g_pack_variant = 1;       // 1 = single-pass k_pack_pyramid where L <= 4, 0 = per-level launches
+static thread_local int g_pack_cg = 0;           // k_pack_pyramid channels per workgroup: 0 = by size (16 / 32), else 8 / 16 / 32
 static thread_local int g_fused_ablate = 0;
        // diagnostics only: 1 = skip output stores, 2 = skip window dots (cube kernel)
 
@@ -345,6 +346,11 @@ int dvc_set_tuning(const char *key, int value) {
         g_build_stpol = value != 0;
         return DVC_OK;
     }
+    if (!strcmp(key, "pack_cg")) {
+        if (value != 0 && value != 8 && value != 16 && value != 32) return fail(DVC_ERR_INVALID, "set_tuning: pack_cg %d", value);
+        g_pack_cg = value;
+        return DVC_OK;
+    }
     if (!strcmp(key, "pack_variant")) {
         if (value < 0 || value > 1) return fail(DVC_ERR_INVALID, "set_tuning: pack_variant %d", value);
         g_pack_variant = value;
@@ -531,18 +537,18 @@ static int pack_pyramid_launch(const float *src, int nslab, int maxh, void *pack
     g.B = B; g.nslab = nslab; g.maxh = maxh; g.sbase = H / nslab; g.srem = H % nslab;
     const int Cp = lay.c_pad;
     const long long ncells = (long long)g.ncy * g.ncx * g.ncz;
-    const bool cg32 = ncells * ceil_div(Cp, 32) * B >= 2048;   // 32 channels per workgroup on big volumes
-    dim3 grid((unsigned)(8 * ceil_div(ncells, 8)), (unsigned)ceil_div(Cp, cg32 ? 32 : 16), (unsigned)B);
-    if (dtype == DVC_BF16) {
-        if (cg32) k_pack_pyramid<bf16_t, 32><<<grid, 256, 0, s>>>(src, (bf16_t *)packed, g);
-        else k_pack_pyramid<bf16_t, 16><<<grid, 256, 0, s>>>(src, (bf16_t *)packed, g);
-    } else if (dtype == DVC_F16) {
-        if (cg32) k_pack_pyramid<f16_t, 32><<<grid, 256, 0, s>>>(src, (f16_t *)packed, g);
-        else k_pack_pyramid<f16_t, 16><<<grid, 256, 0, s>>>(src, (f16_t *)packed, g);
-    } else {
-        if (cg32) k_pack_pyramid<float, 32><<<grid, 256, 0, s>>>(src, (float *)packed, g);
-        else k_pack_pyramid<float, 16><<<grid, 256, 0, s>>>(src, (float *)packed, g);
-    }
+    // 32 channels per workgroup on big volumes, else 16 (tuning "pack_cg" forces 8 / 16 / 32)
+    const int cg = g_pack_cg ? g_pack_cg : ncells * ceil_div(Cp, 32) * B >= 2048 ? 32 : 16;
+    dim3 grid((unsigned)(8 * ceil_div(ncells, 8)), (unsigned)ceil_div(Cp, cg), (unsigned)B);
+    auto launch = [&](auto *dst) {
+        using T = std::remove_pointer_t<decltype(dst)>;
+        if (cg == 32) k_pack_pyramid<T, 32><<<grid, 256, 0, s>>>(src, dst, g);
+        else if (cg == 16) k_pack_pyramid<T, 16><<<grid, 256, 0, s>>>(src, dst, g);
+        else k_pack_pyramid<T, 8><<<grid, 256, 0, s>>>(src, dst, g);
+    };
+    if (dtype == DVC_BF16) launch((bf16_t *)packed);
+    else if (dtype == DVC_F16) launch((f16_t *)packed);
+    else launch((float *)packed);
     return check_launch("pack_targets");
 }
 

@@ -331,6 +331,9 @@ template __global__ void k_pack_pyramid<float, 32>(const float *, float *, PyrGe
 template __global__ void k_pack_pyramid<bf16_t, 32>(const float *, bf16_t *, PyrGeo);
 template __global__ void k_pack_pyramid<f16_t, 16>(const float *, f16_t *, PyrGeo);
 template __global__ void k_pack_pyramid<f16_t, 32>(const float *, f16_t *, PyrGeo);
+template __global__ void k_pack_pyramid<float, 8>(const float *, float *, PyrGeo);
+template __global__ void k_pack_pyramid<bf16_t, 8>(const float *, bf16_t *, PyrGeo);
+template __global__ void k_pack_pyramid<f16_t, 8>(const float *, f16_t *, PyrGeo);
 
 template __global__ void k_pack_rows<float>(const float *, float *, int, int, long long, long long, int, int,
                                             long long, long long);

@@ -330,16 +330,21 @@ def test_single_pass_pack_matches_per_level(shape, C, L):
     lay = ops.layout(H, W, D, L, C)
     for prec in ("bf16", "fp32"):
         dt = ops.dtype_code(prec)
-        # every row (voxels, z padding, the tail up to row_stride) must be written: start from NaN
-        new = torch.full((2, lay.row_stride, lay.c_pad), float("nan"), dtype=ops._TORCH_DT[dt], device=DEV)
-        ops.pack_targets(f2, L, dt, out=new)
         try:
             _lib.set_tuning("pack_variant", 0)
             old = ops.pack_targets(f2, L, dt)
         finally:
             _lib.set_tuning("pack_variant", 1)
-        torch.cuda.synchronize()
-        assert torch.equal(new, old), (shape, C, L, prec)
+        for cg in (0, 8, 16, 32):   # channels per workgroup: by size (0), or forced (tuning "pack_cg")
+            # every row (voxels, z padding, the tail up to row_stride) must be written: start from NaN
+            new = torch.full((2, lay.row_stride, lay.c_pad), float("nan"), dtype=ops._TORCH_DT[dt], device=DEV)
+            try:
+                _lib.set_tuning("pack_cg", cg)
+                ops.pack_targets(f2, L, dt, out=new)
+            finally:
+                _lib.set_tuning("pack_cg", 0)
+            torch.cuda.synchronize()
+            assert torch.equal(new, old), (shape, C, L, prec, cg)
 
 
 @pytest.mark.parametrize("shape,C,L,world", [((32, 32, 32), 128, 4, 8), ((32, 32, 32), 128, 4, 1),
