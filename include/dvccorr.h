@@ -59,7 +59,9 @@ extern "C" {
 #define DVC_MAX_LEVELS 8
 /* 2 (round 4): c_pad rounds to 32 / 64 / 128 then multiples of 128 (was ceil32), DVC_F16, and
  * dvc_corr_backward_mfma */
-#define DVC_ABI_VERSION 2
+/* 3 (round 6): dvc_corr_lookup_proj on a DVC_F32 pyramid reads dvc_proj_pack_exact's hi + lo weight blocks
+ * (2 x dvc_proj_packed_bytes; under version 2 an fp32 pyramid took dvc_proj_pack's single fp16 block) */
+#define DVC_ABI_VERSION 3
 /* The corr pyramid buffer must be allocated with DVC_CORR_GUARD_BYTES of extra
  * space before its first row and after its last row.  dvc_corr_build zeroes
  * them; dvc_corr_lookup's walk kernels load each window run from a clamped
@@ -223,7 +225,9 @@ int dvc_corr_backward_gout64(int64_t Nq, int radius);
  *     against the float32 reference).  DVC_F32 pyramids (dvc_proj_pack_exact weights, round 5):
  *     both operands split into bf16 hi + lo, three MFMAs per step (x_hi w_hi + x_lo w_hi +
  *     x_hi w_lo, float32 accumulation): the fp32 tolerance 1e-5 (the reference's fp32
- *     evaluation, evaluate_phase1.py:115-131).  Supported: radius 1..4, tile-kernel row widths,
+ *     evaluation, evaluate_phase1.py:115-131).  A DVC_F32 call reads 2 x dvc_proj_packed_bytes
+ *     of packed_w: passing dvc_proj_pack's single block there reads past it (ABI 3; the
+ *     Python wrapper refuses a short buffer).  Supported: radius 1..4, tile-kernel row widths,
  *     and for the legacy convention W == D at every non-zero level (DVC_ERR_UNSUPPORTED otherwise). */
 #define DVC_PROJ_COUT 96
 #define DVC_PROJ_MAX_RADIUS 4

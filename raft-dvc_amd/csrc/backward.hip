@@ -1174,17 +1174,39 @@ __global__ __launch_bounds__(256) void k_cell_scatter(const unsigned long long *
     if (i >= n) return;
     const unsigned long long key = keys[i];
     const long long c = (long long)(key >> 32);
-    out[starts[c] + slot[i]] = key;
+    // (bounds: a slot or start that is not what k_bw_keys and the scan produced -- a stale count, as in the round-5
+    // graph-replay fault -- drops the key instead of writing outside the sorted array)
+    const long long d = (long long)starts[c] + slot[i];
+    if ((unsigned long long)d < (unsigned long long)n) out[d] = key;
     cellcnt[c] = 0;
+}
+
+// The cells whose keys need no in-cell order: level l's "outside" cell (coff[l + 1] - 1) holds the queries whose window
+// misses the level (and every query of a size-1 "zero" level).  No gradient reads them -- their dQ partial is zero
+// whatever group they fall in, and no target brick's origin range reaches the cell -- so k_cell_rank leaves them in
+// their arrival order instead of ranking each against the whole cell (a zero level puts all Nq keys of the level
+// into it: Nq^2 / 2 global-memory comparisons at (64, 64, 8) fmaps, verdict r5).
+struct OutsideCells {
+    long long c[DVC_MAX_LEVELS];
+    int L;
+};
+__device__ __forceinline__ bool outside_cell(const OutsideCells &oc, long long c) {
+    bool o = false;
+#pragma unroll
+    for (int l = 0; l < DVC_MAX_LEVELS; ++l) o |= l < oc.L && c == oc.c[l];
+    return o;
 }
 
 constexpr int kRankLds = 4096;   // keys staged per k_cell_rank workgroup
 __global__ __launch_bounds__(256) void k_cell_rank(const unsigned long long *__restrict__ in, long long n,
-                                                   const int *__restrict__ starts, unsigned long long *__restrict__ out) {
+                                                   const int *__restrict__ starts, unsigned long long *__restrict__ out,
+                                                   OutsideCells oc) {
     __shared__ unsigned long long win[kRankLds];
     const long long p0 = (long long)blockIdx.x * 256, p = p0 + threadIdx.x;
-    // the cells of positions p0 .. p0 + 255 span [s0, e1)
-    const int s0 = starts[in[p0] >> 32], e1 = starts[(in[min(p0 + 255, n - 1)] >> 32) + 1];
+    // the cells of positions p0 .. p0 + 255 span [s0, e1); outside cells are not staged (not ranked)
+    const long long c0 = (long long)(in[p0] >> 32), c1 = (long long)(in[min(p0 + 255, n - 1)] >> 32);
+    const int s0 = outside_cell(oc, c0) ? starts[c0 + 1] : starts[c0];
+    const int e1 = outside_cell(oc, c1) ? starts[c1] : starts[c1 + 1];
     const bool staged = e1 - s0 <= kRankLds;
     if (staged)
         for (int j = s0 + (int)threadIdx.x; j < e1; j += 256) win[j - s0] = in[j];
@@ -1192,6 +1214,10 @@ __global__ __launch_bounds__(256) void k_cell_rank(const unsigned long long *__r
     if (p >= n) return;
     const unsigned long long key = in[p];
     const long long c = (long long)(key >> 32);
+    if (outside_cell(oc, c)) {   // arrival order kept
+        out[p] = key;
+        return;
+    }
     const int s = starts[c], e = starts[c + 1];
     int r = 0;
     if (staged) {   // (16 independent LDS reads per step: a chain of single reads waited ~100 cycles per key)
@@ -2075,7 +2101,7 @@ static void win_dims(const dvc_layout &lay, int l, int radius, bool legacy, int 
 // (tuning "bwd_gt_wg": the workgroups per level aimed at, 64 .. 512; the workspace is sized for 512.  Round 5,
 // dense batches at config #3: 128 / 256 / 384 / 512 -> 0.80 / 0.69 / 0.65 / 0.615 ms; 768 / 1024 (level 0 in two
 // splits, sized for the test only) 0.67 / 0.66)
-static thread_local int g_gt_wg = 512;
+static Knob<int> g_gt_wg{512};
 void set_backward_gt_wg(int v) { g_gt_wg = v; }
 static int grad_t_splits(const dvc_layout &lay, int l, long long Nq, int target = 512) {
     const long long bricks = (long long)((lay.H[l] + 3) / 4) * ((lay.W[l] + 3) / 4) * ((lay.D[l] + 3) / 4);
@@ -2112,7 +2138,7 @@ static void bwd_plan(int B, long long Nq, const dvc_layout &lay, int radius, boo
         gw += (size_t)B * Nq * P.nw[l][0] * P.nw[l][1] * P.nw[l][2] * sizeof(float);
         P.coff[l] = cells;
         cells += level_cells(lay, l, P.nw[l]) + 1;   // + the level's "outside" cell
-        P.sp[l] = grad_t_splits(lay, l, Nq, std::min(g_gt_wg, 512));
+        P.sp[l] = grad_t_splits(lay, l, Nq, std::min((int)g_gt_wg, 512));
         const long long bricks = (long long)((lay.H[l] + 3) / 4) * ((lay.W[l] + 3) / 4) * ((lay.D[l] + 3) / 4);
         P.poff[l] = (long long)(part / sizeof(float));
         const int spm = grad_t_splits(lay, l, Nq);   // (the workspace: sized for the default, largest target)
@@ -2190,50 +2216,67 @@ static bool gq_sorted_fits(const BwdArgs &A, int nsl) {
 
 // 1: the gradient sums on the matrix cores wherever the offsets fit (fp32 operands split into bf16 hi/lo pairs,
 // round 4); 0: the VALU kernels for every dtype -- the large-volume fallback, kept testable at any size (tuning
-// "bwd_mfma", thread-local like every dvc_set_tuning knob)
-static thread_local int g_bwd_mfma = 1;
+// "bwd_mfma", process-global like every dvc_set_tuning knob)
+static Knob<int> g_bwd_mfma{1};
 void set_backward_mfma(int v) { g_bwd_mfma = v; }
 // 1: k_win_grad_pairs' 64-bit-addressed instance at every size (tests; the product picks it only past the 31-bit
 // row range, win_grad_needs_g64)
-static thread_local int g_bwd_g64 = 0;
+static Knob<int> g_bwd_g64{0};
 void set_backward_g64(int v) { g_bwd_g64 = v; }
 // 1 (default): bf16 / fp16 blocks store single 16-bit window gradients (kGwS16B / kGwS16H, round 5); 0: the hi/lo
 // pairs of round 4 (tuning "bwd_g16", for A/B and to keep the pair path tested on 16-bit blocks)
-static thread_local int g_bwd_g16 = 1;
+static Knob<int> g_bwd_g16{1};
 void set_backward_g16(int v) { g_bwd_g16 = v; }
 // 1 (default): k_grad_t_dense's batches across origin rows for 16-bit blocks; 0: k_grad_t_mfma's per-row batches
-static thread_local int g_bwd_dense = 1;
+static Knob<int> g_bwd_dense{1};
 void set_backward_dense(int v) { g_bwd_dense = v; }
 // 1 (default): batch element 0's key sort on a side stream beside the window gradients (tuning "bwd_side")
-static thread_local int g_bwd_side = 1;
+static Knob<int> g_bwd_side{1};
 void set_backward_side(int v) { g_bwd_side = v; }
-static thread_local int g_bwd_side_q = 1;
+static Knob<int> g_bwd_side_q{1};
 void set_backward_side_q(int v) { g_bwd_side_q = v; }
 struct BwdSide {
     int dev = -1;
     hipStream_t st = nullptr;
     hipEvent_t fork = nullptr, join = nullptr, wg = nullptr, jq = nullptr;
 };
-// one side stream and its fork / join events per host thread and device, created on first use (never destroyed)
-static BwdSide *bwd_side_stream() {
-    static thread_local BwdSide sides[16];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
-    BwdSide &sd = sides[dev];
+// One side stream and its fork / join events per host thread and device, created on first use and released when
+// the thread exits (a host with thread churn does not leak streams).  Keyed on the device of the caller's stream s;
+// when that is not the current device the backward stays on s alone (a stream can only be created on the current
+// device, and a cross-device fork would fail).
+struct BwdSides {
+    BwdSide s[16];
+    ~BwdSides() {
+        for (BwdSide &sd : s) {
+            for (hipEvent_t e : {sd.fork, sd.join, sd.wg, sd.jq})
+                if (e) (void)hipEventDestroy(e);
+            if (sd.st) (void)hipStreamDestroy(sd.st);
+        }
+    }
+};
+static BwdSide *bwd_side_stream(hipStream_t s) {
+    static thread_local BwdSides sides;
+    int dev = 0, cur = 0;
+    if (hipStreamGetDevice(s, &dev) != hipSuccess || hipGetDevice(&cur) != hipSuccess) return nullptr;
+    if (dev != cur || dev < 0 || dev >= 16) return nullptr;
+    BwdSide &sd = sides.s[dev];
     if (sd.dev == dev) return &sd;
     int least = 0, greatest = 0;   // (the highest priority: the small launches get their slots promptly)
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
-    if (hipStreamCreateWithPriority(&sd.st, hipStreamNonBlocking, greatest) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&sd.fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&sd.join, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&sd.wg, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&sd.jq, hipEventDisableTiming) != hipSuccess)
+    if (!sd.st && hipStreamCreateWithPriority(&sd.st, hipStreamNonBlocking, greatest) != hipSuccess) {
+        sd.st = nullptr;
         return nullptr;
+    }
+    for (hipEvent_t *e : {&sd.fork, &sd.join, &sd.wg, &sd.jq})
+        if (!*e && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
+            *e = nullptr;
+            return nullptr;
+        }
     sd.dev = dev;
     return &sd;
 }
 // 1 (default): the keys' counting sort (k_cell_scatter / k_cell_rank, round 5); 0: rocprim's radix sort + k_cell_starts
-static thread_local int g_bwd_sort = 1;
+static Knob<int> g_bwd_sort{1};
 void set_backward_sort(int v) { g_bwd_sort = v; }
 
 // dtype codes of the packed operands whose gradient sums run on the matrix cores (the rest: VALU)
@@ -2340,7 +2383,10 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
             }
             const unsigned kb = (unsigned)((nkeys + 255) / 256);
             k_cell_scatter<<<kb, 256, 0, st>>>(kin, slot, nkeys, starts, cellcnt, kout);
-            k_cell_rank<<<kb, 256, 0, st>>>(kout, nkeys, starts, kin);
+            OutsideCells oc{};
+            oc.L = A.L;
+            for (int l = 0; l < A.L; ++l) oc.c[l] = P.coff[l + 1] - 1;
+            k_cell_rank<<<kb, 256, 0, st>>>(kout, nkeys, starts, kin, oc);
             if (!launched("cell_sort")) return DVC_ERR_LAUNCH;
         } else {
             // (the cell bits only: the keys enter in (level, query) order and the sort is stable, so within a cell
@@ -2357,7 +2403,7 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     // Round 5: batch element 0's sort needs only the coordinates, so it runs on a side stream beside the window
     // gradients and the target tiles (its ~35 us of small launches hid under k_win_grad_pairs); the main stream
     // waits for it before the first consumer of the sorted keys.  Not while the stream is being captured.
-    BwdSide *side = g_bwd_side ? bwd_side_stream() : nullptr;
+    BwdSide *side = g_bwd_side ? bwd_side_stream(s) : nullptr;
     if (side) {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) side = nullptr;

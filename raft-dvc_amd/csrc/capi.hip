@@ -73,35 +73,35 @@ using namespace dvc;
 
 static thread_local char g_err[512] = "";
 // Kernel selection.  The defaults below are the product configuration (an immutable
-// table); dvc_set_tuning is a diagnostics hook whose overrides are THREAD-LOCAL, so a
-// tuning call on one host thread never changes the kernels another thread launches.
-static thread_local int g_lookup_variant = -1;   // tuning knobs (dvc_set_tuning)
-static thread_local int g_lookup_ablate = 0;
+// table); dvc_set_tuning is a diagnostics hook whose overrides are PROCESS-GLOBAL (round 6: they were
+// thread-local, which a backward run by the autograd engine's worker thread never saw).
+static Knob<int> g_lookup_variant{-1};   // tuning knobs (dvc_set_tuning)
+static Knob<int> g_lookup_ablate{0};
 // diagnostics: device address of a timeline buffer (16 x u64 per workgroup) for the default four-wave r = 4
 // tile instances, set as two 32-bit halves (tuning "lookup_trace_lo" / "lookup_trace_hi"; 0 = off)
-static thread_local int g_trace_lo = 0, g_trace_hi = 0;
-static thread_local int g_lookup_nt = 1;          // nontemporal output stores in the tile kernel
-static thread_local int g_lookup_order = 1;       // tile kernel level order (LookupArgs::order)
-static thread_local int g_lookup_ldpol = 0;       // tile kernel load cache policy (LookupArgs::ldpol)
-static thread_local int g_build_ablate = 0;       // diagnostics only: k_build_bf16 ablation instance
+static Knob<int> g_trace_lo{0}, g_trace_hi{0};
+static Knob<int> g_lookup_nt{1};          // nontemporal output stores in the tile kernel
+static Knob<int> g_lookup_order{1};       // tile kernel level order (LookupArgs::order)
+static Knob<int> g_lookup_ldpol{0};       // tile kernel load cache policy (LookupArgs::ldpol)
+static Knob<int> g_build_ablate{0};       // diagnostics only: k_build_bf16 ablation instance
 // build output stores: 1 = nontemporal (default; round 2 A/B, bench n1 twice each: build 0.545 -> 0.506 ms,
 // step 2.20 -> 2.11 ms -- the 2.46 GB pyramid never fits the caches it would otherwise sweep), 0 = default policy
-static thread_local int g_build_stpol = 1;
+static Knob<int> g_build_stpol{1};
 // column chunks per query tile are doubled while the build grid has fewer workgroups than this (tuning
 // "build_wgs"; 1024 = four per CU)
-static thread_local int g_build_wgs = 1024;
-static thread_local int g_build_variant = 1;      // 1 = two-barrier bf16-store kernel (k_build_bf16_2b), 0 = k_build_bf16
-static thread_local int g_build_f32_variant = 2;  // 2 = k_build_f32r, wave-private staging (default); 1 = k_build_f32r, workgroup staging; 0 = k_build_f32
+static Knob<int> g_build_wgs{1024};
+static Knob<int> g_build_variant{1};      // 1 = two-barrier bf16-store kernel (k_build_bf16_2b), 0 = k_build_bf16
+static Knob<int> g_build_f32_variant{2};  // 2 = k_build_f32r, wave-private staging (default); 1 = k_build_f32r, workgroup staging; 0 = k_build_f32
 // fused lookup kernel where the MFMA path applies: 2 = k_fused_box 2x2x16, 8 waves (default),
 // 3 = k_fused_box 4x4x4 cubes, 8 waves, 4 = k_fused_box 2x2x16, 4 waves, 1 = k_fused_tile, 0 = two-stage VALU
-static thread_local int g_fused_variant = 2;
-static thread_local int g_upflow_rows = 12;       // output rows per k_upflow work item (tools/ab_upflow.py)
-static thread_local int g_upflow_wgs = 1 << 30;   // k_upflow grid cap (workgroups striding over the items); round 2: one
+static Knob<int> g_fused_variant{2};
+static Knob<int> g_upflow_rows{12};       // output rows per k_upflow work item (tools/ab_upflow.py)
+static Knob<int> g_upflow_wgs{1 << 30};   // k_upflow grid cap (workgroups striding over the items); round 2: one
                                                   // workgroup per item, 178 -> 152 us at the #5 tail (tools/ab_upflow.py)
-static thread_local int g_upflow_staged = 1;      // 1 = k_upflow stages an item's low-res box in LDS (all ratios <= 1)
-static thread_local int g_pack_variant = 1;       // 1 = single-pass k_pack_pyramid where L <= 4, 0 = per-level launches
-static thread_local int g_pack_cg = 0;           // k_pack_pyramid channels per workgroup: 0 = by size (16 / 32), else 8 / 16 / 32
-static thread_local int g_fused_ablate = 0;
+static Knob<int> g_upflow_staged{1};      // 1 = k_upflow stages an item's low-res box in LDS (all ratios <= 1)
+static Knob<int> g_pack_variant{1};       // 1 = single-pass k_pack_pyramid where L <= 4, 0 = per-level launches
+static Knob<int> g_pack_cg{0};           // k_pack_pyramid channels per workgroup: 0 = by size (16 / 32), else 8 / 16 / 32
+static Knob<int> g_fused_ablate{0};
        // diagnostics only: 1 = skip output stores, 2 = skip window dots (cube kernel)
 
 static int fail(int code, const char *fmt, ...) {
@@ -174,17 +174,17 @@ static bool tile_ok(const LookupArgs &A, size_t esz) {
 // workgroup per slot, tools/trace_lookup.py); tools/ab_lookup.py, bitwise equal, 149.2 -> 145.2 us median.
 static constexpr long long kSplitTiles = 1024, kSplitRows = 512;
 // rows per chunk of the row split (0 = no row split; 2, 3, 5; tuning "split_ach")
-static thread_local int g_split_ach = 5;
+static Knob<int> g_split_ach{5};
 // launches with fewer query tiles than this take one (tile, level) pair per workgroup (tuning "split_tiles")
-static thread_local long long g_split_tiles = kSplitTiles;
+static Knob<long long> g_split_tiles{kSplitTiles};
 // r = 4 tile kernel: 4 = four waves of 3 + 2 + 2 + 2 output columns (default: two workgroups put two waves
 // on every SIMD), 0 = three 3-column waves.  Round 2 A/B (tools/ab_waves.py, bitwise-equal outputs, median
 // of 40 calls): config #3 bf16 151.8 -> 150.0 us, fp32 220.7 -> 213.9; one rank's slab of an 8 / 4 / 2-way
 // split 26.7 / 39.0 / 78.2 -> 26.2 / 38.9 / 77.4 us (bf16).
-static thread_local int g_lookup_waves = 4;
+static Knob<int> g_lookup_waves{4};
 // diagnostics: cache-policy bits of the tile kernel's output stores on the default bf16 r = 4 path
 // (-1 = the product's nontemporal stores; 0 plain, 16 sc1, 17 sc0 sc1, 18 nt sc1)
-static thread_local int g_lookup_stpol = -1;
+static Knob<int> g_lookup_stpol{-1};
 
 template <typename T, bool NT, int ACH>
 static void launch_tile_r(const LookupArgs &A, dim3 blocks, unsigned threads, hipStream_t s) {
@@ -1023,7 +1023,7 @@ static int launch_upflow(const float *lo, const float *delta, float *lo_out, flo
         return fail(DVC_ERR_UNSUPPORTED, "%s: output plane (%d,%d) x B*C=%lld exceeds 32-bit item indices", what, W, D,
                     (long long)B * C);
     const int vec = (D % 4 == 0) ? 4 : 1;   // 16-byte stores when every plane row is 16-byte aligned
-    const int nx = (int)ceil_div((long long)W * D, 256LL * vec), rows = std::min(g_upflow_rows, H);
+    const int nx = (int)ceil_div((long long)W * D, 256LL * vec), rows = std::min((int)g_upflow_rows, H);
     const int ny = (int)ceil_div(H, rows);
     const unsigned blocks = (unsigned)std::min<long long>((long long)nx * ny * B * C, g_upflow_wgs);
     const float rh = upflow_ratio(h, H), rw = upflow_ratio(w, W), rd = upflow_ratio(d, D);

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 
 #include "dvccorr.h"
 
@@ -26,6 +27,19 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 namespace dvc {
 
 constexpr int kWave = 64;
+
+// A dvc_set_tuning knob: process-global (relaxed atomic), so a value set on the caller's thread also governs the
+// launches PyTorch's autograd engine makes from its own per-device worker thread (round 6; the knobs were
+// thread_local before, which left a backward under loss.backward() on the defaults).
+template <typename T> struct Knob {
+    std::atomic<T> v;
+    explicit constexpr Knob(T x) : v(x) {}
+    operator T() const { return v.load(std::memory_order_relaxed); }
+    Knob &operator=(T x) {
+        v.store(x, std::memory_order_relaxed);
+        return *this;
+    }
+};
 
 // Geometry of the correlation pyramid, passed by value to kernels.
 struct Geo {

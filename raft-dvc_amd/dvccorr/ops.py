@@ -54,6 +54,24 @@ def _stream(t: torch.Tensor) -> ctypes.c_void_p:
     return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
 
 
+
+def _on_device(fn):
+    """Run an op with its tensors' device current (torch.cuda.device), so the C ABI's launches, workspaces and
+    the backward's side stream land on the GPU that owns the data even when the calling thread's current device
+    is another one (a block on cuda:1 driven from a thread whose current device is 0)."""
+    import functools
+
+    @functools.wraps(fn)
+    def run(*args, **kwargs):
+        for a in list(args) + list(kwargs.values()):
+            if isinstance(a, torch.Tensor) and a.is_cuda:
+                with torch.cuda.device(a.device):
+                    return fn(*args, **kwargs)
+        return fn(*args, **kwargs)
+
+    return run
+
+
 def _need_cuda(*ts: torch.Tensor) -> None:
     for t in ts:
         if not t.is_cuda:
@@ -78,6 +96,7 @@ def _f32c(t: torch.Tensor) -> torch.Tensor:
     return t.to(torch.float32).contiguous()
 
 
+@_on_device
 def pack_queries(fmap1_slab: torch.Tensor, dtype: int) -> torch.Tensor:
     _need_cuda(fmap1_slab)
     f = _f32c(fmap1_slab)
@@ -88,6 +107,7 @@ def pack_queries(fmap1_slab: torch.Tensor, dtype: int) -> torch.Tensor:
     return out
 
 
+@_on_device
 def pack_targets(fmap2: torch.Tensor, num_levels: int, dtype: int, out: torch.Tensor = None) -> torch.Tensor:
     """fmap2 -> packed targets of every level; dtype | DVC_BRICKED stores the bricked levels in brick order
     (the materialised build then writes a bricked pyramid, which only the tile lookups read)."""
@@ -104,6 +124,7 @@ def pack_targets(fmap2: torch.Tensor, num_levels: int, dtype: int, out: torch.Te
     return _mark(out, dtype)
 
 
+@_on_device
 def pack_targets_gathered(gathered: torch.Tensor, H: int, num_levels: int, dtype: int) -> torch.Tensor:
     """pack_targets of the fmap2 an H-slab all-gather delivers, read from its receive buffer
     gathered (world, B, C, ceil(H / world), W, D) without assembling fmap2 (dvc_pack_targets_gathered;
@@ -135,6 +156,7 @@ def alloc_corr(B: int, Nq: int, row_stride: int, store_dtype: int, device, zero:
     return buf[g:g + n].view(B, Nq, row_stride)
 
 
+@_on_device
 def build(packed_q: torch.Tensor, packed_t: torch.Tensor, C: int, H: int, W: int, D: int, num_levels: int,
           in_dtype: int, store_dtype: int, col_begin: int = 0, col_end=None, out: torch.Tensor = None) -> torch.Tensor:
     _need_cuda(packed_q, packed_t)
@@ -150,6 +172,7 @@ def build(packed_q: torch.Tensor, packed_t: torch.Tensor, C: int, H: int, W: int
     return out
 
 
+@_on_device
 def pool(corr: torch.Tensor, H: int, W: int, D: int, num_levels: int, src_level: int, store_dtype: int) -> None:
     _need_cuda(corr)
     _expect_layout(corr, store_dtype, "corr_pool")
@@ -158,6 +181,7 @@ def pool(corr: torch.Tensor, H: int, W: int, D: int, num_levels: int, src_level:
           "corr_pool")
 
 
+@_on_device
 def lookup(corr: torch.Tensor, coords: torch.Tensor, H: int, W: int, D: int, num_levels: int, radius: int,
            legacy: bool, store_dtype: int, out: torch.Tensor = None) -> torch.Tensor:
     _need_cuda(corr, coords)
@@ -172,6 +196,7 @@ def lookup(corr: torch.Tensor, coords: torch.Tensor, H: int, W: int, D: int, num
     return out
 
 
+@_on_device
 def proj_pack(weight: torch.Tensor, num_levels: int, radius: int, legacy: bool, exact: bool = False) -> torch.Tensor:
     """convc1.weight (96, L*(2r+1)^3[, 1, 1, 1]) -> the fused kernel's packed fp16 operand (dvc_proj_pack), or for
     fp32 pyramids (exact=True) its bf16 hi + lo blocks (dvc_proj_pack_exact, twice the bytes)."""
@@ -212,6 +237,7 @@ def proj_pack_cached(weight: torch.Tensor, num_levels: int, radius: int, legacy:
     return packed
 
 
+@_on_device
 def lookup_proj(corr: torch.Tensor, coords: torch.Tensor, packed_w: torch.Tensor, bias: torch.Tensor, H: int, W: int,
                 D: int, num_levels: int, radius: int, legacy: bool, store_dtype: int,
                 out: torch.Tensor = None) -> torch.Tensor:
@@ -223,6 +249,11 @@ def lookup_proj(corr: torch.Tensor, coords: torch.Tensor, packed_w: torch.Tensor
     b = _f32c(bias)
     if b.numel() != _lib.PROJ_COUT:
         raise ValueError(f"convc1 bias must have {_lib.PROJ_COUT} entries; got {b.numel()}")
+    need = lib().dvc_proj_packed_bytes(num_levels, radius) * (2 if (int(store_dtype) & ~DVC_BRICKED) == DVC_F32 else 1)
+    have = packed_w.numel() * packed_w.element_size()
+    if have < need:
+        raise ValueError(f"lookup_proj: packed_w holds {have} bytes; this store dtype's consumer reads {need} "
+                         f"(fp32 pyramids take proj_pack(..., exact=True); include/dvccorr.h, ABI 3)")
     if out is None:
         out = torch.empty((B, _lib.PROJ_COUT, Nq), dtype=torch.float32, device=corr.device)
     check(lib().dvc_corr_lookup_proj(_ptr(corr), _ptr(c), _ptr(packed_w), _ptr(b), _ptr(out), B, Nq, H, W, D,
@@ -231,6 +262,7 @@ def lookup_proj(corr: torch.Tensor, coords: torch.Tensor, packed_w: torch.Tensor
     return out
 
 
+@_on_device
 def lookup_fused_proj(packed_q: torch.Tensor, packed_t: torch.Tensor, coords: torch.Tensor, packed_w: torch.Tensor,
                       bias: torch.Tensor, C: int, H: int, W: int, D: int, num_levels: int, radius: int, legacy: bool,
                       dtype: int, out: torch.Tensor = None, workspace: torch.Tensor = None) -> torch.Tensor:
@@ -255,6 +287,7 @@ def lookup_fused_proj(packed_q: torch.Tensor, packed_t: torch.Tensor, coords: to
     return out
 
 
+@_on_device
 def lookup_fused(packed_q: torch.Tensor, packed_t: torch.Tensor, coords: torch.Tensor, C: int, H: int, W: int,
                  D: int, num_levels: int, radius: int, legacy: bool, dtype: int, out: torch.Tensor = None,
                  workspace: torch.Tensor = None) -> torch.Tensor:
@@ -279,6 +312,7 @@ def fused_workspace(B: int, Nq: int, num_levels: int, radius: int, device) -> to
     return torch.empty((max(nws, 4) // 4,), dtype=torch.float32, device=device)
 
 
+@_on_device
 def corr_backward(packed_q: torch.Tensor, packed_t: torch.Tensor, coords: torch.Tensor, grad_out: torch.Tensor,
                   C: int, H: int, W: int, D: int, num_levels: int, radius: int, legacy: bool, dtype: int):
     """d loss / d fmap1 (B, C, Nq) and d loss / d fmap2 (B, C, H, W, D), both float32, from the gradient of
@@ -299,6 +333,7 @@ def corr_backward(packed_q: torch.Tensor, packed_t: torch.Tensor, coords: torch.
     return d1, d2
 
 
+@_on_device
 def sample3d(vol: torch.Tensor, pts: torch.Tensor, legacy: bool) -> torch.Tensor:
     _need_cuda(vol, pts)
     v = _f32c(vol)
@@ -314,10 +349,12 @@ def sample3d(vol: torch.Tensor, pts: torch.Tensor, legacy: bool) -> torch.Tensor
 def coords_grid(B: int, H: int, W: int, D: int, device) -> torch.Tensor:
     out = torch.empty((B, 3, H, W, D), dtype=torch.float32, device=device)
     _need_cuda(out)
-    check(lib().dvc_coords_grid(_ptr(out), B, H, W, D, _stream(out)), "coords_grid")
+    with torch.cuda.device(out.device):
+        check(lib().dvc_coords_grid(_ptr(out), B, H, W, D, _stream(out)), "coords_grid")
     return out
 
 
+@_on_device
 def upflow(flow: torch.Tensor, target_shape) -> torch.Tensor:
     _need_cuda(flow)
     f = _f32c(flow)
@@ -330,6 +367,7 @@ def upflow(flow: torch.Tensor, target_shape) -> torch.Tensor:
     return out
 
 
+@_on_device
 def flow_step(coords1: torch.Tensor, delta_flow, target_shape):
     """(coords1 + delta_flow, upflow_3d(coords1 + delta_flow - coords0, target_shape)) in one pass."""
     _need_cuda(coords1)

@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol():
     for name in declared:
         assert hasattr(L, name), name
     assert set(declared) == set(_lib.EXPORTED)
-    assert L.dvc_abi_version() == 2
+    assert L.dvc_abi_version() == 3
     assert b"gfx950" in L.dvc_version()
 
 

@@ -407,7 +407,8 @@ def test_grad_cfg4_slab(precision, tol):
                                    {"bwd_g16": 0, "bwd_dense": 0}])
 @pytest.mark.parametrize("precision,tol", [("bf16", BF16_TOL), ("fp16", FP16_TOL), ("fp32", GRAD_TOL)])
 def test_grad_round5_paths_off(knobs, precision, tol):
-    """The round-5 backward paths switched off one at a time (tuning knobs, thread-local): the per-row target
+    """The round-5 backward paths switched off one at a time (tuning knobs, process-global since round 6, so the
+    autograd engine's worker thread that runs this backward sees them too): the per-row target
     batches (k_qt_tiles + k_grad_t_mfma), the in-order stream, the dQ pass on the main stream, rocprim's radix sort,
     and the hi/lo window-gradient pairs -- each still passes the C = 128, L = 4, r = 4 golden vectors (grad_cfg2),
     so the fallbacks stay tested while the defaults move on."""
@@ -420,6 +421,109 @@ def test_grad_round5_paths_off(knobs, precision, tol):
     finally:
         for k in knobs:
             _lib.set_tuning(k, defaults[k])
+
+
+def test_tuning_reaches_the_autograd_thread():
+    """the knobs were thread_local, so a backward run by PyTorch's autograd worker thread (loss.backward()
+    on a CUDA graph) ignored a knob set by the caller.  With the knobs process-global, bwd_mfma 0 set here must select
+    the VALU gradient kernels inside loss.backward(): the gradients equal ops.corr_backward's under the same knob on
+    this thread bit for bit, and differ from the matrix-core defaults (another summation order)."""
+    import dvccorr
+    from dvccorr import _lib, ops
+    S, C, L, r = 12, 64, 3, 3
+    seed = 6060
+    f1 = prng.normal(seed, (1, C, S, S, S))
+    f2 = prng.normal(seed + 1, (1, C, S, S, S))
+    coords = prng.flow_coords(seed + 2, 1, S, S, S, 2.5)
+    G = prng.normal(seed + 3, (1, L * (2 * r + 1) ** 3, S, S, S))
+
+    def autograd_grads():
+        t1 = torch.from_numpy(f1).to(DEV).requires_grad_(True)
+        t2 = torch.from_numpy(f2).to(DEV).requires_grad_(True)
+        out = dvccorr.CorrBlock(t1, t2, L, r, precision="fp32")(torch.from_numpy(coords).to(DEV))
+        (out * torch.from_numpy(G).to(DEV)).sum().backward()
+        return t1.grad.reshape(1, C, -1), t2.grad
+
+    dt = ops.dtype_code("fp32")
+    q = ops.pack_queries(torch.from_numpy(f1).to(DEV).reshape(1, C, -1), dt)
+    t = ops.pack_targets(torch.from_numpy(f2).to(DEV), L, dt)
+    cg = torch.from_numpy(coords).to(DEV).reshape(1, 3, -1)
+    gg = torch.from_numpy(G).to(DEV).reshape(1, -1, S ** 3)
+    mfma = autograd_grads()
+    _lib.set_tuning("bwd_mfma", 0)
+    try:
+        valu_ad = autograd_grads()
+        valu_direct = ops.corr_backward(q, t, cg, gg, C, S, S, S, L, r, False, dt)
+        torch.cuda.synchronize()
+    finally:
+        _lib.set_tuning("bwd_mfma", 1)
+    for a, b in zip(valu_ad, valu_direct):
+        assert torch.equal(a, b)
+    assert not torch.equal(mfma[1], valu_ad[1]), "the knob did not reach the autograd thread"
+
+
+@pytest.mark.parametrize("precision,tol", [("bf16", BF16_TOL), ("fp32", GRAD_TOL)])
+def test_grad_zero_level_outside_cell(precision, tol):
+    """Verdict r5: a (64, 64, 8) fmap at C = 128, L = 4, r = 4 (a 256 x 256 x 32 volume at 1/4) has a size-1 level 3
+    ((8, 8, 1), a "zero" level): all 32 K of its keys fall in that level's outside cell, which the counting sort ranked
+    by re-reading the whole cell from memory per key (~1e9 loads).  Outside cells now keep their arrival order (no
+    gradient reads them).  Checked: the gradients against autograd through oracle/torch_cpu.py on a ragged 512-row
+    slab (as test_grad_cfg3_slab), and the backward's time per query within 2x config #3's (32^3, the same 32 K
+    queries, no zero level)."""
+    import dvccorr
+    from dvccorr import ops
+    from oracle import torch_cpu
+    B, C, L, r = 1, 128, 4, 4
+    H, W, D = 64, 64, 8
+    N, n3 = H * W * D, (2 * r + 1) ** 3
+    q0, q1 = 20001, 20001 + 512
+    f1 = prng.normal(7201, (B, C, H, W, D))
+    f2 = prng.normal(7202, (B, C, H, W, D))
+    coords = prng.flow_coords(7203, B, H, W, D, 2.0)
+    Gs = prng.normal(7204, (B, L * n3, q1 - q0))
+    t1 = torch.from_numpy(f1).requires_grad_(True)
+    t2 = torch.from_numpy(f2).requires_grad_(True)
+    pyr = torch_cpu.build_rows(t1, t2, L, q0, q1)
+    out = torch_cpu.lookup_rows(pyr, torch.from_numpy(coords), r, False, q0, q1)
+    (out * torch.from_numpy(Gs)).sum().backward()
+    ref1 = t1.grad.numpy().reshape(B, C, N)[:, :, q0:q1]
+    ref2 = t2.grad.numpy()
+    g1 = torch.from_numpy(f1).to(DEV).requires_grad_(True)
+    g2 = torch.from_numpy(f2).to(DEV).requires_grad_(True)
+    blk = dvccorr.CorrBlock(g1, g2, L, r, precision=precision)
+    G = torch.zeros((B, L * n3, N), device=DEV)
+    G[:, :, q0:q1] = torch.from_numpy(Gs).to(DEV)
+    (blk(torch.from_numpy(coords).to(DEV)) * G.view(B, L * n3, H, W, D)).sum().backward()
+    d1 = g1.grad.reshape(B, C, N)
+    assert bool(torch.isfinite(d1).all()) and bool(torch.isfinite(g2.grad).all())
+    assert not bool(d1[:, :, :q0].any()) and not bool(d1[:, :, q1:].any())
+    e1 = orc.rel_err(d1[:, :, q0:q1].cpu().numpy(), ref1)
+    e2 = orc.rel_err(g2.grad.cpu().numpy(), ref2)
+    assert e1 <= tol and e2 <= tol, (precision, e1, e2)
+
+    # time per query against config #3's shape (same query count)
+    def bwd_ms(shape, seed):
+        h, w, d = shape
+        dt = ops.dtype_code(precision)
+        a = torch.from_numpy(prng.normal(seed, (1, C, h, w, d))).to(DEV)
+        b = torch.from_numpy(prng.normal(seed + 1, (1, C, h, w, d))).to(DEV)
+        c = torch.from_numpy(prng.flow_coords(seed + 2, 1, h, w, d, 2.0)).to(DEV).reshape(1, 3, -1)
+        g = torch.randn((1, L * n3, h * w * d), device=DEV)
+        q = ops.pack_queries(a.reshape(1, C, -1), dt)
+        t = ops.pack_targets(b, L, dt)
+        ops.corr_backward(q, t, c, g, C, h, w, d, L, r, False, dt)
+        torch.cuda.synchronize()
+        e0, e1_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(3):
+            ops.corr_backward(q, t, c, g, C, h, w, d, L, r, False, dt)
+        e1_.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1_) / 3
+
+    t_zero = bwd_ms((H, W, D), 7301)
+    t_cfg3 = bwd_ms((32, 32, 32), 7311)
+    assert t_zero <= 2.0 * t_cfg3, (precision, t_zero, t_cfg3)
 
 
 def test_graph_captured_backward():
