@@ -487,6 +487,8 @@ def main():
                      "(dvc_corr_lookup_fused_proj, convc1 fused, timed together)")
         elif sixteen and 1 <= R <= 4:
             kname = "k_fused_box (dvc_corr_lookup_fused)"
+        elif 1 <= R <= 4 and "fused_variant=0" not in args.tune:
+            kname = "k_fused_box_f32 (dvc_corr_lookup_fused; fp32 operands as three bf16 pieces, six MFMAs per step)"
         else:
             kname = "k_fused_dots + k_lookup_win (dvc_corr_lookup_fused)"
         roof = {"kernel": kname,

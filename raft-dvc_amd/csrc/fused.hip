@@ -205,11 +205,15 @@ __global__ void k_fused_tile(const bf16_t *, const bf16_t *, LookupArgs, int, lo
 // whole (y, x) planes of queries (Nq a multiple of W*D: the full grid or an H-slab of it) and packed targets
 // addressable with 32-bit byte offsets.  fp16 (the AMP block) runs on the box kernels; the round-1 tile kernel
 // (variant 1) is bf16 only, so an fp16 request for it takes the default box kernel.
+// Round 6: fp32 blocks too, on k_fused_box_f32 (fused_box_f32.hip: bf16 hi/lo split operands, fp32 window dots).
 static bool fused_tile_ok(long long Nq, int W, int D, int Cp, long long t_rows, int radius, int dtype) {
-    return (dtype == DVC_BF16 || dtype == DVC_F16) && radius >= 1 && radius <= 4 &&
+    const int es = dtype == DVC_F32 ? 4 : 2;
+    return (dtype == DVC_BF16 || dtype == DVC_F16 || dtype == DVC_F32) && radius >= 1 && radius <= 4 &&
            (Cp == 32 || Cp == 64 || Cp == 128) && Nq % ((long long)W * D) == 0 &&
-           t_rows * Cp * 2 < (1LL << 31) - 65536;
+           t_rows * Cp * es < (1LL << 31) - 65536;
 }
+void launch_fused_box_f32(int radius, const float *Q, const float *Tt, const LookupArgs &A, int Cp, long long t_rows,
+                          int Hq, int Wq, int Dq, float scale, hipStream_t s);
 
 template <int R>
 static void launch_fused_tile(const bf16_t *Q, const bf16_t *Tt, const LookupArgs &A, int Cp, long long t_rows,
@@ -321,7 +325,10 @@ int fused_lookup(const void *packed_q, const void *packed_t, const float *coords
         const int Wq = lay.W[0], Dq = lay.D[0];
         const int Hq = (int)(Nq / ((long long)Wq * Dq));
         const bf16_t *Q = (const bf16_t *)packed_q, *Tt = (const bf16_t *)packed_t;
-        switch (radius) {
+        if (dtype == DVC_F32)
+            launch_fused_box_f32(radius, (const float *)packed_q, (const float *)packed_t, T, Cp, lay.row_stride, Hq, Wq,
+                                 Dq, scale, s);
+        else switch (radius) {
         case 1: launch_fused_mfma_dt<1>(dtype, variant, Q, Tt, T, Cp, lay.row_stride, Hq, Wq, Dq, scale, s); break;
         case 2: launch_fused_mfma_dt<2>(dtype, variant, Q, Tt, T, Cp, lay.row_stride, Hq, Wq, Dq, scale, s); break;
         case 3: launch_fused_mfma_dt<3>(dtype, variant, Q, Tt, T, Cp, lay.row_stride, Hq, Wq, Dq, scale, s); break;

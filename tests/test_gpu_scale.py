@@ -84,11 +84,12 @@ def test_cfg4_rank_slab(rank):
 FP16_TOL = 5e-3     # the reference's AMP tolerance (test_corr_equivalence.py:156-186)
 
 
-@pytest.mark.parametrize("precision,tol", [("bf16", BF16_TOL), ("fp16", FP16_TOL)])
+@pytest.mark.parametrize("precision,tol", [("bf16", BF16_TOL), ("fp16", FP16_TOL), ("fp32", FP32_TOL)])
 def test_cfg5_fused_rows(precision, tol):
     """Config #5: 128^3 x 128 fmaps, L=2, r=4, on-the-fly block (the 9.9 TB volume is never built):
     256 sampled query rows (plus corners, edges and one chunk's lanes 48-63) against the f64 oracle at the
-    operand dtype's tolerance -- bf16 (the bench's dtype) and fp16 (the Trainer's AMP operands)."""
+    operand dtype's tolerance -- bf16 (the bench's dtype), fp16 (the Trainer's AMP operands) and fp32 (the
+    reference's evaluation dtype; round 6: on the matrix cores, k_fused_box_f32)."""
     import dvccorr
     S, C, L, r = 128, 128, 2, 4
     f1, f2, c = _inputs(505, C, S)
