@@ -466,13 +466,14 @@ def main():
     else:   # fused: the "build" only packs fmap1 rows and the pooled fmap2 pyramid (read f32, write bf16/f32)
         bd_bytes = (nq_local + n_targets) * C * 4 + (nq_local + unpadded) * C * store_bytes
         bd_flops = 0.0
-    traffic = None
+    traffic = traffic_src = None
     if os.path.exists(args.traffic_file) and not shard_diag and args.flow == "random":   # PMC passes are per workload
         try:
             tf = json.load(open(args.traffic_file))
             key = f"{args.impl}_{args.precision}_{S}_L{L}_r{R}_n{world if strong else 1}" + \
                 (f"_convc1_{args.convc1}" if args.convc1 else "")
             traffic = tf.get(key, {}).get("lookup_hbm_bytes_per_launch")
+            traffic_src = tf.get(key, {}).get("note") if traffic is not None else None
         except Exception:
             traffic = None
     lk_roof = lk_bytes / (lk_avg * 1e-3) / 1e9 if lk_avg else 0.0
@@ -494,7 +495,8 @@ def main():
         roof = {"kernel": kname,
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "algorithmic_bytes_per_launch": lk_bytes, "avg_launch_ms": round(lk_avg, 4)}
+                "algorithmic_bytes_per_launch": lk_bytes, "avg_launch_ms": round(lk_avg, 4),
+                "traffic_source": traffic_src}   # which PMC pass (file, tree) the traffic figure comes from
         if args.impl == "fused":
             # the reference OTF dot count 2 C (2r+1)^3 L per voxel-query, against the dtype's MFMA peak
             fl = 2.0 * C * (2 * R + 1) ** 3 * L * nq_local

@@ -101,6 +101,9 @@ static Knob<int> g_upflow_wgs{1 << 30};   // k_upflow grid cap (workgroups strid
 static Knob<int> g_upflow_staged{1};      // 1 = k_upflow stages an item's low-res box in LDS (all ratios <= 1)
 static Knob<int> g_pack_variant{1};       // 1 = single-pass k_pack_pyramid where L <= 4, 0 = per-level launches
 static Knob<int> g_pack_cg{0};           // k_pack_pyramid channels per workgroup: 0 = by size (16 / 32), else 8 / 16 / 32
+// smallest padded depth of a bricked level (tuning "brick_min_dp", 32 or 16; set it before packing a block, the
+// layout is decided once per buffer)
+static Knob<int> g_brick_min_dp{32};
 static Knob<int> g_fused_ablate{0};
        // diagnostics only: 1 = skip output stores, 2 = skip window dots (cube kernel)
 
@@ -342,6 +345,11 @@ int dvc_set_tuning(const char *key, int value) {
         g_split_ach = value;
         return DVC_OK;
     }
+    if (!strcmp(key, "brick_min_dp")) {
+        if (value != 16 && value != 32) return fail(DVC_ERR_INVALID, "set_tuning: brick_min_dp %d (16 or 32)", value);
+        g_brick_min_dp = value;
+        return DVC_OK;
+    }
     if (!strcmp(key, "build_stpol")) {
         g_build_stpol = value != 0;
         return DVC_OK;
@@ -492,7 +500,7 @@ int dvc_bricked_levels(const dvc_layout *lay) {
     int m = 0;
     if (!lay) return 0;
     for (int l = 0; l < lay->num_levels && l < 4; ++l)
-        if (!lay->zero_level[l] && lay->Dp[l] >= 32 && lay->W[l] % 8 == 0) m |= 1 << l;
+        if (!lay->zero_level[l] && lay->Dp[l] >= g_brick_min_dp && lay->W[l] % 8 == 0) m |= 1 << l;
     return m;
 }
 

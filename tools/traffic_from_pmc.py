@@ -19,26 +19,33 @@ def pick(d, prefix):
 
 note = "HBM bytes per launch: 2 x FETCH_SIZE + WRITE_SIZE (KB x 1024), rocprofv3 --pmc, gfx950; source: {}"
 out = {}
-m4 = json.load(open(os.path.join(P, "r04", "r04_pmc_mat32.json")))
+m6 = json.load(open(os.path.join(P, "r06", "r06_pmc_mat32.json")))
 out["materialised_bf16_32_L4_r4_n1"] = {
-    "build_hbm_bytes_per_launch": hbm(pick(m4, "k_build_bf16_2b")),
-    "lookup_hbm_bytes_per_launch": hbm(pick(m4, "k_lookup_tile")),
-    "note": note.format("profiles/r04/r04_pmc_mat32.json (DVC_BRICKED level 0; tools/pmc_recipes.sh r4a)")}
-mp = json.load(open(os.path.join(P, "r02_pmc_mat32_convc1_f.json")))
+    "build_hbm_bytes_per_launch": hbm(pick(m6, "k_build_bf16_2b")),
+    "lookup_hbm_bytes_per_launch": hbm(pick(m6, "k_lookup_tile")),
+    "note": note.format("profiles/r06/r06_pmc_mat32.json (round 6; tree 2e233ac = the round-6 lookup and build kernels; "
+                        "DVC_BRICKED level 0)")}
+mp = json.load(open(os.path.join(P, "r06", "r06_pmc_mat32_convc1.json")))
 out["materialised_bf16_32_L4_r4_n1_convc1_fused"] = {
     "lookup_hbm_bytes_per_launch": hbm(pick(mp, "k_lookup_tile")),
-    "note": note.format("profiles/r02_pmc_mat32_convc1_f.json (k_lookup_tile<PROJ>, DVC_BRICKED level 0)")}
-f = json.load(open(os.path.join(P, "r03", "r03_pmc_fused128.json")))
+    "note": note.format("profiles/r06/r06_pmc_mat32_convc1.json (round 6, tree 6665544; k_lookup_tile<PROJ>, "
+                        "DVC_BRICKED level 0)")}
+f = json.load(open(os.path.join(P, "r06", "r06_pmc_fused128.json")))
 out["fused_bf16_128_L2_r4_n1"] = {
-    "lookup_hbm_bytes_per_launch": hbm(pick(f, "k_fused_box")),
-    "note": note.format("profiles/r03/r03_pmc_fused128.json")}
+    "lookup_hbm_bytes_per_launch": hbm(pick(f, "k_fused_box<")),
+    "note": note.format("profiles/r06/r06_pmc_fused128.json (round 6, tree 6665544)")}
+f32 = json.load(open(os.path.join(P, "r06", "r06_pmc_fused128_fp32.json")))
+out["fused_fp32_128_L2_r4_n1"] = {
+    "lookup_hbm_bytes_per_launch": hbm(pick(f32, "k_fused_box_f32")),
+    "note": note.format("profiles/r06/r06_pmc_fused128_fp32.json (round 6, tree 6665544; k_fused_box_f32)")}
 fp = json.load(open(os.path.join(P, "r03", "r03_pmc_fused128_convc1.json")))
 out["fused_bf16_128_L2_r4_n1_convc1_fused"] = {
     "lookup_hbm_bytes_per_launch": sum(hbm(pick(fp, k)) for k in ("k_otf_keys", "k_fused_proj", "k_rows_to_channels")),
-    "note": note.format("profiles/r03/r03_pmc_fused128_convc1.json") + " (k_otf_keys + k_fused_proj + k_rows_to_channels)"}
+    "note": note.format("profiles/r03/r03_pmc_fused128_convc1.json") + " (k_otf_keys + k_fused_proj + k_rows_to_channels; "
+                                                                      "round 3, kernels unchanged since)"}
 old = json.load(open(os.path.join(P, "traffic.json")))
-for k, v in old.items():   # keep round-1 entries no round-2 pass replaced, marked as such
+for k, v in old.items():   # keep entries no round-6 pass replaced, as they were
     if k not in out:
-        out[k] = dict(v, note=v.get("note", "") + " (round 1)")
+        out[k] = v
 json.dump(out, open(os.path.join(P, "traffic.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))
