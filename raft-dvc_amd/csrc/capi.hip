@@ -35,7 +35,7 @@ template <typename T>
 __global__ void k_corr_pool(T *, long long, long long, long long, int, int, long long, int, int, int, int);
 template <typename T, int R, bool WINBUF, bool ALIGNED> __global__ void k_lookup_win(LookupArgs);
 template <typename T> __global__ void k_lookup_generic(LookupArgs);
-template <typename T, int R, bool NT, int ABL, int PROJ, int ACH, int NWV = 0, int SPOL = -1>
+template <typename T, int R, bool NT, int ABL, int PROJ, int ACH, int NWV = 0, int SPOL = -1, bool XLP = false>
 __global__ void k_lookup_tile(LookupArgs);
 __global__ void k_proj_pack(const float *, bf16_t *, int, int, int, long long, int);
 __global__ void k_sample3d(const float *, const float *, float *, int, int, int, int, int, long long, int);
@@ -82,7 +82,7 @@ static Knob<int> g_lookup_ablate{0};
 static Knob<int> g_trace_lo{0}, g_trace_hi{0};
 static Knob<int> g_lookup_nt{1};          // nontemporal output stores in the tile kernel
 static Knob<int> g_lookup_order{1};       // tile kernel level order (LookupArgs::order)
-static Knob<int> g_lookup_ldpol{0};       // tile kernel load cache policy (LookupArgs::ldpol)
+static Knob<int> g_lookup_ldpol{0};       // tile kernel load cache policy (LookupArgs::ldpol; not the convc1 instances)
 static Knob<int> g_build_ablate{0};       // diagnostics only: k_build_bf16 ablation instance
 // build output stores: 1 = nontemporal (default; round 2 A/B, bench n1 twice each: build 0.545 -> 0.506 ms,
 // step 2.20 -> 2.11 ms -- the 2.46 GB pyramid never fits the caches it would otherwise sweep), 0 = default policy
@@ -906,11 +906,20 @@ int dvc_corr_lookup_proj(const void *corr, const float *coords, const void *pack
     hipStream_t s = (hipStream_t)stream;
 #define DVC_PROJ_LAUNCH(T, P)                                                                \
     switch (radius) {                                                                        \
-    case 1: k_lookup_tile<T, 1, true, 0, P, 0><<<blocks, threads, 0, s>>>(A); break;           \
-    case 2: k_lookup_tile<T, 2, true, 0, P, 0><<<blocks, threads, 0, s>>>(A); break;           \
-    case 3: k_lookup_tile<T, 3, true, 0, P, 0><<<blocks, threads, 0, s>>>(A); break;           \
-    default: k_lookup_tile<T, 4, true, 0, P, 0><<<blocks, threads, 0, s>>>(A); break;          \
+    case 1: k_lookup_tile<T, 1, true, 0, P, 0, 0, -1, DVC_PROJ_XLP><<<blocks, threads, 0, s>>>(A); break;           \
+    case 2: k_lookup_tile<T, 2, true, 0, P, 0, 0, -1, DVC_PROJ_XLP><<<blocks, threads, 0, s>>>(A); break;           \
+    case 3: k_lookup_tile<T, 3, true, 0, P, 0, 0, -1, DVC_PROJ_XLP><<<blocks, threads, 0, s>>>(A); break;           \
+    default: k_lookup_tile<T, 4, true, 0, P, 0, 0, -1, DVC_PROJ_XLP><<<blocks, threads, 0, s>>>(A); break;          \
     }
+#if DVC_DIAG
+    if (store_dtype == DVC_BF16 && radius == 4) {
+        A.trace = (unsigned long long *)(((unsigned long long)(unsigned)g_trace_hi << 32) | (unsigned)g_trace_lo);
+        if (A.trace) {   // diagnostics only: every-level timeline stamps (tools/trace_proj.py)
+            k_lookup_tile<bf16_t, 4, true, 16, 1, 0, 0, -1, DVC_PROJ_XLP><<<blocks, threads, 0, s>>>(A);
+            return check_launch("corr_lookup_proj");
+        }
+    }
+#endif
     if (store_dtype == DVC_BF16) { DVC_PROJ_LAUNCH(bf16_t, 1) }
     else if (store_dtype == DVC_F16) { DVC_PROJ_LAUNCH(f16_t, 1) }
     else { DVC_PROJ_LAUNCH(float, 2) }   // fp32 pyramid: the exact split consumer (dvc_proj_pack_exact weights)

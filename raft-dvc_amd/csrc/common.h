@@ -15,6 +15,12 @@
 #ifndef DVC_DIAG
 #define DVC_DIAG 0
 #endif
+// 1: the convc1-fused tile lookup prefetches each next level under the current one's last row (lookup_tile.h XLP;
+// round 6 A/B, gpurun_out/r6g: 0.137 ms against 0.108 without -- the prefetch's live state spills 45 VGPRs at two
+// waves per SIMD and the next level's first plane waits a full latency in the last row; off)
+#ifndef DVC_PROJ_XLP
+#define DVC_PROJ_XLP 0
+#endif
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));

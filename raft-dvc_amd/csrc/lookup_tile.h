@@ -194,7 +194,7 @@ struct ProjCfg {
 #ifndef DVC_PROJ_ABL
 #define DVC_PROJ_ABL 0
 #endif
-template <typename T, int R, bool NT, int ABL, int PROJ, int ACH, int NWV = 0, int SPOL = -1>
+template <typename T, int R, bool NT, int ABL, int PROJ, int ACH, int NWV = 0, int SPOL = -1, bool XLP = false>
 __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)), PROJ == 2 ? 1 : 2) void k_lookup_tile(
     LookupArgs A) {
     using C = TileCfg<T, R, NWV>;
@@ -235,13 +235,18 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
             const f16x8 *wp = reinterpret_cast<const f16x8 *>(A.proj_w) + lane;
             // PROJ 2: the lo weights, one packed block after the hi ones
             const long long wlo = PROJ == 2 ? (long long)A.Ltot * n * NWP * OT * 64 : 0;
+            const bool xlp_c = XLP && !A.split_levels;   // (PROJ: ACH == 0, PD == 2) the producers' cross-level prefetch
+            bool started_c = false;
             for (int li = 0; li < A.nl; ++li) {
                 const int l = A.l0 + (rev ? A.nl - 1 - li : li);
                 if (A.zero[l] || A.generic[l]) continue;   // (the producers skip the same levels)
-                __syncthreads();
-                __syncthreads();   // level preamble: window table
-                __syncthreads();
-                __syncthreads();   // planes 0 and 1 staged
+                if (!(xlp_c && started_c)) {
+                    __syncthreads();
+                    __syncthreads();   // level preamble: window table
+                    __syncthreads();   // plane 0 staged
+                }
+                __syncthreads();       // plane 1 staged (a prefetched level's only preamble barrier)
+                started_c = true;
                 for (int a = 0; a < n; ++a) {
                     // this row's weight block, [wave slice ks][16-channel tile ot][lane] x 8 fp16
                     const f16x8 *wr = wp + (long long)(l * n + a) * NWP * OT * 64;
@@ -329,9 +334,16 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
     // ABL & 8 (diagnostics only): thread 0 stamps s_memrealtime (100 MHz) at checkpoints of the first level it
     // processes into A.trace[wg * 16 + k] with a vector (buffer) store
     const long long wg = ((long long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-    int trace_level = 1;   // only the first level is traced
+    int trace_level = 1;   // only the first level is traced (ABL & 16: every level, 64 stamps per workgroup)
+    int trace_li = 0;      // (ABL & 16) the level's position in the workgroup's walk
     auto stamp = [&](int k) {
-        if constexpr ((ABL & 8) != 0) {
+        if constexpr ((ABL & 16) != 0) {
+            if (tid == 0 && k < 16)
+                __builtin_amdgcn_raw_buffer_store_b64(
+                    __builtin_bit_cast(u32x2, (unsigned long long)__builtin_amdgcn_s_memrealtime()),
+                    __builtin_amdgcn_make_buffer_rsrc(A.trace, (short)0, 0x7fffffff, 0x00020000),
+                    (int)((wg * 64 + (k == 15 ? 3 : trace_li) * 16 + k) * 8), 0, 0);
+        } else if constexpr ((ABL & 8) != 0) {
             if (tid == 0 && (trace_level || k == 15) && k < 16)
                 __builtin_amdgcn_raw_buffer_store_b64(
                     __builtin_bit_cast(u32x2, (unsigned long long)__builtin_amdgcn_s_memrealtime()),
@@ -360,7 +372,6 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
     const int chstep_u = A.legacy ? 1 : n;       // output-channel step per U (W-axis) offset
     const int chstep_v = A.legacy ? n : 1;       // ... per V (D-axis) offset
     const int u0 = BAL ? wave * FLO + min(wave, REM) : wave * C::COLS;   // this wave's columns u0 .. u0 + NU - 1
-    const int ldpol = A.ldpol;
 
     // store of output (row a, column u, offset v) of this lane's query
     auto out_rsrc = [&](float *obase, int a, int u) {
@@ -374,8 +385,152 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
     };
 
     static_assert(!PROJ || ACH == 0, "the convc1 consumer accumulates every row of the tile");
-    // output rows [a0, a0 + NA) of level l; planes a0 .. a0 + NA of the window
-    auto level = [&](int l, auto nu_c, auto na_c, int a0) {
+    using Chunk = typename std::conditional<C::CB == 16, u32x4, u32x2>::type;
+    constexpr int PD = PROJ ? 2 : C::PD;   // (the convc1 consumer's 96 accumulators: keep the registers)
+    // Cross-level prefetch (round 6; XLP): a workgroup that walks every level of its tile (no level split, no row
+    // split: the convc1-fused lookup always, the plain lookup on launches of >= 1024 tiles) starts the next level's
+    // pipeline under the current level's last rows -- its window table (end of row n - 3, wave 0), chunk addresses,
+    // LDS offsets and plane 0 / 1 loads (start of row n - 1, when this level's staging registers and chunk state
+    // are dead), plane 0 written to the free LDS slot and plane 2's loads issued at the end of row n - 1.  The
+    // next level then begins at its first row instead of a table barrier pair and two dependent plane round
+    // trips: tools/trace_proj.py measured that restart at 12-13 us per level of the ~100 us convc1 lookup.
+    // (XLP instances only: the hooks' live values cost the split-level instances registers they do not use)
+    const bool xlp = XLP && ACH == 0 && PD == 2 && !A.split_levels;
+    Chunk st_x[PD][C::MAXCH];   // (XLP) planes staged in registers, carried from one level into the next
+    // this thread's chunks of every plane: (query j, column c, z-chunk k).  voff = byte offset of the chunk in
+    // window plane 0; window plane wp adds wp * plane_bytes.  pk = LDS offset / 8 (low 16 bits; 0xffff: no chunk)
+    // | mask of the window planes inside the level (high 16 bits).  Planes outside it are not loaded: their LDS
+    // slots keep earlier, finite data, and their weights are 0.
+    int voff[C::MAXCH];
+    unsigned pk[C::MAXCH];
+    struct LevelGeo {
+        int Hl, Wl, Dl, Dpl, NC, ZW, ZC, nch, SQ, plane_bytes, lev_b;
+        bool bk8;
+    };
+    auto geo = [&](int l) {
+        LevelGeo g;
+        g.Hl = A.H[l]; g.Wl = A.W[l]; g.Dl = A.D[l]; g.Dpl = A.Dp[l];
+        g.NC = min(NW, g.Wl);
+        g.ZW = min(g.Dpl, C::ZWMAX);
+        g.ZC = g.ZW / CE;                   // chunks per column
+        g.nch = 64 * g.NC * g.ZC;           // chunks per plane slot
+        g.SQ = g.NC * g.ZW * ES + 8;
+        g.plane_bytes = g.Wl * g.Dpl * ES;
+        g.lev_b = (int)A.off[l] * ES;
+        // a bricked level (DVC_BRICKED, bit l of A.brick): voxel (y, x, z) at
+        // ((y * W/8 + x/8) * Dp/8 + z/8) * 64 + (x%8) * 8 + z%8, i.e. (1, 8, 8) bricks of one 128-byte
+        // line, so the strip of a window plane touches lines of 8 columns x 8 z instead of 2 x 32
+        // (Dp = 32) or 1 x 64; the strip's z-chunk that the query's run never reaches is not loaded.
+        g.bk8 = (A.brick >> l) & 1;
+        return g;
+    };
+    // this lane's query at level l: window origin (ih, iu, iv) and the strip origin (cs, za)
+    auto window = [&](int l, const LevelGeo &g, WinAxes &ax, int &ih, int &iu, int &iv, int &cs, int &za) {
+        const float sc = (float)(1 << l);
+        window_axes(cy / sc, cx / sc, cz / sc, g.Hl, g.Wl, g.Dl, A.legacy, ax);
+        // (a NaN / huge coordinate moves the window far outside the level: every
+        //  weight below is then folded to 0 and the output is 0, as the reference's)
+        ih = (int)ax.kh - R; iu = (int)ax.ku - R; iv = (int)ax.kv - R;
+        cs = min(max(iu, 0), g.Wl - g.NC);
+        za = min(max(iv & ~(CE - 1), 0), g.Dpl - g.ZW);
+    };
+    auto write_tab = [&](const LevelGeo &g, int ih, int cs, int za, int iv, int iu) {   // (wave 0)
+        tab[0][lane] = min(max(ih, -2 * NW), g.Hl);
+        tab[1][lane] = cs;
+        tab[2][lane] = za;
+        tab[3][lane] = iv;
+        tab[4][lane] = iu;
+    };
+    // chunk decode from the window table: what & 1 -> voff (returns the mask of chunks plane 0 loads),
+    // what & 2 -> pk
+    auto chunk_setup = [&](const LevelGeo &g, int what) -> unsigned {
+        // chunk index -> (query, column, z-chunk) by float reciprocals: idx < 2^12 and divisors <= 60, so
+        // (idx + 0.5) / d sits >= 1/120 from an integer while the float error is < 2^-11 (no integer divides)
+        const int NCZ = g.NC * g.ZC;
+        const float inv_ncz = 1.0f / (float)NCZ, inv_zc = 1.0f / (float)g.ZC;
+        // byte offsets fit 32 bits (the buffer covers one tile's rows: 64 x row_stride x ES < 2^31)
+        const int rs_b = (int)A.row_stride * ES;
+        unsigned m0 = 0;
+#pragma unroll
+        for (int k = 0; k < C::MAXCH; ++k) {
+            const int idx = tid + k * C::THREADS;
+            const int j = (int)(((float)idx + 0.5f) * inv_ncz);
+            const int rem = idx - j * NCZ;
+            const int c = (int)(((float)rem + 0.5f) * inv_zc);
+            const int zc = rem - c * g.ZC;
+            const bool ok = idx < g.nch;
+            const int jj = ok ? j : 0;
+            const int ihj = tab[0][jj];
+            const int plo = min(max(-ihj, 0), NW), phi = min(max(g.Hl - ihj, 0), NW);
+            unsigned mask = ok && jj < nvalid ? ((1u << phi) - 1u) & ~((1u << plo) - 1u) : 0u;
+            // only chunks the window reads: its columns [iu, iu + NW) (the strip is clamped into the level, so
+            // at a border it holds columns outside the window) and the z-chunks its run [iv, iv + NW) reaches.
+            // Every other chunk is read with weight 0 or not at all (coff clamps into the window's columns).
+            const int zs = tab[2][jj] + zc * CE, ivj = tab[3][jj], x = tab[1][jj] + c, xw = x - tab[4][jj];
+            if (!(zs < ivj + NW && zs + CE > ivj) || (unsigned)xw >= (unsigned)NW) mask = 0u;
+            if (what & 2) pk[k] = (ok ? (unsigned)(jj * g.SQ + (c * g.ZW + zc * CE) * ES) >> 3 : 0xffffu) | (mask << 16);
+            if (what & 1) {
+                const int inplane = g.bk8 ? (((x >> 3) * (g.Dpl >> 3) + (zs >> 3)) * 64 + (x & 7) * 8 + (zs & 7))
+                                          : x * g.Dpl + zs;
+                voff[k] = jj * rs_b + g.lev_b + (ihj * g.Wl * g.Dpl + inplane) * ES;
+                m0 |= (mask & 1u) << k;
+            }
+        }
+        return m0;
+    };
+    // PROJ: every chunk load is issued, unconditionally: a chunk the plane does not need gets an offset past the
+    // buffer's range, which reads zeros with no memory traffic.  (Round 6: loads under a per-chunk branch leave
+    // hipcc's waitcnt pass unable to count the younger loads in flight, so each plane's LDS write waited for
+    // vmcnt(0) -- for the NEXT plane's loads too, issued a row earlier: the convc1-fused instance, whose rows have
+    // no output stores to pad the count, ran its two-row prefetch one row deep.  Alternating A/B at config #3,
+    // gpurun_out/r6g: convc1-fused lookup 0.1151 / 0.1179 -> 0.1101 / 0.1061 ms.  The plain lookup keeps the
+    // branches: its 27 output stores per row keep the waits precise enough, and the extra load instructions of
+    // the masked chunks cost it 5 %, 0.1338 -> 0.1404 ms, in the same A/B.)
+    constexpr bool UNCOND = PROJ == 1;   // (PROJ 2, fp32 blocks at one workgroup per CU: branches, -2 % otherwise)
+    constexpr int OOB = 0x7fff0000;
+    auto load_chunk = [&](Chunk &dst, int o) {
+        if constexpr (!UNCOND) {   // (tuning "lookup_ldpol" 2: the plane loads' cache-policy A/B of round 2)
+            if (A.ldpol == 2) {
+                if constexpr (C::CB == 16)
+                    dst = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, o, 0, 2));
+                else dst = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_in, o, 0, 2));
+                return;
+            }
+        }
+        if constexpr (C::CB == 16) dst = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, o, 0, 0));
+        else dst = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_in, o, 0, 0));
+    };
+    auto load_plane = [&](int wp, int plane_bytes, Chunk (&dst)[C::MAXCH]) {
+#pragma unroll
+        for (int k = 0; k < C::MAXCH; ++k) {
+            if constexpr ((ABL & 2) != 0) dst[k] = Chunk{(unsigned)k};
+            else if constexpr (UNCOND)   // (bricks keep whole planes: same plane stride)
+                load_chunk(dst[k], (pk[k] & (1u << (16 + wp))) ? voff[k] + wp * plane_bytes : OOB);
+            else if (pk[k] & (1u << (16 + wp)))
+                load_chunk(dst[k], voff[k] + wp * plane_bytes);
+        }
+    };
+    auto write_plane = [&](int slot, int wp, const Chunk (&src)[C::MAXCH]) {
+        unsigned char *sb = smem + C::GUARD + slot * C::SLOT;
+#pragma unroll
+        for (int k = 0; k < C::MAXCH; ++k) {
+            if (pk[k] & (1u << (16 + wp))) {
+                const unsigned o = (pk[k] & 0xffffu) * 8;
+                if constexpr (C::CB == 16) {
+                    u32x2 lo = {src[k][0], src[k][1]}, hi = {src[k][2], src[k][3]};
+                    *reinterpret_cast<u32x2 *>(sb + o) = lo;
+                    *reinterpret_cast<u32x2 *>(sb + o + 8) = hi;
+                } else {
+                    *reinterpret_cast<u32x2 *>(sb + o) = src[k];
+                }
+            }
+        }
+    };
+
+    // output rows [a0, a0 + NA) of level l; planes a0 .. a0 + NA of the window.  pre: this level's pipeline was
+    // started by the previous level (XLP); lnx: the next level of the walk to start under this one's last rows
+    // (-1: none)
+    auto level = [&](int l, auto nu_c, auto na_c, int a0, bool pre, int lnx) {
         constexpr int NU = decltype(nu_c)::value;
         constexpr int NA = decltype(na_c)::value;
         float *obase = A.out + ((long long)b * A.Ltot + l) * n3 * Nq;   // wave-uniform
@@ -390,21 +545,11 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
                 }
             return;
         }
-        const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
-        const float sc = (float)(1 << l);
+        const LevelGeo g = geo(l);
+        const int Hl = g.Hl, Wl = g.Wl, Dl = g.Dl, NC = g.NC, ZW = g.ZW, SQ = g.SQ;
         WinAxes ax;
-        window_axes(cy / sc, cx / sc, cz / sc, Hl, Wl, Dl, A.legacy, ax);
-        // (a NaN / huge coordinate moves the window far outside the level: every
-        //  weight below is then folded to 0 and the output is 0, as the reference's)
-        const int ih = (int)ax.kh - R, iu = (int)ax.ku - R, iv = (int)ax.kv - R;
-        const int NC = min(NW, Wl);
-        const int ZW = min(Dpl, C::ZWMAX);
-        const int cs = min(max(iu, 0), Wl - NC);
-        const int za = min(max(iv & ~(CE - 1), 0), Dpl - ZW);
-        const int SQ = NC * ZW * ES + 8;
-        const int ZC = ZW / CE;                          // chunks per column
-        const int nch = 64 * NC * ZC;                    // chunks per plane slot
-        const int plane_bytes = Wl * Dpl * ES;
+        int ih, iu, iv, cs, za;
+        window(l, g, ax, ih, iu, iv, cs, za);
 
         // per-axis weights (reference float32 arithmetic), zero padding folded in
         float wv0[n], wv1[n];
@@ -438,97 +583,13 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
         }
 
         stamp(1);
-        __syncthreads();   // previous level's LDS reads are done; table free
-        if (wave == 0) {
-            tab[0][lane] = min(max(ih, -2 * NW), Hl);
-            tab[1][lane] = cs;
-            tab[2][lane] = za;
-            tab[3][lane] = iv;
-            tab[4][lane] = iu;
+        if (!pre) {
+            __syncthreads();   // previous level's LDS reads are done; table free
+            if (wave == 0) write_tab(g, ih, cs, za, iv, iu);
+            __syncthreads();
+            stamp(2);
+            chunk_setup(g, 3);
         }
-        __syncthreads();
-        stamp(2);
-        // a bricked level (DVC_BRICKED, bit l of A.brick): voxel (y, x, z) at
-        // ((y * W/8 + x/8) * Dp/8 + z/8) * 64 + (x%8) * 8 + z%8, i.e. (1, 8, 8) bricks of one 128-byte
-        // line, so the strip of a window plane touches lines of 8 columns x 8 z instead of 2 x 32
-        // (Dp = 32) or 1 x 64; the strip's z-chunk that the query's run never reaches is not loaded.
-        const bool bk8 = (A.brick >> l) & 1;
-
-        // this thread's chunks of every plane: (query j, column c, z-chunk k).  voff =
-        // byte offset of the chunk in window plane 0; window plane wp adds wp * plane_bytes.
-        // pk = LDS offset / 8 (low 16 bits; 0xffff: no chunk) | mask of the window planes
-        // inside the level (high 16 bits).  Planes outside it are not loaded: their LDS
-        // slots keep earlier, finite data, and their weights are 0.
-        int voff[C::MAXCH];
-        unsigned pk[C::MAXCH];
-        // chunk index -> (query, column, z-chunk) by float reciprocals: idx < 2^12 and divisors <= 60, so
-        // (idx + 0.5) / d sits >= 1/120 from an integer while the float error is < 2^-11 (no integer divides)
-        const int NCZ = NC * ZC;
-        const float inv_ncz = 1.0f / (float)NCZ, inv_zc = 1.0f / (float)ZC;
-        // byte offsets fit 32 bits (the buffer covers one tile's rows: 64 x row_stride x ES < 2^31)
-        const int rs_b = (int)A.row_stride * ES, lev_b = (int)A.off[l] * ES;
-#pragma unroll
-        for (int k = 0; k < C::MAXCH; ++k) {
-            const int idx = tid + k * C::THREADS;
-            const int j = (int)(((float)idx + 0.5f) * inv_ncz);
-            const int rem = idx - j * NCZ;
-            const int c = (int)(((float)rem + 0.5f) * inv_zc);
-            const int zc = rem - c * ZC;
-            const bool ok = idx < nch;
-            const int jj = ok ? j : 0;
-            const int ihj = tab[0][jj];
-            const int plo = min(max(-ihj, 0), NW), phi = min(max(Hl - ihj, 0), NW);
-            unsigned mask = ok && jj < nvalid ? ((1u << phi) - 1u) & ~((1u << plo) - 1u) : 0u;
-            // only chunks the window reads: its columns [iu, iu + NW) (the strip is clamped into the level, so
-            // at a border it holds columns outside the window) and the z-chunks its run [iv, iv + NW) reaches.
-            // Every other chunk is read with weight 0 or not at all (coff clamps into the window's columns).
-            {
-                const int zs = tab[2][jj] + zc * CE, ivj = tab[3][jj], xw = tab[1][jj] + c - tab[4][jj];
-                if (!(zs < ivj + NW && zs + CE > ivj) || (unsigned)xw >= (unsigned)NW) mask = 0u;
-            }
-            pk[k] = (ok ? (unsigned)(jj * SQ + (c * ZW + zc * CE) * ES) >> 3 : 0xffffu) | (mask << 16);
-            const int zs = tab[2][jj] + zc * CE, x = tab[1][jj] + c;
-            const int inplane = bk8 ? (((x >> 3) * (Dpl >> 3) + (zs >> 3)) * 64 + (x & 7) * 8 + (zs & 7))
-                                    : x * Dpl + zs;
-            voff[k] = jj * rs_b + lev_b + (ihj * Wl * Dpl + inplane) * ES;
-        }
-        using Chunk = typename std::conditional<C::CB == 16, u32x4, u32x2>::type;
-        auto load_plane = [&](int wp, Chunk (&st)[C::MAXCH]) {
-#pragma unroll
-            for (int k = 0; k < C::MAXCH; ++k) {
-                if constexpr ((ABL & 2) != 0) st[k] = Chunk{(unsigned)k};
-                else if (pk[k] & (1u << (16 + wp))) {
-                    const int o = voff[k] + wp * plane_bytes;   // (bricks keep whole planes: same plane stride)
-                    if constexpr (C::CB == 16) {
-                        if (ldpol == 2)
-                            st[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, o, 0, 2));
-                        else
-                            st[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_in, o, 0, 0));
-                    } else {
-                        if (ldpol == 2)
-                            st[k] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_in, o, 0, 2));
-                        else
-                            st[k] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_in, o, 0, 0));
-                    }
-                }
-            }
-        };
-        auto write_plane = [&](int slot, int wp, const Chunk (&st)[C::MAXCH]) {
-            unsigned char *sb = smem + C::GUARD + slot * C::SLOT;
-#pragma unroll
-            for (int k = 0; k < C::MAXCH; ++k) {
-                if (pk[k] & (1u << (16 + wp))) {
-                    const unsigned o = (pk[k] & 0xffffu) * 8;
-                    if constexpr (C::CB == 16) {
-                        u32x2 lo = {st[k][0], st[k][1]}, hi = {st[k][2], st[k][3]};
-                        *reinterpret_cast<u32x2 *>(sb + o) = lo;
-                        *reinterpret_cast<u32x2 *>(sb + o + 8) = hi;
-                    } else {
-                        *reinterpret_cast<u32x2 *>(sb + o) = st[k];
-                    }
-                }
-            }
-        };
         constexpr bool BF = std::is_same<T, bf16_t>::value;
         unsigned sel_e = 0, sel_o = 0;   // bf16: v_perm selectors of this lane's run parity (same for every column)
         if constexpr (BF) bf16_run_selectors((rz & 1) != 0, sel_e, sel_o);
@@ -547,27 +608,53 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
         // row p - 2 (into the slot of plane p - 2, read by rows p - 3 and p - 2), and its register set then takes
         // plane p + PD, loaded PD - 1 rows ahead of its own write
         constexpr int NPL = NA + 1;   // window planes this workgroup reads
-        constexpr int PD = PROJ ? 2 : C::PD;   // (the convc1 consumer's 96 accumulators: keep the registers)
-        Chunk st[PD][C::MAXCH];
         ZRun<n> zp[NU + 1];       // z-lerped columns of the lower plane of the current row
+        // planes staged in registers (relative plane p in st[p % PD]): per level unless XLP carries them over
+        Chunk st_l[PD][C::MAXCH];
+        Chunk(*st)[C::MAXCH] = XLP ? st_x : st_l;
+        if (!pre) {
+            if constexpr (XLP) {
+                // (the staging registers carry nothing into a level that was not prefetched: an arbitrary value
+                //  lets the register allocator end their live ranges at the previous level's last write -- the
+                //  plane loads and LDS writes are predicated per chunk, which it cannot match up)
 #pragma unroll
-        for (int p = 0; p < PD; ++p)
-            if (p < NPL) load_plane(a0 + p, st[p]);
-        write_plane(0, a0, st[0]);
-        if (PD < NPL) load_plane(a0 + PD, st[0]);
-        stamp(3);
-        __syncthreads();          // plane a0 in slot 0
+                for (int p = 0; p < PD; ++p)
+#pragma unroll
+                    for (int k = 0; k < C::MAXCH; ++k) st[p][k] = __builtin_nondeterministic_value(st[p][k]);
+            }
+#pragma unroll
+            for (int p = 0; p < PD; ++p)
+                if (p < NPL) load_plane(a0 + p, g.plane_bytes, st[p]);
+            write_plane(0, a0, st[0]);
+            if (PD < NPL) load_plane(a0 + PD, g.plane_bytes, st[0]);
+            stamp(3);
+            __syncthreads();          // plane a0 in slot 0
+        }
+        // (pre: plane 0 was written to slot 0 before the previous level's last row barrier, planes 1 and 2 are in
+        //  flight in st[1] and st[0])
         stamp(4);
 #pragma unroll
         for (int k = 0; k <= NU; ++k) lerp_col(0, k, zp[k]);
         write_plane(1, a0 + 1, st[1 % PD]);
-        if (PD > 2 && PD + 1 < NPL) load_plane(a0 + PD + 1, st[1 % PD]);
+        if (PD > 2 && PD + 1 < NPL) load_plane(a0 + PD + 1, g.plane_bytes, st[1 % PD]);
         __syncthreads();          // plane a0 + 1 in slot 1
         stamp(5);
+        LevelGeo gx{};            // (XLP) the next level's geometry
 #pragma unroll
         for (int ia = 0; ia < NA; ++ia) {
             const int a = a0 + ia;
-            if (PD == 2 && ia + 3 < NPL) load_plane(a + 3, st[(ia + 1) & 1]);   // in flight for two rows
+            if (PD == 2 && ia + 3 < NPL) load_plane(a + 3, g.plane_bytes, st[(ia + 1) & 1]);   // in flight for two rows
+            if constexpr (XLP && PD == 2 && NA >= 3) {
+                if (ia == NA - 1 && lnx >= 0) {
+                    // XLP: this level's loads are all issued (voff is dead) and its last plane was written at the end
+                    // of row NA - 2 (pk is dead, st[0] and st[1] free): the next level's chunk addresses, LDS
+                    // offsets and masks, and its plane 0 and 1 loads
+                    gx = geo(lnx);
+                    chunk_setup(gx, 3);
+                    load_plane(0, gx.plane_bytes, st[0]);
+                    load_plane(1, gx.plane_bytes, st[1]);
+                }
+            }
             float wy0, wy1;
             axis_weights(ax.ph, ax.kh, a - R, ax.hs, ax.hs, wy0, wy1);
             wy0 = (unsigned)(ih + a) < (unsigned)Hl ? wy0 : 0.0f;
@@ -671,7 +758,23 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
             }
             if (ia + 2 < NPL) {   // plane a+2 into the slot of plane a (read in row a-1)
                 write_plane(ia & 1, a + 2, st[(ia + 2) % PD]);
-                if (PD > 2 && ia + 2 + PD < NPL) load_plane(a + 2 + PD, st[(ia + 2) % PD]);
+                if (PD > 2 && ia + 2 + PD < NPL) load_plane(a + 2 + PD, g.plane_bytes, st[(ia + 2) % PD]);
+            }
+            if constexpr (XLP && PD == 2 && NA >= 3) {
+                if (ia == NA - 3 && lnx >= 0 && wave == 0) {
+                    // XLP: the next level's window table (read after this row's barrier; this level read its own
+                    // before its first row)
+                    const LevelGeo gn = geo(lnx);
+                    WinAxes axn;
+                    int ihn, iun, ivn, csn, zan;
+                    window(lnx, gn, axn, ihn, iun, ivn, csn, zan);
+                    write_tab(gn, ihn, csn, zan, ivn, iun);
+                }
+                if (ia == NA - 1 && lnx >= 0) {
+                    // XLP: the next level's plane 0 into slot 0 (last read in row NA - 2), its plane 2 loads into st[0]
+                    write_plane(0, 0, st[0]);
+                    load_plane(2, gx.plane_bytes, st[0]);
+                }
             }
             __syncthreads();
             stamp(6 + ia);
@@ -686,22 +789,32 @@ __global__ __launch_bounds__(64 * (TileCfg<T, R, NWV>::NWAVES + (PROJ ? 1 : 0)),
     constexpr int NA_FULL = ACH > 0 ? ACH : n;
     constexpr int NA_TAIL = ACH > 0 ? n - ACH * (NCH_A - 1) : n;    // rows of the last chunk
     const int a0 = ACH > 0 ? (int)blockIdx.z * ACH : 0;
-    auto rows = [&](int l, auto nu_c) {
-        if (NA_TAIL == NA_FULL || a0 + NA_FULL <= n) level(l, nu_c, std::integral_constant<int, NA_FULL>{}, a0);
-        else level(l, nu_c, std::integral_constant<int, NA_TAIL>{}, a0);
+    auto rows = [&](int l, auto nu_c, bool pre, int lnx) {
+        if (NA_TAIL == NA_FULL || a0 + NA_FULL <= n) level(l, nu_c, std::integral_constant<int, NA_FULL>{}, a0, pre, lnx);
+        else level(l, nu_c, std::integral_constant<int, NA_TAIL>{}, a0, pre, lnx);
     };
+    auto walk_level = [&](int li) { return A.l0 + (rev ? A.nl - 1 - li : li); };
+    auto runs = [&](int l) { return !A.zero[l] && !A.generic[l]; };   // levels with a row pipeline
+    bool started = false;   // a level with a row pipeline has run (XLP: the next one is prefetched)
     for (int li = li0; li < li1; ++li) {
-        const int l = A.l0 + (rev ? A.nl - 1 - li : li);
+        const int l = walk_level(li);
         if (A.generic[l] && !A.zero[l]) continue;   // legacy level with W != D: k_lookup_generic
+        int lnx = -1;
+        if (xlp && runs(l))
+            for (int lj = li + 1; lj < li1 && lnx < 0; ++lj)
+                if (runs(walk_level(lj))) lnx = walk_level(lj);
+        const bool pre = xlp && started && runs(l);
         if constexpr (BAL) {
-            if (REM > 0 && wave < REM) rows(l, std::integral_constant<int, FLO + 1>{});
-            else rows(l, std::integral_constant<int, FLO>{});
+            if (REM > 0 && wave < REM) rows(l, std::integral_constant<int, FLO + 1>{}, pre, lnx);
+            else rows(l, std::integral_constant<int, FLO>{}, pre, lnx);
         } else if (NU_LAST == C::COLS || wave < C::NWAVES - 1) {
-            rows(l, std::integral_constant<int, C::COLS>{});
+            rows(l, std::integral_constant<int, C::COLS>{}, pre, lnx);
         } else {
-            rows(l, std::integral_constant<int, NU_LAST>{});
+            rows(l, std::integral_constant<int, NU_LAST>{}, pre, lnx);
         }
+        started |= runs(l);
         trace_level = 0;
+        ++trace_li;
     }
     stamp(15);
 }

@@ -4,9 +4,9 @@ namespace dvc {
 
 // convc1-fused instances of k_lookup_tile (lookup_tile.h; radii whose (2r+1) x 3 row values fit one
 // 32-k slice) and their weight packing
-#define DVC_TILE_PROJ(T, R) template __global__ void k_lookup_tile<T, R, true, 0, 1, 0>(LookupArgs);
+#define DVC_TILE_PROJ(T, R) template __global__ void k_lookup_tile<T, R, true, 0, 1, 0, 0, -1, DVC_PROJ_XLP>(LookupArgs);
 // fp32 pyramids: the exact split consumer (PROJ 2, bf16 hi/lo operands, lookup_tile.h)
-#define DVC_TILE_PROJX(R) template __global__ void k_lookup_tile<float, R, true, 0, 2, 0>(LookupArgs);
+#define DVC_TILE_PROJX(R) template __global__ void k_lookup_tile<float, R, true, 0, 2, 0, 0, -1, DVC_PROJ_XLP>(LookupArgs);
 DVC_TILE_PROJX(1) DVC_TILE_PROJX(2) DVC_TILE_PROJX(3) DVC_TILE_PROJX(4)
 DVC_TILE_PROJ(bf16_t, 1) DVC_TILE_PROJ(bf16_t, 2) DVC_TILE_PROJ(bf16_t, 3) DVC_TILE_PROJ(bf16_t, 4)
 DVC_TILE_PROJ(f16_t, 1) DVC_TILE_PROJ(f16_t, 2) DVC_TILE_PROJ(f16_t, 3) DVC_TILE_PROJ(f16_t, 4)

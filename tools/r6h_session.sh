@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round 6: tile-kernel GPU tests on the final lookup_tile.h, then alternating A/B against libdvccorr_base.so (HEAD
+# before the round-6 tile changes) for the convc1-fused and the default line.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/${TAG:-r6h}; mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu ${TESTS:-tests/test_gpu_proj.py tests/test_gpu_proj_grad.py tests/test_gpu_epe.py tests/test_gpu_parity.py tests/test_gpu_bricked.py tests/test_gpu_scale.py tests/test_gpu_amp.py} > $OUT/pytest.log 2>&1
+rc=$?; tail -3 $OUT/pytest.log; grep -E "^FAILED" $OUT/pytest.log | head -5; [ $rc -ne 0 ] && exit $rc
+L=raft-dvc_amd/dvccorr
+one() {  # name lib args...
+  local name=$1 lib=$2; shift 2
+  DVCCORR_LIB=$PWD/$L/$lib timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 10 "$@" > $OUT/$name.json 2> $OUT/$name.err || { tail -5 $OUT/$name.err; exit 3; }
+  python3 -c "import json;d=json.loads(open('$OUT/$name.json').read().strip().splitlines()[-1]);print('$name', round(d['ms_per_step'],4), d['lookup_avg_ms'], d['roofline']['frac'])"
+}
+for i in 1 2; do
+  one c_new_$i libdvccorr.so --convc1
+  one c_base_$i libdvccorr_base.so --convc1
+done
+for i in 1 2; do
+  one n_new_$i libdvccorr.so
+  one n_base_$i libdvccorr_base.so
+  one f32c_new_$i libdvccorr.so --convc1 --precision fp32
+  one f32c_base_$i libdvccorr_base.so --convc1 --precision fp32
+done
