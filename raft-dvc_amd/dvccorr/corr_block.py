@@ -198,7 +198,7 @@ class CorrBlock(_Block):
     trainer.py:249-257).  fp32 blocks run the same kernels on bf16 hi/lo splits of every operand, ~2^-16 relative
     per product -- not the exact fp32 sums of the reference's autograd: the golden gradients agree to <= 1e-5
     (tests/test_gpu_backward.py, GRAD_TOL).  dvccorr._lib.set_tuning("bwd_mfma", 0) selects the exact fp32 VALU kernels
-    (per calling thread)."""
+    (process-wide, so also for the backward that the autograd engine runs on its own thread)."""
 
     def __init__(self, fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int = 4, radius: int = 4,
                  legacy_wd_swap: bool = False, *, precision: Optional[str] = None, build: str = "gemm",
