@@ -246,6 +246,29 @@ def test_bricked_levels(shape, L, expect):
             assert torch.equal(torch.sort(idx).values, torch.arange(h * w * lay.Dp[l]))
 
 
+def test_brick_min_dp_knob():
+    """Tuning "brick_min_dp" (round 6 A/B: level 1 of config #3 in (1, 8, 8) bricks too) lowers the bricked-level
+    threshold to Dp >= 16 for every layout decided after it, is refused for other values, and the product default
+    (32) comes back; the knob is process-global like every dvc_set_tuning key."""
+    import threading
+    from dvccorr import _lib
+    lay = _lib.layout(32, 32, 32, 4, 32)
+    assert _lib.bricked_levels(lay) == 0b0001
+    seen = []
+    try:
+        _lib.set_tuning("brick_min_dp", 16)
+        t = threading.Thread(target=lambda: seen.append(_lib.bricked_levels(_lib.layout(32, 32, 32, 4, 32))))
+        t.start()
+        t.join()
+        assert _lib.bricked_levels(lay) == 0b0011
+        assert seen == [0b0011], "the knob did not reach another host thread"
+        with pytest.raises(ValueError):   # (DVC_ERR_INVALID)
+            _lib.set_tuning("brick_min_dp", 8)
+    finally:
+        _lib.set_tuning("brick_min_dp", 32)
+    assert _lib.bricked_levels(lay) == 0b0001
+
+
 def test_brick_flag_policy(monkeypatch):
     """The materialised block bricks its wide levels only for the tile kernel's cases."""
     from dvccorr import _lib
