@@ -100,6 +100,9 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--tune", default="", help="diagnostics: comma list key=value of dvc_set_tuning knobs")
     ap.add_argument("--cpu-rows", type=int, default=4096, help="query rows of the bounded CPU sample")
+    ap.add_argument("--coord-fields", type=int, default=0,
+                    help="diagnostics: distinct coordinate fields the step's lookups cycle through (0 = one per lookup, "
+                         "the metric's setting; 1 = every lookup at the same coordinates: the reuse bound)")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
     return ap.parse_args(argv)
 
@@ -409,7 +412,9 @@ def main():
     f1 = torch.randn(B, C, S, S, S, generator=g)
     f2 = torch.randn(B, C, S, S, S, generator=g)
     base = dvccorr.coords_grid_3d(B, S, S, S, torch.device("cpu"))
-    coords_list = [base + synthetic_flow(args.flow, B, S, args.max_flow, g) for _ in range(args.iters)]
+    nfields = args.iters if args.coord_fields <= 0 else min(args.coord_fields, args.iters)
+    fields = [base + synthetic_flow(args.flow, B, S, args.max_flow, g) for _ in range(nfields)]
+    coords_list = [fields[i % nfields] for i in range(args.iters)]
     if shard_diag:
         h0, h1 = slab_bounds(S, args.shard_of, args.shard_rank)
     else:
@@ -571,7 +576,7 @@ def main():
             "data": (f"synthetic: N(0,1) feature maps, coords = identity + "
                      + (f"U(-{args.max_flow:g},{args.max_flow:g}) i.i.d. per voxel" if args.flow == "random" else
                         f"a smooth field (3 sinusoids per axis, |flow| <= {args.max_flow:g})")
-                     + f", {args.iters} coord fields per step"),
+                     + f", {args.iters if args.coord_fields <= 0 else min(args.coord_fields, args.iters)} coord fields per step"),
             "config": {"workload": f"corr build + {args.iters} lookups{f' + convc1 ({args.convc1})' if args.convc1 else ''}, {S}^3 x {C} fmaps ({args.encoder * S}^3 "
                                    f"input, 1/{args.encoder} encoder), L={L}, r={R}, {args.impl}, {args.precision} build / fp32 lookup",
                        "global_batch": B if strong else B * world, "query_voxels": nq_total, "levels": L,

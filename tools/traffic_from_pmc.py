@@ -19,12 +19,11 @@ def pick(d, prefix):
 
 note = "HBM bytes per launch: 2 x FETCH_SIZE + WRITE_SIZE (KB x 1024), rocprofv3 --pmc, gfx950; source: {}"
 out = {}
-m6 = json.load(open(os.path.join(P, "r06", "r06_pmc_mat32.json")))
+m6 = json.load(open(os.path.join(P, "r06", "r06_pmc_mat32_z.json")))
 out["materialised_bf16_32_L4_r4_n1"] = {
     "build_hbm_bytes_per_launch": hbm(pick(m6, "k_build_bf16_2b")),
     "lookup_hbm_bytes_per_launch": hbm(pick(m6, "k_lookup_tile")),
-    "note": note.format("profiles/r06/r06_pmc_mat32.json (round 6; tree 2e233ac = the round-6 lookup and build kernels; "
-                        "DVC_BRICKED level 0)")}
+    "note": note.format("profiles/r06/r06_pmc_mat32_z.json (round-6 closing tree; DVC_BRICKED level 0)")}
 mp = json.load(open(os.path.join(P, "r06", "r06_pmc_mat32_convc1.json")))
 out["materialised_bf16_32_L4_r4_n1_convc1_fused"] = {
     "lookup_hbm_bytes_per_launch": hbm(pick(mp, "k_lookup_tile")),
