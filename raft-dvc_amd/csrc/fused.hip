@@ -21,6 +21,7 @@
 
 #include "common.h"
 #include "lookup_common.h"
+#include "fused_common.h"
 
 namespace dvc {
 
@@ -237,10 +238,10 @@ __global__ void k_fused_box(const bf16_t *, const bf16_t *, LookupArgs, int, lon
 template <int R, int NWV, int TY, int TX, int TZ, typename E>
 static void launch_fused_box(const bf16_t *Q, const bf16_t *Tt, const LookupArgs &A, int Cp, long long t_rows,
                              int Hq, int Wq, int Dq, float scale, hipStream_t s) {
-    // boxes in 4 x 4 x 2 groups, padded to a multiple of 8 workgroups (one range per XCD)
-    const long long ngy = ((Hq + TY - 1) / TY + 3) / 4, ngx = ((Wq + TX - 1) / TX + 3) / 4,
-                    ngz = ((Dq + TZ - 1) / TZ + 1) / 2;
-    const long long tiles = (long long)A.B * ngy * ngx * ngz * 32;
+    // boxes in kBoxGY x kBoxGX x kBoxGZ groups (fused_common.h), padded to a multiple of 8 workgroups (one range per XCD)
+    const long long ngy = ((Hq + TY - 1) / TY + kBoxGY - 1) / kBoxGY, ngx = ((Wq + TX - 1) / TX + kBoxGX - 1) / kBoxGX,
+                    ngz = ((Dq + TZ - 1) / TZ + kBoxGZ - 1) / kBoxGZ;
+    const long long tiles = (long long)A.B * ngy * ngx * ngz * (kBoxGY * kBoxGX * kBoxGZ);
     const unsigned grid = (unsigned)(8 * ((tiles + 7) / 8));
 #if DVC_DIAG
     if constexpr (R == 4 && NWV == 8 && TY == 2 && TX == 2 && TZ == 16 && std::is_same<E, bf16_t>::value) {

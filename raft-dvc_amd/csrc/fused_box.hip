@@ -72,8 +72,8 @@ __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__re
 
     // XCD-aware box order: workgroup g runs on XCD g % 8 (round-robin dispatch), so each
     // XCD gets a contiguous range of logical boxes, walked in groups of GY x GX x GZ
-    // neighbouring boxes whose unions overlap in that XCD's L2.
-    constexpr int GY = 4, GX = 4, GZ = 2;
+    // neighbouring boxes whose unions overlap in that XCD's L2 (kBoxG*, fused_common.h).
+    constexpr int GY = kBoxGY, GX = kBoxGX, GZ = kBoxGZ;   // (fused_common.h)
     const int nty = (Hq + TY - 1) / TY, ntx = (Wq + TX - 1) / TX, ntz = (Dq + TZ - 1) / TZ;
     const int ngy = (nty + GY - 1) / GY, ngx = (ntx + GX - 1) / GX, ngz = (ntz + GZ - 1) / GZ;
     const int per_b = ngy * ngx * ngz * (GY * GX * GZ);

@@ -87,7 +87,7 @@ __global__ __launch_bounds__(256, 1) void k_fused_box_f32(const float *__restric
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
     // XCD-aware box order (as k_fused_box): each XCD a contiguous range of boxes in 4 x 4 x 2 groups
-    constexpr int GY = 4, GX = 4, GZ = 2;
+    constexpr int GY = kBoxGY, GX = kBoxGX, GZ = kBoxGZ;   // (fused_common.h)
     const int nty = (Hq + TY - 1) / TY, ntx = (Wq + TX - 1) / TX, ntz = (Dq + TZ - 1) / TZ;
     const int ngy = (nty + GY - 1) / GY, ngx = (ntx + GX - 1) / GX, ngz = (ntz + GZ - 1) / GZ;
     const int per_b = ngy * ngx * ngz * (GY * GX * GZ);
@@ -400,8 +400,9 @@ __global__ __launch_bounds__(256, 1) void k_fused_box_f32(const float *__restric
 template <int R>
 static void launch_box_f32_r(const float *Q, const float *Tt, const LookupArgs &A, int Cp, long long t_rows, int Hq,
                              int Wq, int Dq, float scale, hipStream_t s) {
-    const long long ngy = ((Hq + 1) / 2 + 3) / 4, ngx = ((Wq + 1) / 2 + 3) / 4, ngz = ((Dq + 15) / 16 + 1) / 2;
-    const long long tiles = (long long)A.B * ngy * ngx * ngz * 32;
+    const long long ngy = ((Hq + 1) / 2 + kBoxGY - 1) / kBoxGY, ngx = ((Wq + 1) / 2 + kBoxGX - 1) / kBoxGX,
+                    ngz = ((Dq + 15) / 16 + kBoxGZ - 1) / kBoxGZ;
+    const long long tiles = (long long)A.B * ngy * ngx * ngz * (kBoxGY * kBoxGX * kBoxGZ);
     const unsigned grid = (unsigned)(8 * ((tiles + 7) / 8));
     switch (Cp / 32) {
     case 1: k_fused_box_f32<R, 1><<<grid, 256, 0, s>>>(Q, Tt, A, Cp, t_rows, Hq, Wq, Dq, scale); break;

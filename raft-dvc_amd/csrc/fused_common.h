@@ -56,6 +56,12 @@ template <> struct E16<f16_t> {
     static __device__ __forceinline__ float hi(unsigned w) { return bits16_to_f32<f16_t>(w >> 16); }
 };
 
+// The box group each XCD runs at once in the on-the-fly box kernels (k_fused_box, k_fused_box_f32): 32 boxes (one per
+// CU of an XCD) as 8 x 4 x 1 boxes of 2 x 2 x 16 queries = a 16 x 8 x 16 query block, whose level-0 union of windows
+// is ~11 % smaller than the 4 x 4 x 2 group's (8 x 8 x 32 queries).  Round 6 A/B at config #5 (gpurun_out/r6l):
+// bf16 10.70 / 10.68 -> 10.38 / 10.32 ms per lookup; fp32 unchanged.  Kernels and host grids share these.
+constexpr int kBoxGY = 8, kBoxGX = 4, kBoxGZ = 1;
+
 template <int n> struct BRun {
     f32x2 p[n / 2];
     float t;
