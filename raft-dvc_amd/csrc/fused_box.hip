@@ -13,7 +13,7 @@
 //            4 queries, scales and rounds them to bf16 exactly as the materialised build
 //            rounds the corr volume, and writes each value that falls in its query's
 //            integer window straight into that query's dense (2r+2)^3 window in LDS
-//            (the others go to a per-lane scratch slot: no branches, no staging).
+//            (the other lanes masked off: no staging).
 //   phase 2  the window walk of lookup_tile.hip (z-lerp per column run, then the four
 //            (y, x) bilinear terms, packed f32), each wave a few output columns.
 //
@@ -48,8 +48,7 @@ template <int R, int NWAVES> struct BoxCfg {
     static constexpr int WROW = (NW + 2) * 2;                     // bytes of one window z-row (bf16)
     static constexpr int WQ = ((NW * NW * WROW + 15) & ~15) + 16; // bytes per query window (16-B aligned)
     static constexpr int GUARD = 64;
-    static constexpr int TRASH = GUARD + 64 * WQ;                 // per-lane scratch slots
-    static constexpr int LDS = (TRASH + 64 * 4 + GUARD + 15) & ~15;
+    static constexpr int LDS = (GUARD + 64 * WQ + GUARD + 15) & ~15;
     static constexpr int COLS = NWAVES >= 8 ? 2 : 3;              // output columns per wave (phase 2)
 };
 
@@ -135,7 +134,6 @@ __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__re
     const int vstep = buni((int)(chstep_v * Nq * 4));
     const int out_bytes = buni((int)(n * n * Nq * 4));
     const f32x2 sc2 = splat2(scale);   // materialised: no op_sel broadcast beside MFMAs (common.h)
-    const int trash = C::TRASH + lane * 4;
     unsigned sink = 0;
     const int u0 = wave * C::COLS;
     __syncthreads();   // LDS cleared
@@ -273,10 +271,10 @@ __global__ __launch_bounds__(64 * NWAVES, 1) void k_fused_box(const bf16_t *__re
                     const bool rok = rowok[j];
                     const int t0 = z0 - ov[j];                   // stored-row offset of this lane's first pair
                     const int base = wb[j] + rowu;
-                    const int a0 = rok && (unsigned)t0 <= (unsigned)NW ? base : trash;
-                    const int a1 = rok && (unsigned)(t0 + 2) <= (unsigned)NW ? base + 4 : trash;
-                    *reinterpret_cast<unsigned *>(smem + a0) = p01;
-                    *reinterpret_cast<unsigned *>(smem + a1) = p23;
+                    // values outside the query's window: the lane is masked off (round 6; a store of every lane with
+                    // those values sent to a per-lane scratch slot was 1 % slower at config #5)
+                    if (rok && (unsigned)t0 <= (unsigned)NW) *reinterpret_cast<unsigned *>(smem + base) = p01;
+                    if (rok && (unsigned)(t0 + 2) <= (unsigned)NW) *reinterpret_cast<unsigned *>(smem + base + 4) = p23;
                 }
             };
             // two operand sets in flight; the MFMAs of iteration k + 1 are issued before the

@@ -41,8 +41,7 @@ template <int R> struct BoxF32Cfg {
     // same offset in every window) hits 32 distinct bank pairs per 32-lane group
     static constexpr int WQ = SLICE + 4 * ((2 - SLICE / 4) % 64 + 64) % 256;
     static constexpr int GUARD = 64;
-    static constexpr int TRASH = GUARD + 64 * WQ;           // per-lane scratch slots for values outside a window
-    static constexpr int LDS = (TRASH + 64 * 4 + GUARD + 15) & ~15;
+    static constexpr int LDS = (GUARD + 64 * WQ + GUARD + 15) & ~15;
     static constexpr int NWAVES = 4, COLS = 3;
     static_assert((WQ / 4) % 64 == 2 && WQ % 8 == 0, "window stride");
     static_assert(LDS <= 160 * 1024, "LDS");
@@ -148,7 +147,6 @@ __global__ __launch_bounds__(256, 1) void k_fused_box_f32(const float *__restric
     const int q4 = active ? (int)(qg * 4) : 0x7ffffff0;
     const int vstep = buni((int)(chstep_v * Nq * 4));
     const int out_bytes = buni((int)(n * n * Nq * 4));
-    const int trash = C::TRASH + lane * 4;
     const int u0 = wave * C::COLS;
     __syncthreads();   // LDS cleared
 
@@ -310,7 +308,7 @@ __global__ __launch_bounds__(256, 1) void k_fused_box_f32(const float *__restric
 #pragma unroll
                         for (int i = 0; i < 4; ++i) {
                             const bool in = rowok[j] && (unsigned)(zl + i - ov[j]) < (unsigned)NW;
-                            *reinterpret_cast<float *>(smem + (in ? base + 4 * i : trash)) = acc[j][i] * scale;
+                            if (in) *reinterpret_cast<float *>(smem + base + 4 * i) = acc[j][i] * scale;   // (masked)
                         }
                     }
                 };

@@ -269,6 +269,8 @@ __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict_
                     const bool rok = (unsigned)(y - oh[j]) < (unsigned)NW && (unsigned)(x - ou[j]) < (unsigned)NW;
                     const int t0 = z0 - ov[j];
                     const int base = wb[j] + rowu;
+                    // (every lane stores, out-of-window values to its scratch slot: masking the lanes off as
+                    // k_fused_box does measured 0.3 % slower here, round 6)
                     const int a0 = rok && (unsigned)t0 <= (unsigned)NW ? base : trash;
                     const int a1 = rok && (unsigned)(t0 + 2) <= (unsigned)NW ? base + 4 : trash;
                     *reinterpret_cast<unsigned *>(smem + a0) = p01;
