@@ -546,6 +546,15 @@ def main():
         build_info["frac"] = round(bd_flops / (bd_avg * 1e-3) / 1e12 / F32_PEAK_TFS, 4) if args.precision == "fp32" \
             else round(bd_bytes / (bd_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
 
+    if rank == 0 and world == 1 and not shard_diag and roof.get("bound") == "hbm" and roof.get("unit") == "GB/s":
+        # context for the HBM fraction: the plain device copy rate of this box (read + write bytes), and the
+        # kernel's counter traffic per launch at its measured time, against it (traffic from the PMC file above)
+        cp = copy_rate(dev, stream)
+        roof["same_box_copy"] = cp
+        if roof.get("traffic"):
+            tr = roof["traffic"] / (roof["avg_launch_ms"] * 1e-3) / 1e9
+            roof["traffic_gbs"] = round(tr, 1)
+            roof["traffic_frac_of_copy"] = round(tr / cp["GB/s"], 3)
     tail = flow_tail(args, coords_slab, S, B, dev, stream, _lib, dvccorr)
     bwd = bwd_amp = None
     if world == 1 and not shard_diag and args.convc1 is None:
@@ -598,6 +607,27 @@ def main():
         print(json.dumps(line), flush=True)
     if dist:
         torch.distributed.destroy_process_group()
+
+
+def copy_rate(dev, stream, nbytes=1 << 30, reps=7):
+    """Device-to-device copy of 1 GiB (torch copy_, ROCm's own copy kernel): median read + write bytes per second.
+    The mixed read/write rate a streaming kernel gets on this box, next to the 8 TB/s spec the fraction uses."""
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device=dev).fill_(1.0)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        b.copy_(a)
+        e1.record(stream)
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    ts.sort()
+    med = ts[len(ts) // 2]
+    del a, b
+    return {"GB/s": round(2 * nbytes / (med * 1e-3) / 1e9, 1), "what": "torch copy_ of 1 GiB, read + write bytes, "
+            f"median of {reps}", "ms": round(med, 4)}
 
 
 def backward_timing(args, f1, f2, coords, dims, dev, stream, precision=None):

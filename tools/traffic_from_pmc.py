@@ -19,24 +19,24 @@ def pick(d, prefix):
 
 note = "HBM bytes per launch: 2 x FETCH_SIZE + WRITE_SIZE (KB x 1024), rocprofv3 --pmc, gfx950; source: {}"
 out = {}
-m6 = json.load(open(os.path.join(P, "r06", "r06_pmc_mat32_z.json")))
+m6 = json.load(open(os.path.join(P, "r06", "r06_pmc_mat32_y.json")))
 out["materialised_bf16_32_L4_r4_n1"] = {
     "build_hbm_bytes_per_launch": hbm(pick(m6, "k_build_bf16_2b")),
     "lookup_hbm_bytes_per_launch": hbm(pick(m6, "k_lookup_tile")),
-    "note": note.format("profiles/r06/r06_pmc_mat32_z.json (round-6 closing tree; DVC_BRICKED level 0)")}
+    "note": note.format("profiles/r06/r06_pmc_mat32_y.json (round-6 last tree; DVC_BRICKED level 0)")}
 mp = json.load(open(os.path.join(P, "r06", "r06_pmc_mat32_convc1.json")))
 out["materialised_bf16_32_L4_r4_n1_convc1_fused"] = {
     "lookup_hbm_bytes_per_launch": hbm(pick(mp, "k_lookup_tile")),
     "note": note.format("profiles/r06/r06_pmc_mat32_convc1.json (round 6, tree 6665544; k_lookup_tile<PROJ>, "
                         "DVC_BRICKED level 0)")}
-f = json.load(open(os.path.join(P, "r06", "r06_pmc_fused128.json")))
+f = json.load(open(os.path.join(P, "r06", "r06_pmc_fused128_y.json")))
 out["fused_bf16_128_L2_r4_n1"] = {
     "lookup_hbm_bytes_per_launch": hbm(pick(f, "k_fused_box<")),
-    "note": note.format("profiles/r06/r06_pmc_fused128.json (round 6, tree 6665544)")}
-f32 = json.load(open(os.path.join(P, "r06", "r06_pmc_fused128_fp32.json")))
+    "note": note.format("profiles/r06/r06_pmc_fused128_y.json (round-6 last tree: 8x4x1 box group, masked window writes)")}
+f32 = json.load(open(os.path.join(P, "r06", "r06_pmc_fused128_fp32_y.json")))
 out["fused_fp32_128_L2_r4_n1"] = {
     "lookup_hbm_bytes_per_launch": hbm(pick(f32, "k_fused_box_f32")),
-    "note": note.format("profiles/r06/r06_pmc_fused128_fp32.json (round 6, tree 6665544; k_fused_box_f32)")}
+    "note": note.format("profiles/r06/r06_pmc_fused128_fp32_y.json (round-6 last tree; k_fused_box_f32)")}
 fp = json.load(open(os.path.join(P, "r03", "r03_pmc_fused128_convc1.json")))
 out["fused_bf16_128_L2_r4_n1_convc1_fused"] = {
     "lookup_hbm_bytes_per_launch": sum(hbm(pick(fp, k)) for k in ("k_otf_keys", "k_fused_proj", "k_rows_to_channels")),
