@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include "common.h"
+#include "lookup_common.h"
 
 #include <type_traits>
 
@@ -35,6 +36,7 @@ template <typename T>
 __global__ void k_corr_pool(T *, long long, long long, long long, int, int, long long, int, int, int, int);
 template <typename T, int R, bool WINBUF, bool ALIGNED> __global__ void k_lookup_win(LookupArgs);
 template <typename T> __global__ void k_lookup_generic(LookupArgs);
+template <typename T, int R, int SE, bool WINBUF> __global__ void k_lookup_stretch(LookupArgs, StretchGeo);
 template <typename T, int R, bool NT, int ABL, int PROJ, int ACH, int NWV = 0, int SPOL = -1, bool XLP = false>
 __global__ void k_lookup_tile(LookupArgs);
 __global__ void k_proj_pack(const float *, bf16_t *, int, int, int, long long, int);
@@ -83,6 +85,7 @@ static Knob<int> g_trace_lo{0}, g_trace_hi{0};
 static Knob<int> g_lookup_nt{1};          // nontemporal output stores in the tile kernel
 static Knob<int> g_lookup_order{1};       // tile kernel level order (LookupArgs::order)
 static Knob<int> g_lookup_ldpol{0};       // tile kernel load cache policy (LookupArgs::ldpol; not the convc1 instances)
+static Knob<int> g_lookup_stretch{1};     // legacy W != D levels: 1 = k_lookup_stretch (LDS-staged), 0 = k_lookup_generic
 static Knob<int> g_build_ablate{0};       // diagnostics only: k_build_bf16 ablation instance
 // build output stores: 1 = nontemporal (default; round 2 A/B, bench n1 twice each: build 0.545 -> 0.506 ms,
 // step 2.20 -> 2.11 ms -- the 2.46 GB pyramid never fits the caches it would otherwise sweep), 0 = default policy
@@ -265,6 +268,48 @@ static void launch_tile_nt(const LookupArgs &A0, hipStream_t s) {
     launch_tile_r<T, NT, 0>(A, blocks, threads, s);
 }
 
+namespace dvc {
+int lookup_stretch_enabled() { return g_lookup_stretch; }
+// Legacy level (H, W, D) with W != D (LookupArgs::generic): k_lookup_stretch, one wave per (64 queries, output plane a,
+// chunk of kStretchSE W-axis samples).  A sample axis advances (W-1)/(D-1) (W axis) or (D-1)/(W-1) (D axis) per offset, so
+// the corners of k consecutive samples span at most ceil((k - 1) s) + 2 positions; +1 for float32 rounding of
+// norm/unnorm, clipped to the level.  false: the caller takes k_lookup_generic (tuning lookup_stretch 0, radius outside
+// 1..6, or a stretch too wide for 64 KB of LDS per wave).  The on-the-fly path (fused.hip) takes the same geometry
+// with esz = 4 (its window box of fp32 dots).
+bool stretch_geo(int H, int W, int D, int R, int esz, StretchGeo &g) {
+    if (W < 2 || D < 2 || H < 1) return false;
+    const double sw = (double)(W - 1) / (double)(D - 1);
+    g.WX = std::min((int)ceil((kStretchSE - 1) * sw - 1e-9) + 3, W);
+    g.DX = std::min((int)ceil(2.0 * R / sw - 1e-9) + 3, D);
+    g.RB = (int)round_up((long long)g.DX * esz, 16);
+    g.LS = 2 * g.WX * g.RB;
+    if ((g.LS / 16) % 2 == 0) g.LS += 16;   // an odd number of 16-byte units per lane: lanes start on spread banks
+    g.NYB = std::min(2 * R + 3, H);
+    g.WXF = std::min((int)ceil(2.0 * R * sw - 1e-9) + 3, W);
+    g.boxe = (long long)g.NYB * g.WXF * g.DX;
+    return 64 * (size_t)g.LS <= 64 * 1024;
+}
+}  // namespace dvc
+template <typename T>
+static bool launch_stretch(const LookupArgs &G, const dvc_layout &lay, int l, hipStream_t s) {
+    const int R = G.r;
+    if (!g_lookup_stretch || R < 1 || R > 6) return false;
+    StretchGeo g;
+    if (!stretch_geo(lay.H[l], lay.W[l], lay.D[l], R, (int)sizeof(T), g)) return false;
+    const int n = 2 * R + 1, ne = (n + kStretchSE - 1) / kStretchSE;
+    const unsigned blocks = (unsigned)((long long)G.B * G.nqb * n * ne);
+    const size_t lds = 64 * (size_t)g.LS;
+    switch (R) {
+    case 1: k_lookup_stretch<T, 1, kStretchSE, false><<<blocks, 64, lds, s>>>(G, g); break;
+    case 2: k_lookup_stretch<T, 2, kStretchSE, false><<<blocks, 64, lds, s>>>(G, g); break;
+    case 3: k_lookup_stretch<T, 3, kStretchSE, false><<<blocks, 64, lds, s>>>(G, g); break;
+    case 4: k_lookup_stretch<T, 4, kStretchSE, false><<<blocks, 64, lds, s>>>(G, g); break;
+    case 5: k_lookup_stretch<T, 5, kStretchSE, false><<<blocks, 64, lds, s>>>(G, g); break;
+    default: k_lookup_stretch<T, 6, kStretchSE, false><<<blocks, 64, lds, s>>>(G, g); break;
+    }
+    return true;
+}
+
 template <typename T, bool AL>
 static void launch_lookup_v(const LookupArgs &A, unsigned blocks, hipStream_t s) {
     switch (A.r) {
@@ -308,6 +353,11 @@ int dvc_set_tuning(const char *key, int value) {
     if (!strcmp(key, "lookup_variant")) {
         if (value < 0 || value > 2) return fail(DVC_ERR_INVALID, "set_tuning: lookup_variant %d", value);
         g_lookup_variant = value;
+        return DVC_OK;
+    }
+    if (!strcmp(key, "lookup_stretch")) {
+        if (value != 0 && value != 1) return fail(DVC_ERR_INVALID, "set_tuning: lookup_stretch %d (0 or 1)", value);
+        g_lookup_stretch = value;
         return DVC_OK;
     }
     if (!strcmp(key, "lookup_nt")) {
@@ -818,11 +868,19 @@ int dvc_corr_lookup(const void *corr, const float *coords, float *out, int B, in
     else if (store_dtype == DVC_F16) launch_lookup<f16_t>(A, blocks, s);
     else launch_lookup<float>(A, blocks, s);
     if ((rc = check_launch("corr_lookup"))) return rc;
-    if (radius >= 1 && radius <= 6) {   // legacy levels with W != D: per-output kernel, one launch per level
+    if (radius >= 1 && radius <= 6) {   // legacy levels with W != D: one launch per level
         for (int l = 0; l < lay.num_levels; ++l) {
             if (!A.generic[l] || A.zero[l]) continue;
             LookupArgs G = A;
             G.l0 = l; G.nl = 1;
+            bool staged = false;
+            if (store_dtype == DVC_BF16) staged = launch_stretch<bf16_t>(G, lay, l, s);
+            else if (store_dtype == DVC_F16) staged = launch_stretch<f16_t>(G, lay, l, s);
+            else staged = launch_stretch<float>(G, lay, l, s);
+            if (staged) {
+                if ((rc = check_launch("corr_lookup_stretch"))) return rc;
+                continue;
+            }
             const unsigned gb = (unsigned)ceil_div((long long)G.nach * B * G.nqb, 4);
             if (store_dtype == DVC_BF16) k_lookup_generic<bf16_t><<<gb, 256, 0, s>>>(G);
             else if (store_dtype == DVC_F16) k_lookup_generic<f16_t><<<gb, 256, 0, s>>>(G);

@@ -26,6 +26,9 @@
 namespace dvc {
 
 template <typename T, int R, bool WINBUF, bool ALIGNED> __global__ void k_lookup_win(LookupArgs);
+template <typename T, int R, int SE, bool WINBUF> __global__ void k_lookup_stretch(LookupArgs, StretchGeo);
+bool stretch_geo(int H, int W, int D, int R, int esz, StretchGeo &g);
+int lookup_stretch_enabled();
 
 constexpr long long kFusedChunk = 65536;   // queries per window-buffer chunk
 
@@ -110,6 +113,92 @@ __global__ __launch_bounds__(256) void k_fused_dots(const T *__restrict__ Q, con
         }
         wq[p] = acc;
     }
+}
+
+// Legacy levels with W != D on the fly (round 6).  The legacy sampler's samples are stretched along W and D (see
+// k_lookup_stretch, lookup.hip), so there is no (2r+2)^3 integer window; instead each query gets the box of integer
+// positions its samples' corners can touch -- NYB x WXF x DX (StretchGeo, clipped to the level; origin from the
+// first sample of each axis, the arithmetic k_lookup_stretch<.., WINBUF> repeats) -- and this kernel fills it with
+// scale * <Q[q], T_l[y][x][z]> (one wavefront per query, lanes over the box, k_fused_dots' dot and order), then
+// k_lookup_stretch interpolates from the box: bit-identical to k_fused_generic, which recomputed the 8 corner dots of
+// every output (5.8-6.7 ms per lookup at a 32^3-class non-cubic fmap, tools/bench_legacy.py).
+template <typename T>
+__global__ __launch_bounds__(256) void k_fused_dots_stretch(const T *__restrict__ Q, const T *__restrict__ Tt,
+                                                            LookupArgs A, StretchGeo G, float *__restrict__ ws,
+                                                            int Cp, long long t_rows, float scale) {
+    __shared__ u32x4 sq[4][64];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const long long item = (long long)blockIdx.x * 4 + w;
+    if (item >= (long long)A.B * A.nq) return;
+    const int b = (int)(item / A.nq);
+    const long long qi = item - (long long)b * A.nq;
+    const long long q = A.q0 + qi;
+    const int l = A.l0, R = A.r;
+    const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
+    const int nck = Cp / Dot<T>::kPerChunk;
+    const T *qrow = Q + ((long long)b * A.Nq + q) * Cp;
+    if (lane < nck) sq[w][lane] = *reinterpret_cast<const u32x4 *>(qrow + lane * Dot<T>::kPerChunk);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS writes landed
+    float cy, cx, cz;
+    load_coords(A.coords, b, A.Nq, q, cy, cx, cz);
+    const float sc = (float)(1 << l);
+    const float py = cy / sc, px = cx / sc, pz = cz / sc;
+    const float h1 = (float)(Hl - 1), w1 = (float)(Wl - 1), d1 = (float)(Dl - 1);
+    auto first = [](float i) {   // floor of an axis' first sample (0 when not finite), as k_lookup_stretch takes it
+        const bool ok = fabsf(i) < 1e7f;
+        return (int)(ok ? floorf(i) : 0.0f);
+    };
+    const int ysb = min(max(first(unnorm_coord(norm_coord(py + (float)(-R), h1), h1)), 0), Hl - G.NYB);
+    const int xsb = min(max(first(unnorm_coord(norm_coord(pz + (float)(-R), d1), w1)), 0), Wl - G.WXF);
+    const int zsb = min(max(first(unnorm_coord(norm_coord(px + (float)(-R), w1), d1)), 0), Dl - G.DX);
+    const T *Tb = Tt + ((long long)b * t_rows + A.off[l]) * Cp;
+    float *wq = ws + ((long long)b * A.nq + qi) * G.boxe;
+    for (long long p = lane; p < G.boxe; p += 64) {
+        const int zz = (int)(p % G.DX);
+        const long long t = p / G.DX;
+        const int xx = (int)(t % G.WXF), yy = (int)(t / G.WXF);
+        const T *trow = Tb + (((long long)(ysb + yy) * Wl + (xsb + xx)) * Dpl + (zsb + zz)) * Cp;
+        float acc = 0.0f;
+        for (int c = 0; c < nck; ++c)
+            acc = Dot<T>::chunk(*reinterpret_cast<const u32x4 *>(trow + c * Dot<T>::kPerChunk), sq[w][c], acc);
+        wq[p] = acc * scale;
+    }
+}
+
+template <typename T>
+static bool fused_level_stretch(const T *Q, const T *Tt, const LookupArgs &A0, float *ws, size_t ws_bytes, int Cp,
+                                long long t_rows, float scale, hipStream_t s) {
+    const int l = A0.l0, R = A0.r;
+    StretchGeo g;
+    if (!lookup_stretch_enabled() || R < 1 || R > 6 || !ws ||
+        !stretch_geo(A0.H[l], A0.W[l], A0.D[l], R, (int)sizeof(float), g))
+        return false;
+    // queries per pass: the boxes of B x nq queries in the workspace, 64 bytes left for the 16-byte row reads' overrun
+    long long per = ws_bytes > 64 ? (long long)((ws_bytes - 64) / sizeof(float)) / ((long long)A0.B * g.boxe) : 0;
+    per = per / 64 * 64;
+    if (per < 64) return false;
+    const int n = 2 * R + 1, ne = (n + kStretchSE - 1) / kStretchSE;
+    const size_t lds = 64 * (size_t)g.LS;
+    for (long long q0 = 0; q0 < A0.nq; q0 += per) {
+        LookupArgs A = A0;
+        A.q0 = A0.q0 + q0;
+        A.nq = std::min(per, A0.nq - q0);
+        A.nqb = (A.nq + 63) / 64;
+        const long long waves = (long long)A.B * A.nq;
+        k_fused_dots_stretch<T><<<(unsigned)((waves + 3) / 4), 256, 0, s>>>(Q, Tt, A, g, ws, Cp, t_rows, scale);
+        A.corr = ws;
+        const unsigned blocks = (unsigned)((long long)A.B * A.nqb * n * ne);
+        switch (R) {
+        case 1: k_lookup_stretch<float, 1, kStretchSE, true><<<blocks, 64, lds, s>>>(A, g); break;
+        case 2: k_lookup_stretch<float, 2, kStretchSE, true><<<blocks, 64, lds, s>>>(A, g); break;
+        case 3: k_lookup_stretch<float, 3, kStretchSE, true><<<blocks, 64, lds, s>>>(A, g); break;
+        case 4: k_lookup_stretch<float, 4, kStretchSE, true><<<blocks, 64, lds, s>>>(A, g); break;
+        case 5: k_lookup_stretch<float, 5, kStretchSE, true><<<blocks, 64, lds, s>>>(A, g); break;
+        default: k_lookup_stretch<float, 6, kStretchSE, true><<<blocks, 64, lds, s>>>(A, g); break;
+        }
+    }
+    return true;
 }
 
 // Per-output fallback: any radius, legacy levels with W != D.
@@ -352,7 +441,20 @@ int fused_lookup(const void *packed_q, const void *packed_t, const float *coords
             if (tile && !generic) continue;   // done by k_fused_tile
             if (generic) {
                 const long long total = (long long)B * A.nq * n3;
-                if (dtype == DVC_BF16)
+                const size_t wsb = win_ok && !A.zero[l] ? fused_workspace_bytes(B, Nq, 0, radius) : 0;
+                bool staged = false;
+                if (wsb && dtype == DVC_BF16)
+                    staged = fused_level_stretch<bf16_t>((const bf16_t *)packed_q, (const bf16_t *)packed_t, A,
+                                                         (float *)workspace, wsb, Cp, lay.row_stride, scale, s);
+                else if (wsb && dtype == DVC_F16)
+                    staged = fused_level_stretch<f16_t>((const f16_t *)packed_q, (const f16_t *)packed_t, A,
+                                                        (float *)workspace, wsb, Cp, lay.row_stride, scale, s);
+                else if (wsb)
+                    staged = fused_level_stretch<float>((const float *)packed_q, (const float *)packed_t, A,
+                                                        (float *)workspace, wsb, Cp, lay.row_stride, scale, s);
+                if (staged) {
+                    // (launch errors: checked below)
+                } else if (dtype == DVC_BF16)
                     k_fused_generic<bf16_t><<<(unsigned)((total + 255) / 256), 256, 0, s>>>(
                         (const bf16_t *)packed_q, (const bf16_t *)packed_t, A, Cp, lay.row_stride, scale);
                 else if (dtype == DVC_F16)

@@ -255,6 +255,136 @@ __global__ __launch_bounds__(256) void k_lookup_generic(LookupArgs A) {
                       outp, Nq);
 }
 
+// --- legacy levels with W != D: stretched boxes staged in LDS (round 6) --------------------
+// The legacy sampler (corr.py:49-50) reads the W axis at unnorm(norm(d + e - R, D - 1), W - 1) and the D axis at
+// unnorm(norm(w + bb - R, W - 1), D - 1): on a level with W != D an axis' 2r+1 samples are (W-1)/(D-1) (or its
+// inverse) apart, so there is no (2r+2)^3 integer window for the tile kernels.  k_lookup_generic gathers the 8 corners
+// of every output straight from HBM, one 2-byte load each -- 5832 scattered loads per query and level at r = 4, bound
+// by L2 requests: 16-23x the fixed convention's tile lookup on the same shape (tools/bench_legacy.py).
+// Here one wave = (64 queries, output plane a, a chunk of SE consecutive W-axis samples e): each lane (= query)
+// stages the two H planes its plane-a samples touch -- the WX x DX box (the host's bound on the chunk's stretched
+// extent, clipped to the level) around its chunk's corners -- into its own LDS region with 16-byte loads, then forms
+// its SE x (2r+1) outputs from 8 LDS corners each with tri_sample's arithmetic and term order: bit-identical to
+// k_lookup_generic.  (One wave per (query tile, a, chunk): 27 waves per tile at r = 4, small LDS regions, so
+// many waves per CU hide the LDS and load latencies a whole-window-per-lane version exposed at one wave per CU.)
+// LS: bytes of a lane's region (2 planes x WX rows x RB bytes, an odd number of 16-byte units: bank spread).
+template <typename T, int R, int SE, bool WINBUF>
+__global__ __launch_bounds__(64) void k_lookup_stretch(LookupArgs A, StretchGeo G) {
+    constexpr int n = 2 * R + 1, NE = (n + SE - 1) / SE;
+    const int WX = G.WX, DX = G.DX, RB = G.RB, LS = G.LS;
+    extern __shared__ __attribute__((aligned(16))) unsigned char st_smem[];
+    const int lane = threadIdx.x;
+    const int l = A.l0;
+    const long long nqb = A.nqb;
+    long long blk = blockIdx.x;
+    const int ec = (int)(blk % NE);
+    blk /= NE;
+    const int a = (int)(blk % n);
+    blk /= n;
+    const int b = (int)(blk / nqb);
+    if (b >= A.B) return;
+    const long long qi = (blk - (long long)b * nqb) * 64 + lane;
+    const bool active = qi < A.nq;
+    const long long Nq = A.Nq, q = A.q0 + (active ? qi : 0);
+    const long long n3 = (long long)n * n * n;
+    float *outp = A.out + ((long long)b * A.Ltot + l) * n3 * Nq + q;
+    const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l], Dpl = A.Dp[l];
+    float cy = 0.f, cx = 0.f, cz = 0.f;
+    if (active) load_coords(A.coords, b, Nq, q, cy, cx, cz);
+    const float sc = (float)(1 << l);
+    const float py = cy / sc, px = cx / sc, pz = cz / sc;
+    const float h1 = (float)(Hl - 1), w1 = (float)(Wl - 1), d1 = (float)(Dl - 1);
+    // one axis sample as tri_sample takes it: finite flag, floor, corner weights (w0 of k, w1 of k + 1)
+    auto sample = [](float i, int &k, float &w0, float &w1_, bool &ok) {
+#pragma clang fp contract(off)
+        ok = fabsf(i) < 1e7f;
+        const float f = ok ? floorf(i) : 0.0f;
+        k = (int)f;
+        w1_ = i - f;
+        w0 = (f + 1.0f) - i;
+    };
+    const int e0 = ec * SE;
+    int y0, x0[SE], z0[n];
+    float wy0, wy1, wx0[SE], wx1[SE], wz0[n], wz1[n];
+    bool oky, okx[SE], okz[n];
+    sample(unnorm_coord(norm_coord(py + (float)(a - R), h1), h1), y0, wy0, wy1, oky);
+#pragma unroll
+    for (int i = 0; i < SE; ++i)   // W axis <- d coordinate (legacy); samples past 2r+1 are never stored
+        sample(unnorm_coord(norm_coord(pz + (float)(e0 + i - R), d1), w1), x0[i], wx0[i], wx1[i], okx[i]);
+#pragma unroll
+    for (int bb = 0; bb < n; ++bb)   // D axis <- w coordinate
+        sample(unnorm_coord(norm_coord(px + (float)(bb - R), w1), d1), z0[bb], wz0[bb], wz1[bb], okz[bb]);
+    // staged box origin: the chunk's first corner, clipped so the box lies in the level (every in-range corner of
+    // this lane's chunk is inside [xs, xs + WX) x [zs, zs + DX); WX <= W and DX <= D on the host)
+    const int xs = min(max(x0[0], 0), Wl - WX), zs = min(max(z0[0], 0), Dl - DX);
+    unsigned char *reg = st_smem + lane * LS;
+    const T *lvl;
+    int ysb = 0, xsb = 0;   // WINBUF: the query's window box origin (k_fused_dots_stretch's, same arithmetic)
+    if constexpr (WINBUF) {
+        int k;
+        float u0, u1;
+        bool ok;
+        sample(unnorm_coord(norm_coord(py + (float)(-R), h1), h1), k, u0, u1, ok);
+        ysb = min(max(k, 0), Hl - G.NYB);
+        sample(unnorm_coord(norm_coord(pz + (float)(-R), d1), w1), k, u0, u1, ok);
+        xsb = min(max(k, 0), Wl - G.WXF);
+        lvl = reinterpret_cast<const T *>(A.corr) + ((long long)b * A.nq + (active ? qi : 0)) * G.boxe;
+    } else {
+        lvl = reinterpret_cast<const T *>(A.corr) + ((long long)b * Nq + q) * A.row_stride + A.off[l];
+    }
+    const int nch = RB / 16;
+    for (int dy = 0; dy < 2; ++dy) {   // planes y0, y0 + 1 (clamped rows: out-of-range corners are never read back)
+        const int yc = min(max(y0 + dy, 0), Hl - 1);
+        for (int xi = 0; xi < WX; ++xi) {
+            // (WINBUF: rows outside the query's box are clamped into it -- none of them holds an in-range corner)
+            const long long row = WINBUF ? (long long)min(max(yc - ysb, 0), G.NYB - 1) * G.WXF +
+                                               min(max(xs + xi - xsb, 0), G.WXF - 1)
+                                         : (long long)yc * Wl + (xs + xi);
+            const unsigned char *src =
+                reinterpret_cast<const unsigned char *>(lvl + row * (WINBUF ? DX : Dpl) + (WINBUF ? 0 : zs));
+            unsigned char *dst = reg + (dy * WX + xi) * RB;
+            for (int k = 0; k < nch; ++k) {
+                u32x4 v;
+                __builtin_memcpy(&v, src + 16 * k, 16);
+                *reinterpret_cast<u32x4 *>(dst + 16 * k) = v;
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < SE; ++i) {
+        const int e = e0 + i;
+        if (e >= n) break;   // (uniform: the last chunk may be short)
+        float pxy[2][2];     // (cx, cy) weight products, tri_sample's (wx * wy) first
+        {
+#pragma clang fp contract(off)
+            pxy[0][0] = wx0[i] * wy0;
+            pxy[0][1] = wx0[i] * wy1;
+            pxy[1][0] = wx1[i] * wy0;
+            pxy[1][1] = wx1[i] * wy1;
+        }
+#pragma unroll
+        for (int bb = 0; bb < n; ++bb) {
+#pragma clang fp contract(off)
+            float acc = 0.0f;
+#pragma unroll
+            for (int czz = 0; czz < 2; ++czz)
+#pragma unroll
+                for (int cyy = 0; cyy < 2; ++cyy)
+#pragma unroll
+                    for (int cxx = 0; cxx < 2; ++cxx) {
+                        const int x = x0[i] + cxx, y = y0 + cyy, z = z0[bb] + czz;
+                        const bool inb =
+                            (unsigned)x < (unsigned)Wl && (unsigned)y < (unsigned)Hl && (unsigned)z < (unsigned)Dl;
+                        const int off = inb ? (cyy * WX + (x - xs)) * RB + (z - zs) * (int)sizeof(T) : 0;
+                        const float v = StoreT<T>::load(reinterpret_cast<const T *>(reg + off));
+                        const float w = pxy[cxx][cyy] * (czz ? wz1[bb] : wz0[bb]);
+                        acc = inb ? acc + v * w : acc;
+                    }
+            if (active) outp[(long long)((a * n + bb) * n + e) * Nq] = okx[i] && oky && okz[bb] ? acc : 0.0f;
+        }
+    }
+}
+
 template <typename T, int R, bool WINBUF, bool ALIGNED>
 __global__ __launch_bounds__(256) void k_lookup_win(LookupArgs A) {
     constexpr int n = 2 * R + 1, NW = 2 * R + 2, NWP = (NW + 3) & ~3;
@@ -438,6 +568,15 @@ template __global__ void k_lookup_win<float, 6, true, false>(LookupArgs);
 template __global__ void k_lookup_generic<float>(LookupArgs);
 template __global__ void k_lookup_generic<bf16_t>(LookupArgs);
 template __global__ void k_lookup_generic<f16_t>(LookupArgs);
+#define DVC_STRETCH_INST(T, WB)                                                                     \
+    template __global__ void k_lookup_stretch<T, 1, 3, WB>(LookupArgs, StretchGeo);                \
+    template __global__ void k_lookup_stretch<T, 2, 3, WB>(LookupArgs, StretchGeo);                \
+    template __global__ void k_lookup_stretch<T, 3, 3, WB>(LookupArgs, StretchGeo);                \
+    template __global__ void k_lookup_stretch<T, 4, 3, WB>(LookupArgs, StretchGeo);                \
+    template __global__ void k_lookup_stretch<T, 5, 3, WB>(LookupArgs, StretchGeo);                \
+    template __global__ void k_lookup_stretch<T, 6, 3, WB>(LookupArgs, StretchGeo);
+DVC_STRETCH_INST(float, false) DVC_STRETCH_INST(bf16_t, false) DVC_STRETCH_INST(f16_t, false)
+DVC_STRETCH_INST(float, true)
 
 // --- bilinear_sampler_3d on a plain (B, C, Hv, Wv, Dv) float32 volume ---------------------
 __global__ __launch_bounds__(256) void k_sample3d(const float *__restrict__ vol, const float *__restrict__ pts,

@@ -74,4 +74,14 @@ __device__ __forceinline__ void axis_weights(float p, float kp, int d, float sn,
     w0 = (k + 1.0f) - x;
 }
 
+// Geometry of a legacy W != D level for k_lookup_stretch (lookup.hip), from the host: WX x DX the staged box of one
+// wave's chunk of W-axis samples (WX columns, DX values along D, RB bytes per staged row, LS bytes per lane's LDS
+// region); WINBUF (the on-the-fly path) reads a per-query window box of NYB x WXF x DX dots (boxe floats) instead of
+// the pyramid row.
+constexpr int kStretchSE = 3;   // W-axis samples per k_lookup_stretch wave
+struct StretchGeo {
+    int WX, DX, RB, LS, NYB, WXF;
+    long long boxe;
+};
+
 }  // namespace dvc

@@ -269,6 +269,20 @@ def test_brick_min_dp_knob():
     assert _lib.bricked_levels(lay) == 0b0001
 
 
+def test_lookup_stretch_knob():
+    """Tuning "lookup_stretch" (round 6): 1 (default) routes legacy W != D levels to k_lookup_stretch (and the on-the-fly
+    path to its window boxes), 0 to the per-output generic kernels; other values are refused.  (The GPU tests compare
+    the two bit for bit, tests/test_gpu_stretch.py.)"""
+    from dvccorr import _lib
+    try:
+        _lib.set_tuning("lookup_stretch", 0)
+        _lib.set_tuning("lookup_stretch", 1)
+        with pytest.raises(ValueError):   # (DVC_ERR_INVALID)
+            _lib.set_tuning("lookup_stretch", 2)
+    finally:
+        _lib.set_tuning("lookup_stretch", 1)
+
+
 def test_brick_flag_policy(monkeypatch):
     """The materialised block bricks its wide levels only for the tile kernel's cases."""
     from dvccorr import _lib
