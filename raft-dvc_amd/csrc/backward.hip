@@ -530,6 +530,104 @@ __global__ __launch_bounds__(256) void k_win_grad_generic(BwdArgs A) {
     }
 }
 
+// Round 6: the same box, one H plane at a time in LDS.  k_win_grad_generic's read-modify-writes go to global memory
+// (5832 dependent ones per query and level at r = 4: 3.3 ms of a 4.2 ms legacy backward at a 32 x 32 x 16 fmap,
+// tools/legacy_bwd_prof.py); here a 64-lane workgroup keeps each lane's plane j (nu x nv floats) in LDS, adds the
+// contributions of the outputs whose H corners land on it -- plane a's samples sit at box rows a - 1 .. a + 1, so the
+// outputs a in [j - 2, j + 1] -- in k_win_grad_generic's order (a, tu, tv, corner), and flushes the finished plane
+// (hi/lo pairs for the 16-bit formats).  Every box element sees the same sequence of fmas from the same zero:
+// bit-identical to k_win_grad_generic (tests/test_gpu_stretch.py).  PL: bytes of one lane's plane region.
+template <int R, int FMT>
+__global__ __launch_bounds__(64) void k_win_grad_stretch(BwdArgs A, int PL) {
+    constexpr int n = 2 * R + 1;
+    extern __shared__ __attribute__((aligned(16))) unsigned char wgs_smem[];
+    const int lane = threadIdx.x;
+    const long long nqb = (A.Nq + 63) / 64;
+    const long long item = blockIdx.x;
+    if (item >= (long long)A.B * A.L * nqb) return;
+    const int bl = (int)(item / nqb);
+    const int l = bl % A.L, b = bl / A.L;
+    if (!A.generic[l]) return;   // (uniform)
+    const long long q0 = (item - (long long)bl * nqb) * 64;
+    const long long q = q0 + lane;
+    const bool active = q < A.Nq;
+    const int nh = A.nwh[l], nu = A.nwu[l], nv = A.nwv[l];
+    const int npl = nu * nv;
+    const long long nw3 = bw_nw3(A, l);
+    float *gw = A.gwin + A.goff[l] + ((long long)b * A.Nq + (active ? q : q0)) * nw3;
+    float *pl = reinterpret_cast<float *>(wgs_smem + lane * PL);
+    const bool zero = A.zero[l];
+    const int Hl = A.H[l], Wl = A.W[l], Dl = A.D[l];
+    float cy = 0.f, cx = 0.f, cz = 0.f;
+    if (active) load_coords(A.coords, b, A.Nq, q, cy, cx, cz);
+    WinAxes ax;
+    bw_axes(A, l, cy, cx, cz, ax);
+    int oh, ou, ov;
+    bw_origin(A, l, R, ax, oh, ou, ov);
+    auto corner = [&](float p, int t, float sn, float su, int o, int S, int nw, int &j, float &w0, float &w1) {
+#pragma clang fp contract(off)
+        const float x = roundtrip(p + (float)(t - R), sn, su);
+        j = 0; w0 = 0.0f; w1 = 0.0f;
+        if (!(fabsf(x) < 1e7f)) return;
+        const float fx = floorf(x);
+        const int k = (int)fx;
+        if (k - o < 0 || k - o + 1 >= nw) return;
+        j = k - o;
+        w1 = (unsigned)(k + 1) < (unsigned)S ? x - fx : 0.0f;
+        w0 = (unsigned)k < (unsigned)S ? (fx + 1.0f) - x : 0.0f;
+    };
+    int ju[n], jv[n];
+    float wu0[n], wu1[n], wv0[n], wv1[n];
+#pragma unroll
+    for (int t = 0; t < n; ++t) {
+        corner(ax.pu, t, ax.un, ax.uu, ou, Wl, nu, ju[t], wu0[t], wu1[t]);
+        corner(ax.pv, t, ax.vn, ax.vu, ov, Dl, nv, jv[t], wv0[t], wv1[t]);
+    }
+    const long long chu = A.legacy ? 1 : n, chv = A.legacy ? n : 1;
+    const float *g = A.gout + (long long)bl * n * n * n * A.Nq + (active ? q : q0);
+    for (int j = 0; j < nh; ++j) {
+        for (int i = 0; i < PL / 16; ++i) reinterpret_cast<u32x4 *>(pl)[i] = u32x4{0u, 0u, 0u, 0u};
+        for (int a = max(j - 2, 0); a <= min(j + 1, n - 1) && !zero; ++a) {
+            int jh;
+            float wh0, wh1;
+            corner(ax.ph, a, ax.hs, ax.hs, oh, Hl, nh, jh, wh0, wh1);
+            // this lane's H corner of output plane a on box plane j: bit hb of k_win_grad_generic's corner index
+            const int hb = !active || (wh0 == 0.0f && wh1 == 0.0f) ? -1 : jh == j ? 0 : jh == j - 1 ? 1 : -1;
+            if (__builtin_amdgcn_ballot_w64(hb >= 0) == 0) continue;   // (uniform)
+            const float wh = hb == 1 ? wh1 : wh0;
+            const float *ga = g + (long long)a * n * n * A.Nq;
+#pragma unroll
+            for (int tu = 0; tu < n; ++tu) {
+                const bool uon = hb >= 0 && !(wu0[tu] == 0.0f && wu1[tu] == 0.0f);
+#pragma unroll
+                for (int tv = 0; tv < n; ++tv) {
+                    const float gv = uon ? ga[(tu * chu + tv * chv) * A.Nq] : 0.0f;
+#pragma unroll
+                    for (int c4 = 0; c4 < 4; ++c4) {   // corners (u bit, v bit) = (c4 & 1, c4 >> 1), in corner order
+                        const int ub = c4 & 1, vb = c4 >> 1;
+                        float w;
+                        {
+#pragma clang fp contract(off)
+                            w = ((ub ? wu1[tu] : wu0[tu]) * wh) * (vb ? wv1[tv] : wv0[tv]);
+                        }
+                        if (uon && w != 0.0f) {
+                            float *d = pl + (ju[tu] + ub) * nv + jv[tv] + vb;
+                            *d = __builtin_fmaf(w, gv, *d);
+                        }
+                    }
+                }
+            }
+        }
+        if (active) {   // plane j of the lane's box
+            float *dst = gw + (long long)j * npl;
+            for (int i = 0; i < npl; ++i) {
+                if constexpr (FMT != kGwF32) reinterpret_cast<unsigned *>(dst)[i] = gw_pair<FMT>(pl[i]);
+                else dst[i] = pl[i];
+            }
+        }
+    }
+}
+
 // Cross-wave sum of the four waves' 64 x (2 channels) partials: waves 2, 3 -> LDS ->
 // waves 0, 1; wave 1 -> LDS -> wave 0.  Fixed order (deterministic).  Every wave of the
 // block must call it.
@@ -2235,6 +2333,9 @@ static Knob<int> g_bwd_side{1};
 void set_backward_side(int v) { g_bwd_side = v; }
 static Knob<int> g_bwd_side_q{1};
 void set_backward_side_q(int v) { g_bwd_side_q = v; }
+// legacy W != D levels' window gradients: 1 = k_win_grad_stretch (LDS planes), 0 = k_win_grad_generic (global boxes)
+static Knob<int> g_bwd_stretch{1};
+void set_backward_stretch(int v) { g_bwd_stretch = v; }
 struct BwdSide {
     int dev = -1;
     hipStream_t st = nullptr;
@@ -2441,10 +2542,25 @@ static int backward_r(const TT *Q, const TT *Tt, BwdArgs &A, const dvc_layout &l
     }
     if (!launched("win_grad")) return DVC_ERR_LAUNCH;
     if (any_generic) {
-        switch (fmt) {
-        case kGwF16: k_win_grad_generic<R, kGwF16><<<wgrid, 256, 0, s>>>(A); break;
-        case kGwBf16: k_win_grad_generic<R, kGwBf16><<<wgrid, 256, 0, s>>>(A); break;
-        default: k_win_grad_generic<R, kGwF32><<<wgrid, 256, 0, s>>>(A); break;
+        // k_win_grad_stretch: one lane's box plane in LDS (the largest generic level's), 64 KB per workgroup at most
+        int pmax = 0;
+        for (int l = 0; l < A.L; ++l)
+            if (A.generic[l]) pmax = std::max(pmax, A.nwu[l] * A.nwv[l]);
+        int PL = (int)(((long long)pmax * 4 + 15) / 16 * 16);
+        if ((PL / 16) % 2 == 0) PL += 16;   // an odd number of 16-byte units per lane: lanes start on spread banks
+        const unsigned sgrid = (unsigned)((long long)A.B * A.L * ((A.Nq + 63) / 64));
+        if (g_bwd_stretch && 64LL * PL <= 64 * 1024) {
+            switch (fmt) {
+            case kGwF16: k_win_grad_stretch<R, kGwF16><<<sgrid, 64, 64 * PL, s>>>(A, PL); break;
+            case kGwBf16: k_win_grad_stretch<R, kGwBf16><<<sgrid, 64, 64 * PL, s>>>(A, PL); break;
+            default: k_win_grad_stretch<R, kGwF32><<<sgrid, 64, 64 * PL, s>>>(A, PL); break;
+            }
+        } else {
+            switch (fmt) {
+            case kGwF16: k_win_grad_generic<R, kGwF16><<<wgrid, 256, 0, s>>>(A); break;
+            case kGwBf16: k_win_grad_generic<R, kGwBf16><<<wgrid, 256, 0, s>>>(A); break;
+            default: k_win_grad_generic<R, kGwF32><<<wgrid, 256, 0, s>>>(A); break;
+            }
         }
         if (!launched("win_grad_generic")) return DVC_ERR_LAUNCH;
     }

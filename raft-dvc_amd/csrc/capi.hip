@@ -64,6 +64,7 @@ void set_backward_sort(int v);
 void set_backward_dense(int v);
 void set_backward_side(int v);
 void set_backward_side_q(int v);
+void set_backward_stretch(int v);
 void set_backward_gt_wg(int v);
 __global__ void k_coords_grid(float *, long long, int, int, int);
 template <bool DELTA, bool SUBGRID, int VEC, bool STAGED>
@@ -432,6 +433,11 @@ int dvc_set_tuning(const char *key, int value) {
     if (!strcmp(key, "bwd_gt_wg")) {   // target-gradient workgroups aimed at per level (splits), 64 .. 512
         if (value < 64 || value > 512) return fail(DVC_ERR_INVALID, "set_tuning: bwd_gt_wg %d", value);
         set_backward_gt_wg(value);
+        return DVC_OK;
+    }
+    if (!strcmp(key, "bwd_stretch")) {   // legacy W != D levels' window gradients: 1 = LDS planes, 0 = global boxes
+        if (value < 0 || value > 1) return fail(DVC_ERR_INVALID, "set_tuning: bwd_stretch %d", value);
+        set_backward_stretch(value);
         return DVC_OK;
     }
     if (!strcmp(key, "bwd_side_q")) {   // 1 = batch element 0's sorted dQ pass on the side stream too

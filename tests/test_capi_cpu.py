@@ -279,8 +279,12 @@ def test_lookup_stretch_knob():
         _lib.set_tuning("lookup_stretch", 1)
         with pytest.raises(ValueError):   # (DVC_ERR_INVALID)
             _lib.set_tuning("lookup_stretch", 2)
+        _lib.set_tuning("bwd_stretch", 0)
+        with pytest.raises(ValueError):
+            _lib.set_tuning("bwd_stretch", 3)
     finally:
         _lib.set_tuning("lookup_stretch", 1)
+        _lib.set_tuning("bwd_stretch", 1)
 
 
 def test_brick_flag_policy(monkeypatch):

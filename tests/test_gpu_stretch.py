@@ -116,3 +116,33 @@ def test_fused_stretch_against_materialised_fp32():
     b = _lookup(f1, f2, c, 2, 4, "fp32", 1)
     err = float((a - b).abs().max() / b.abs().max())
     assert err <= 1e-5, err
+
+
+def _backward(f1, f2, coords, L, r, precision, stretch):
+    from dvccorr import _lib, ops
+    B, C, H, W, D = f1.shape
+    dt = ops.dtype_code(precision)
+    q = ops.pack_queries(f1.reshape(B, C, -1), dt)
+    t = ops.pack_targets(f2, L, dt)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    gout = torch.randn(B, L * (2 * r + 1) ** 3, H * W * D, device=DEV, generator=g)
+    _lib.set_tuning("bwd_stretch", stretch)
+    try:
+        d1, d2 = ops.corr_backward(q, t, coords.reshape(B, 3, -1).contiguous(), gout, C, H, W, D, L, r, True, dt)
+        torch.cuda.synchronize()
+        return d1, d2
+    finally:
+        _lib.set_tuning("bwd_stretch", 1)
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp16", "fp32"])
+@pytest.mark.parametrize("shape,L", [((12, 16, 8), 3), ((9, 7, 20), 2), ((16, 8, 16), 4), ((8, 24, 6), 2)])
+def test_backward_stretch_matches_generic_bitwise(shape, L, precision):
+    """Legacy W != D window gradients: k_win_grad_stretch (LDS planes) against k_win_grad_generic (global boxes)."""
+    H, W, D = shape
+    for r in (1, 4) if precision == "bf16" else (4,):
+        f1, f2, c = _inputs(2, 32, H, W, D, 3.0, seed=H + W * 7 + D + r, specials=True)
+        a1, a2 = _backward(f1, f2, c, L, r, precision, 1)
+        b1, b2 = _backward(f1, f2, c, L, r, precision, 0)
+        assert torch.isfinite(a1).all() and torch.isfinite(a2).all()
+        assert torch.equal(a1, b1) and torch.equal(a2, b2), (shape, L, r, precision)

@@ -65,6 +65,14 @@ with torch.no_grad():
         r["lookup_convc1_ms"] = timed(lambda: blk.lookup_convc1(coords, wc, bc))
         fb = dvccorr.CorrBlockFused(f1, f2, L, R, legacy, precision=a.precision)
         r["fused_lookup_ms"] = timed(lambda: fb(coords))
+        # the training backward (dvc_corr_backward: d fmap1, d fmap2 of one lookup) on these inputs
+        from dvccorr import ops
+        dt = ops.dtype_code(a.precision)
+        q = ops.pack_queries(f1.reshape(1, C, -1), dt)
+        t = ops.pack_targets(f2, L, dt)
+        gout = torch.randn(1, L * (2 * R + 1) ** 3, H * W * D, device=dev)
+        cf = coords.reshape(1, 3, -1).contiguous()
+        r["backward_ms"] = timed(lambda: ops.corr_backward(q, t, cf, gout, C, H, W, D, L, R, legacy, dt))
         if legacy:   # same values through both impls (the generic kernels of each)
             d = (blk(coords) - fb(coords)).abs().max().item()
             r["materialised_vs_fused_maxdiff"] = d
