@@ -274,12 +274,18 @@ int dvc_flow_step(const float *coords1, const float *delta_flow, float *coords1_
                   int w, int d, int H, int W, int D, void *stream);
 
 /* Diagnostics hook for A/B timing.  The product kernel selection is a fixed table;
- * an override set here is THREAD-LOCAL (it changes only the calling host thread's
- * launches, on any stream), so the library holds no process-wide mutable state.
+ * an override set here is PROCESS-GLOBAL (round 6; it was thread-local, which a
+ * backward run on the autograd engine's worker thread never saw): it changes every
+ * later launch of every host thread, on any stream, until set back.
  *   "lookup_variant" 2 = LDS-staged tile kernel (default), 0 = walk with unaligned
  *                    16-byte run loads, 1 = walk with aligned chunks + v_perm shifter;
+ *   "lookup_stretch" 1 = legacy W != D levels on k_lookup_stretch (LDS-staged stretched
+ *                    boxes; the on-the-fly path on window-dot boxes), 0 = per-output
+ *                    generic kernels (bit-identical results either way);
+ *   "bwd_stretch"    1 = legacy W != D window gradients in LDS planes, 0 = global boxes
+ *                    (bit-identical);
  *   "upflow_staged"  1 = k_upflow through an LDS-staged low-res box (default), 0 = direct;
- *   "fused_variant", "build_variant", "upflow_rows", ... see capi.hip;
+ *   "fused_variant", "build_variant", "upflow_rows", "bwd_*", ... see capi.hip;
  *   "*_ablate"       diagnostics only, invalidates outputs. */
 int dvc_set_tuning(const char *key, int value);
 
