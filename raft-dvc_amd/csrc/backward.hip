@@ -537,6 +537,7 @@ __global__ __launch_bounds__(256) void k_win_grad_generic(BwdArgs A) {
 // outputs a in [j - 2, j + 1] -- in k_win_grad_generic's order (a, tu, tv, corner), and flushes the finished plane
 // (hi/lo pairs for the 16-bit formats).  Every box element sees the same sequence of fmas from the same zero:
 // bit-identical to k_win_grad_generic (tests/test_gpu_stretch.py).  PL: bytes of one lane's plane region.
+constexpr int kRunV = 8;   // k_win_grad_stretch: box rows of at most this many values take the register-run path
 template <int R, int FMT>
 __global__ __launch_bounds__(64) void k_win_grad_stretch(BwdArgs A, int PL) {
     constexpr int n = 2 * R + 1;
@@ -596,6 +597,43 @@ __global__ __launch_bounds__(64) void k_win_grad_stretch(BwdArgs A, int PL) {
             if (__builtin_amdgcn_ballot_w64(hb >= 0) == 0) continue;   // (uniform)
             const float wh = hb == 1 ? wh1 : wh0;
             const float *ga = g + (long long)a * n * n * A.Nq;
+            if constexpr (R <= 4) if (nv <= kRunV) {   // (r = 5, 6: the unrolled rows no longer fit the registers)
+                // short box rows (W > D: the D samples are compressed): per (tu, u corner) the row's nv values ride in
+                // registers while the (tv, v corner) contributions land by select -- each element still sees its fmas
+                // in (tu, tv, corner) order from the row's current value, so the sums are the same bits
+#pragma unroll
+                for (int tu = 0; tu < n; ++tu) {
+                    const bool uon = hb >= 0 && !(wu0[tu] == 0.0f && wu1[tu] == 0.0f);
+                    if (__builtin_amdgcn_ballot_w64(uon) == 0) continue;   // (uniform)
+                    float gt[n];
+#pragma unroll
+                    for (int tv = 0; tv < n; ++tv) gt[tv] = uon ? ga[(tu * chu + tv * chv) * A.Nq] : 0.0f;
+#pragma unroll
+                    for (int ub = 0; ub < 2; ++ub) {
+                        float *row = pl + (ju[tu] + ub) * nv;
+                        float run[kRunV];
+#pragma unroll
+                        for (int k = 0; k < kRunV; ++k) run[k] = k < nv ? row[k] : 0.0f;
+#pragma unroll
+                        for (int tv = 0; tv < n; ++tv)
+#pragma unroll
+                            for (int vb = 0; vb < 2; ++vb) {
+                                float w;
+                                {
+#pragma clang fp contract(off)
+                                    w = ((ub ? wu1[tu] : wu0[tu]) * wh) * (vb ? wv1[tv] : wv0[tv]);
+                                }
+                                const int pv = uon && w != 0.0f ? jv[tv] + vb : -1;
+#pragma unroll
+                                for (int k = 0; k < kRunV; ++k) run[k] = k == pv ? __builtin_fmaf(w, gt[tv], run[k]) : run[k];
+                            }
+#pragma unroll
+                        for (int k = 0; k < kRunV; ++k)
+                            if (k < nv) row[k] = run[k];
+                    }
+                }
+                continue;
+            }
 #pragma unroll
             for (int tu = 0; tu < n; ++tu) {
                 const bool uon = hb >= 0 && !(wu0[tu] == 0.0f && wu1[tu] == 0.0f);
