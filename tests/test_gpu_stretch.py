@@ -146,3 +146,18 @@ def test_backward_stretch_matches_generic_bitwise(shape, L, precision):
         b1, b2 = _backward(f1, f2, c, L, r, precision, 0)
         assert torch.isfinite(a1).all() and torch.isfinite(a2).all()
         assert torch.equal(a1, b1) and torch.equal(a2, b2), (shape, L, r, precision)
+
+
+def test_stretch_too_wide_falls_back():
+    """A stretch whose staged boxes would need more than 64 KB of LDS per wave (W-1 = 21 (D-1) here) keeps the
+    generic kernels; the result is the same either way."""
+    f1, f2, c = _inputs(1, 32, 6, 64, 4, 2.0, seed=9)
+    a = _lookup(f1, f2, c, 1, 4, "bf16", 1)
+    b = _lookup(f1, f2, c, 1, 4, "bf16", 0)
+    assert torch.equal(a, b)
+    fa = _lookup_fused(f1, f2, c, 1, 4, "bf16", 1)
+    fb = _lookup_fused(f1, f2, c, 1, 4, "bf16", 0)
+    assert torch.equal(fa, fb)
+    ga = _backward(f1, f2, c, 1, 4, "bf16", 1)
+    gb = _backward(f1, f2, c, 1, 4, "bf16", 0)
+    assert torch.equal(ga[0], gb[0]) and torch.equal(ga[1], gb[1])
