@@ -453,6 +453,21 @@ __global__ __launch_bounds__(512, 1) void k_fused_proj(const bf16_t *__restrict_
     if ((ABL & 8) && sink == 0x9e3779b9u) rows_out[0] = (float)sink;   // keeps the diagnostics' dots live
 }
 
+// r = 1 instances live in fused_proj_r1.hip, compiled without SLP vectorisation: with it, their one SLP-formed
+// packed-FP32 add reads the high half of a pair for the low lane (the hazard tools/isa_check.py guards, see splat2 in
+// common.h); every other radius compiles clean with SLP, 2.5 % faster at config #5 (round 6, gpurun_out/r6slp:
+// 8.70 -> 8.49 ms per convc1-fused lookup).
+#define DVC_FPROJ_R1(KS, E)                                                                                      \
+    extern template __global__ void k_fused_proj<1, KS, 0, E>(const bf16_t *, const bf16_t *, LookupArgs,         \
+                                                             const unsigned long long *, int, int, long long, float, \
+                                                             float *);
+#ifndef DVC_FPROJ_R1_TU
+DVC_FPROJ_R1(1, bf16_t) DVC_FPROJ_R1(2, bf16_t) DVC_FPROJ_R1(4, bf16_t)
+DVC_FPROJ_R1(1, f16_t) DVC_FPROJ_R1(2, f16_t) DVC_FPROJ_R1(4, f16_t)
+#endif
+#undef DVC_FPROJ_R1
+
+#ifndef DVC_FPROJ_R1_TU
 // [B][Nq][96] -> (B, 96, Nq): 64 queries x 96 channels per block through LDS
 __global__ __launch_bounds__(256) void k_rows_to_channels(const float *__restrict__ rows, float *__restrict__ out,
                                                           long long Nq) {
@@ -621,5 +636,7 @@ int fused_lookup_proj(const void *packed_q, const void *packed_t, const float *c
     if (!launched("rows_to_channels")) return DVC_ERR_LAUNCH;
     return DVC_OK;
 }
+
+#endif  // DVC_FPROJ_R1_TU
 
 }  // namespace dvc

@@ -12,12 +12,20 @@ one() {  # name lib args...
   DVCCORR_LIB=$PWD/$L/$lib timeout -k 10 300 python -u bench.py --no-cpu-baseline --impl fused --size 128 --encoder 2 --levels 2 "$@" > $OUT/$name.json 2> $OUT/$name.err || { tail -5 $OUT/$name.err; exit 3; }
   python3 -c "import json;d=json.loads(open('$OUT/$name.json').read().strip().splitlines()[-1]);print('$name', round(d['ms_per_step'],4), d['lookup_avg_ms'], d['roofline']['frac'])"
 }
-for i in 1 2; do
+for i in $([ -n "${CONVC1_ONLY:-}" ] || echo 1 2); do
   one b_base_$i libdvccorr.so --steps 3 --warmup 1
   for v in "$@"; do
     one b_${v#libdvccorr_}_$i $v --steps 3 --warmup 1
   done
 done
+if [ -n "${CONVC1_ONLY:-}" ]; then   # the convc1 on-the-fly path only
+  for i in 1 2 3; do
+    for v in libdvccorr.so "$@"; do
+      one c_${v#libdvccorr_}_$i $v --convc1 --steps 3 --warmup 1
+    done
+  done
+  exit 0
+fi
 if [ -n "${MODES:-}" ]; then   # convc1 / fp32 instances too
   for i in 1 2; do
     for v in libdvccorr.so "$@"; do
