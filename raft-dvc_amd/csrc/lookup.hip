@@ -350,6 +350,19 @@ __global__ __launch_bounds__(64) void k_lookup_stretch(LookupArgs A, StretchGeo 
             }
         }
     }
+    // per-axis corner offsets into the lane's staged box and in-level flags, hoisted out of the output loop (the
+    // corner sums below keep tri_sample's order and products: the same bits)
+    int zo[n][2];
+    bool zin[n][2];
+#pragma unroll
+    for (int bb = 0; bb < n; ++bb)
+#pragma unroll
+        for (int czz = 0; czz < 2; ++czz) {
+            const int z = z0[bb] + czz;
+            zin[bb][czz] = (unsigned)z < (unsigned)Dl;
+            zo[bb][czz] = zin[bb][czz] ? (z - zs) * (int)sizeof(T) : 0;
+        }
+    const bool yin0 = (unsigned)y0 < (unsigned)Hl, yin1 = (unsigned)(y0 + 1) < (unsigned)Hl;
 #pragma unroll
     for (int i = 0; i < SE; ++i) {
         const int e = e0 + i;
@@ -362,6 +375,18 @@ __global__ __launch_bounds__(64) void k_lookup_stretch(LookupArgs A, StretchGeo 
             pxy[1][0] = wx1[i] * wy0;
             pxy[1][1] = wx1[i] * wy1;
         }
+        int xyo[2][2];   // (cx, cy): row offset of the corner column in the staged box
+        bool xyin[2][2];
+#pragma unroll
+        for (int cxx = 0; cxx < 2; ++cxx) {
+            const int x = x0[i] + cxx;
+            const bool xin = (unsigned)x < (unsigned)Wl;
+#pragma unroll
+            for (int cyy = 0; cyy < 2; ++cyy) {
+                xyin[cxx][cyy] = xin && (cyy ? yin1 : yin0);
+                xyo[cxx][cyy] = xyin[cxx][cyy] ? (cyy * WX + (x - xs)) * RB : 0;
+            }
+        }
 #pragma unroll
         for (int bb = 0; bb < n; ++bb) {
 #pragma clang fp contract(off)
@@ -372,10 +397,8 @@ __global__ __launch_bounds__(64) void k_lookup_stretch(LookupArgs A, StretchGeo 
                 for (int cyy = 0; cyy < 2; ++cyy)
 #pragma unroll
                     for (int cxx = 0; cxx < 2; ++cxx) {
-                        const int x = x0[i] + cxx, y = y0 + cyy, z = z0[bb] + czz;
-                        const bool inb =
-                            (unsigned)x < (unsigned)Wl && (unsigned)y < (unsigned)Hl && (unsigned)z < (unsigned)Dl;
-                        const int off = inb ? (cyy * WX + (x - xs)) * RB + (z - zs) * (int)sizeof(T) : 0;
+                        const bool inb = xyin[cxx][cyy] && zin[bb][czz];
+                        const int off = inb ? xyo[cxx][cyy] + zo[bb][czz] : 0;
                         const float v = StoreT<T>::load(reinterpret_cast<const T *>(reg + off));
                         const float w = pxy[cxx][cyy] * (czz ? wz1[bb] : wz0[bb]);
                         acc = inb ? acc + v * w : acc;
