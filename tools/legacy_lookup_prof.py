@@ -13,6 +13,7 @@ import dvccorr  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--shape", default="32,32,16")
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--fused", action="store_true", help="the on-the-fly block instead of the materialised one")
 a = ap.parse_args()
 H, W, D = (int(x) for x in a.shape.split(","))
 dev = torch.device("cuda:0")
@@ -21,7 +22,8 @@ f1 = torch.randn(1, 128, H, W, D, generator=g).to(dev)
 f2 = torch.randn(1, 128, H, W, D, generator=g).to(dev)
 c = (dvccorr.coords_grid_3d(1, H, W, D, torch.device("cpu")) + (torch.rand(1, 3, H, W, D, generator=g) * 4 - 2)).to(dev)
 with torch.no_grad():
-    blk = dvccorr.CorrBlock(f1, f2, 4, 4, True, precision="bf16")
+    cls = dvccorr.CorrBlockFused if a.fused else dvccorr.CorrBlock
+    blk = cls(f1, f2, 4, 4, True, precision="bf16")
     for _ in range(a.reps):
         out = blk(c)
 torch.cuda.synchronize()
